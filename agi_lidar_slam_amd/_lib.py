@@ -1,0 +1,162 @@
+"""ctypes binding of ``include/slio.h`` (the C-ABI of libslio.so).
+
+There is no CPU fallback: if the HIP library cannot be loaded the import of
+the device API raises, so a silent non-native path cannot exist.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libslio.so")
+
+SLIO_NUM_MATCH = 5
+SLIO_NPROD = 91
+SLIO_NHTH = 78
+SLIO_NSUPER = 8
+SLIO_CHUNK = 128
+SLIO_MODE_REFERENCE = 0
+SLIO_MODE_FIXED = 1
+SLIO_KERNEL_SEARCH = 0
+SLIO_KERNEL_REUSE = 1
+SLIO_KERNEL_SUPER = 2
+
+ERRORS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ECAPACITY", -5: "ESTATE"}
+
+
+class SlioParams(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("max_points", C.c_int32),
+        ("rank", C.c_int32),
+        ("nranks", C.c_int32),
+        ("grid_cell", C.c_float),
+        ("plane_threshold", C.c_float),
+        ("max_match_sqd", C.c_float),
+        ("reserved", C.c_int32),
+        ("max_grid_cells", C.c_int64),
+    ]
+
+
+class SlioPose(C.Structure):
+    _fields_ = [
+        ("rot", C.c_double * 4),
+        ("pos", C.c_double * 3),
+        ("rli", C.c_double * 4),
+        ("tli", C.c_double * 3),
+    ]
+
+
+class SlioState(C.Structure):
+    _fields_ = [
+        ("pos", C.c_double * 3),
+        ("rot", C.c_double * 4),
+        ("rli", C.c_double * 4),
+        ("tli", C.c_double * 3),
+        ("vel", C.c_double * 3),
+        ("bg", C.c_double * 3),
+        ("ba", C.c_double * 3),
+        ("grav", C.c_double * 3),
+    ]
+
+
+class SlioIkfStats(C.Structure):
+    _fields_ = [
+        ("passes", C.c_int32),
+        ("searches", C.c_int32),
+        ("valid_passes", C.c_int32),
+        ("converged", C.c_int32),
+        ("last_m", C.c_int64),
+        ("device_ms", C.c_double),
+    ]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
+
+_P = C.c_void_p
+_FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int32)
+_I64P = C.POINTER(C.c_int64)
+_U8P = C.POINTER(C.c_uint8)
+
+# name -> (restype, argtypes); every symbol include/slio.h declares
+SIGNATURES = {
+    "slio_params_default": (C.c_int, [C.POINTER(SlioParams)]),
+    "slio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioParams)]),
+    "slio_destroy": (C.c_int, [_P]),
+    "slio_set_stream": (C.c_int, [_P, _P]),
+    "slio_last_error": (C.c_char_p, []),
+    "slio_map_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
+    "slio_map_share": (C.c_int, [_P, _P]),
+    "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),
+    "slio_scan_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
+    "slio_shard_range": (C.c_int, [_P, _I64P, _I64P]),
+    "slio_iterate_async": (C.c_int, [_P, C.POINTER(SlioPose), C.c_int, C.c_int, C.POINTER(_DP)]),
+    "slio_set_super_buffer": (C.c_int, [_P, _P]),
+    "slio_super_download": (C.c_int, [_P, _DP]),
+    "slio_reduce_super": (C.c_int, [_DP, _DP, _DP, _I64P]),
+    "slio_iterate": (C.c_int, [_P, C.POINTER(SlioPose), C.c_int, C.c_int, _DP, _DP, _I64P]),
+    "slio_get_neighbors": (C.c_int, [_P, _IP, _FP, _U8P]),
+    "slio_get_planes": (C.c_int, [_P, _FP]),
+    "slio_get_residuals": (C.c_int, [_P, _FP]),
+    "slio_profile": (C.c_int, [_P, C.c_int]),
+    "slio_profile_read": (C.c_int, [_P, C.c_int, _DP, _I64P]),
+    "slio_ikf_update": (
+        C.c_int,
+        [_P, C.POINTER(SlioState), _DP, C.c_double, C.c_int, C.c_int, C.c_int, ALLREDUCE_FN, _P,
+         C.POINTER(SlioIkfStats)],
+    ),
+    "slio_state_boxplus": (C.c_int, [C.POINTER(SlioState), _DP, C.POINTER(SlioState)]),
+    "slio_state_boxminus": (C.c_int, [C.POINTER(SlioState), C.POINTER(SlioState), _DP]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libslio.so once and bind every declared signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: build it with `python -m agi_lidar_slam_amd.build` "
+            "(there is no CPU fallback for the device path)")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the library lacks a declared symbol
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class SlioError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = load().slio_last_error()
+        msg = msg.decode() if msg else ""
+        raise SlioError(f"{what}: {ERRORS.get(rc, rc)}: {msg}")
+
+
+def fptr(a: np.ndarray):
+    return a.ctypes.data_as(_FP)
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_DP)
+
+
+def iptr(a: np.ndarray):
+    return a.ctypes.data_as(_IP)
+
+
+def u8ptr(a: np.ndarray):
+    return a.ctypes.data_as(_U8P)

@@ -1,0 +1,60 @@
+// slio_common.hpp — internal declarations shared by the device runtime
+// (slio_device.hip) and the host IKF driver (slio_ikf.cpp).
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/slio.h"
+
+#if defined(__HIPCC__)
+#define SLIO_HD __host__ __device__
+#else
+#define SLIO_HD
+#endif
+
+namespace slio {
+
+// thread-local last-error message behind slio_last_error()
+void set_error(const std::string& msg);
+
+// Reduction product table: product k accumulates row[pa[k]] * row[pb[k]]
+// over the selected points of a pass, where the per-point row is
+//   row[0..11] = h_x (esekfom.hpp:217-221), row[12] = h = -pd2 (esekfom.hpp:225),
+//   row[13]    = 1 for an effective point (so the product counts m).
+// k in [0, 78)  : H^T H upper triangle, row-major (i <= j)
+// k in [78, 90) : H^T h
+// k == 90       : m
+constexpr int kRow = 14;
+inline void product_table(uint8_t pa[SLIO_NPROD], uint8_t pb[SLIO_NPROD]) {
+  int k = 0;
+  for (int i = 0; i < 12; ++i)
+    for (int j = i; j < 12; ++j) {
+      pa[k] = (uint8_t)i;
+      pb[k] = (uint8_t)j;
+      ++k;
+    }
+  for (int i = 0; i < 12; ++i) {
+    pa[k] = (uint8_t)i;
+    pb[k] = 12;
+    ++k;
+  }
+  pa[k] = 13;
+  pb[k] = 13;
+}
+
+// Chunk / super-chunk geometry of the fixed summation tree.  The scan of n
+// points is cut into C = ceil(n / SLIO_CHUNK) chunks; super-chunk s covers
+// chunks [s*C/8, (s+1)*C/8); rank r of N owns super-chunks [r*8/N, (r+1)*8/N).
+// The tree (chunk -> super -> total) does not depend on N, so 1/2/4/8 ranks
+// produce bitwise-identical sums.
+SLIO_HD inline int64_t num_chunks(int64_t n) { return (n + SLIO_CHUNK - 1) / SLIO_CHUNK; }
+SLIO_HD inline int64_t super_lo(int64_t C, int s) { return (C * s) / SLIO_NSUPER; }
+inline void rank_chunks(int64_t n, int rank, int nranks, int64_t* c0, int64_t* c1) {
+  int64_t C = num_chunks(n);
+  int per = SLIO_NSUPER / nranks;
+  *c0 = super_lo(C, rank * per);
+  *c1 = super_lo(C, (rank + 1) * per);
+}
+
+}  // namespace slio

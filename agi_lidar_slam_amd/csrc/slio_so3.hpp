@@ -1,0 +1,165 @@
+// slio_so3.hpp — host-side restatement of the state algebra the IKF needs.
+//
+// The reference uses Sophus::SO3 from strasdat/Sophus @ a621ff (non-templated,
+// README.md:41) on top of Eigen 3.3 quaternions; neither is in the image, so
+// their published algorithms are restated here:
+//   SO3::exp      = expAndTheta (unit quaternion from axis-angle, SMALL_EPS 1e-10)
+//   SO3::log      = logAndTheta (atan-based, Hertzberg et al.)
+//   SO3(Matrix3d) = Eigen Quaternion-from-rotation-matrix (trace branch)
+//   SO3 * SO3     = Eigen quaternion product, then normalize()
+//   SO3::matrix() = Eigen QuaternionBase::toRotationMatrix
+//   SO3 * vector  = Eigen QuaternionBase::_transformVector
+// Quaternions are stored (w, x, y, z) in this build.
+#pragma once
+
+#include <cmath>
+
+namespace slio {
+
+struct Quat {
+  double w = 1.0, x = 0.0, y = 0.0, z = 0.0;
+};
+
+inline Quat qmul(const Quat& a, const Quat& b) {
+  Quat r;
+  r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+  r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+  r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+  r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+  return r;
+}
+
+inline Quat qnormalized(const Quat& q) {
+  const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  return Quat{q.w / n, q.x / n, q.y / n, q.z / n};
+}
+
+// row-major 3x3
+inline void qmatrix(const Quat& q, double R[9]) {
+  const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
+  const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+  const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+  const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+  R[0] = 1.0 - (tyy + tzz);
+  R[1] = txy - twz;
+  R[2] = txz + twy;
+  R[3] = txy + twz;
+  R[4] = 1.0 - (txx + tzz);
+  R[5] = tyz - twx;
+  R[6] = txz - twy;
+  R[7] = tyz + twx;
+  R[8] = 1.0 - (txx + tyy);
+}
+
+inline Quat qfrom_matrix(const double m[9]) {
+  auto M = [&](int r, int c) { return m[r * 3 + c]; };
+  Quat q;
+  double t = M(0, 0) + M(1, 1) + M(2, 2);
+  if (t > 0.0) {
+    t = std::sqrt(t + 1.0);
+    q.w = 0.5 * t;
+    t = 0.5 / t;
+    q.x = (M(2, 1) - M(1, 2)) * t;
+    q.y = (M(0, 2) - M(2, 0)) * t;
+    q.z = (M(1, 0) - M(0, 1)) * t;
+  } else {
+    int i = 0;
+    if (M(1, 1) > M(0, 0)) i = 1;
+    if (M(2, 2) > M(i, i)) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+    double v[3];
+    v[i] = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (M(k, j) - M(j, k)) * t;
+    v[j] = (M(j, i) + M(i, j)) * t;
+    v[k] = (M(k, i) + M(i, k)) * t;
+    q.x = v[0];
+    q.y = v[1];
+    q.z = v[2];
+  }
+  return q;
+}
+
+constexpr double kSmallEps = 1e-10;
+
+inline Quat so3_exp(const double om[3]) {
+  const double theta = std::sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+  const double half = 0.5 * theta;
+  double imag;
+  const double real = std::cos(half);
+  if (theta < kSmallEps) {
+    const double t2 = theta * theta;
+    const double t4 = t2 * t2;
+    imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;
+  } else {
+    imag = std::sin(half) / theta;
+  }
+  return qnormalized(Quat{real, imag * om[0], imag * om[1], imag * om[2]});
+}
+
+inline void so3_log(const Quat& q, double out[3]) {
+  const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z);
+  const double w = q.w;
+  double f;
+  if (n < kSmallEps) {
+    f = 2.0 / w - 2.0 * (n * n) / (w * (w * w));
+  } else if (std::fabs(w) < kSmallEps) {
+    f = (w > 0 ? M_PI : -M_PI) / n;
+  } else {
+    f = 2.0 * std::atan(n / w) / n;
+  }
+  out[0] = f * q.x;
+  out[1] = f * q.y;
+  out[2] = f * q.z;
+}
+
+// SO3(a.matrix()^T * b.matrix()).log()  (esekfom.hpp:242-246)
+inline void so3_boxminus(const Quat& b, const Quat& a, double out[3]) {
+  double Ra[9], Rb[9], M[9];
+  qmatrix(a, Ra);
+  qmatrix(b, Rb);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      M[i * 3 + j] = Ra[0 * 3 + i] * Rb[0 * 3 + j] + Ra[1 * 3 + i] * Rb[1 * 3 + j] +
+                     Ra[2 * 3 + i] * Rb[2 * 3 + j];
+  so3_log(qfrom_matrix(M), out);
+}
+
+// In-place Gauss-Jordan inverse with partial pivoting of an n x n row-major
+// matrix (stands in for Eigen's PartialPivLU-based inverse()). Returns false
+// on an exactly singular pivot.
+template <int N>
+inline bool invert(const double* A, double* out) {
+  double a[N][2 * N];
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      a[i][j] = A[i * N + j];
+      a[i][N + j] = (i == j) ? 1.0 : 0.0;
+    }
+  for (int c = 0; c < N; ++c) {
+    int p = c;
+    double best = std::fabs(a[c][c]);
+    for (int r = c + 1; r < N; ++r)
+      if (std::fabs(a[r][c]) > best) {
+        best = std::fabs(a[r][c]);
+        p = r;
+      }
+    if (best == 0.0) return false;
+    if (p != c)
+      for (int j = 0; j < 2 * N; ++j) std::swap(a[c][j], a[p][j]);
+    const double inv = 1.0 / a[c][c];
+    for (int j = 0; j < 2 * N; ++j) a[c][j] *= inv;
+    for (int r = 0; r < N; ++r) {
+      if (r == c) continue;
+      const double f = a[r][c];
+      if (f == 0.0) continue;
+      for (int j = 0; j < 2 * N; ++j) a[r][j] -= f * a[c][j];
+    }
+  }
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) out[i * N + j] = a[i][N + j];
+  return true;
+}
+
+}  // namespace slio

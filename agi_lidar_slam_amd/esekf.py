@@ -1,0 +1,243 @@
+"""Python mirror of the reference's filter interface on the MI355X path.
+
+Names, argument meaning and error behaviour follow
+``esekfom::esekf`` (src/S-FAST_LIO/include/esekfom.hpp:42-351),
+``state_ikfom`` (use-ikfom.hpp:18-27) and the parts of ``KD_TREE`` the IKF
+uses (Build, size; ikd_Tree.h:45-299).  Every numeric pass runs on the GPU
+through libslio.so (include/slio.h); this module only marshals arguments.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+G_M_S2 = 9.81          # common_lib.h:21
+LASER_POINT_COV = 0.001  # laserMapping.cpp:29
+NUM_MATCH_POINTS = 5   # common_lib.h:22
+
+
+@dataclass
+class StateIkfom:
+    """state_ikfom (use-ikfom.hpp:18-27); rotations as unit quaternions (w, x, y, z)."""
+    pos: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    rot: np.ndarray = field(default_factory=lambda: np.array([1.0, 0, 0, 0]))
+    offset_R_L_I: np.ndarray = field(default_factory=lambda: np.array([1.0, 0, 0, 0]))
+    offset_T_L_I: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    vel: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    bg: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    ba: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    grav: np.ndarray = field(default_factory=lambda: np.array([0.0, 0.0, -G_M_S2]))
+
+    def to_c(self) -> L.SlioState:
+        s = L.SlioState()
+        for name, arr in (("pos", self.pos), ("rot", self.rot), ("rli", self.offset_R_L_I),
+                          ("tli", self.offset_T_L_I), ("vel", self.vel), ("bg", self.bg),
+                          ("ba", self.ba), ("grav", self.grav)):
+            getattr(s, name)[:] = [float(v) for v in arr]
+        return s
+
+    @staticmethod
+    def from_c(s: L.SlioState) -> "StateIkfom":
+        return StateIkfom(pos=np.array(s.pos[:]), rot=np.array(s.rot[:]),
+                          offset_R_L_I=np.array(s.rli[:]), offset_T_L_I=np.array(s.tli[:]),
+                          vel=np.array(s.vel[:]), bg=np.array(s.bg[:]), ba=np.array(s.ba[:]),
+                          grav=np.array(s.grav[:]))
+
+    def to_array(self) -> np.ndarray:
+        """The 26 doubles of slio_state, in memory order."""
+        return np.concatenate([self.pos, self.rot, self.offset_R_L_I, self.offset_T_L_I,
+                               self.vel, self.bg, self.ba, self.grav]).astype(np.float64)
+
+    @staticmethod
+    def from_array(a: np.ndarray) -> "StateIkfom":
+        a = np.asarray(a, dtype=np.float64)
+        return StateIkfom(pos=a[0:3].copy(), rot=a[3:7].copy(), offset_R_L_I=a[7:11].copy(),
+                          offset_T_L_I=a[11:14].copy(), vel=a[14:17].copy(), bg=a[17:20].copy(),
+                          ba=a[20:23].copy(), grav=a[23:26].copy())
+
+
+def _params(device: int, max_points: int, rank: int, nranks: int, grid_cell: float,
+            plane_threshold: float, max_match_sqd: float) -> L.SlioParams:
+    lib = L.load()
+    p = L.SlioParams()
+    L.check(lib.slio_params_default(C.byref(p)), "slio_params_default")
+    p.device, p.max_points, p.rank, p.nranks = device, max_points, rank, nranks
+    p.grid_cell, p.plane_threshold, p.max_match_sqd = grid_cell, plane_threshold, max_match_sqd
+    return p
+
+
+class _Handle:
+    def __init__(self, params: L.SlioParams):
+        self.lib = L.load()
+        self.h = C.c_void_p()
+        L.check(self.lib.slio_create(C.byref(self.h), C.byref(params)), "slio_create")
+        self.params = params
+
+    def close(self):
+        if self.h:
+            self.lib.slio_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class KdTreeMap(_Handle):
+    """Stands where ``KD_TREE<PointType> ikdtree`` stands (static snapshot).
+
+    ``Build`` mirrors KD_TREE::Build (ikd_Tree.cpp:355-367); neighbour indices
+    reported by the filter refer to rows of the array passed to Build.
+    """
+
+    def __init__(self, device: int = 0, grid_cell: float = 1.0):
+        super().__init__(_params(device, 1, 0, 1, grid_cell, 0.1, 5.0))
+        self.points = np.zeros((0, 3), np.float32)
+
+    def Build(self, points: np.ndarray) -> None:
+        pts = np.ascontiguousarray(np.asarray(points, dtype=np.float32)[:, :3])
+        x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
+        L.check(self.lib.slio_map_upload(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0]),
+                "KdTreeMap.Build")
+        self.points = pts
+
+    def size(self) -> int:
+        return int(self.points.shape[0])
+
+    def grid_info(self):
+        dims = (C.c_int32 * 3)()
+        cell = C.c_float()
+        n = C.c_int64()
+        L.check(self.lib.slio_map_info(self.h, dims, C.byref(cell), C.byref(n)), "map_info")
+        return tuple(dims), cell.value, n.value
+
+
+@dataclass
+class DynShareData:
+    """dyn_share_datastruct (esekfom.hpp:32-40), reduced form."""
+    valid: bool = True
+    converge: bool = True
+    HTH: np.ndarray | None = None   # 12x12
+    HTh: np.ndarray | None = None   # 12
+    m: int = 0
+
+
+class Esekf(_Handle):
+    """esekfom::esekf on the MI355X path."""
+
+    def __init__(self, device: int = 0, max_points: int = 100000, rank: int = 0,
+                 nranks: int = 1, plane_threshold: float = 0.1, max_match_sqd: float = 5.0):
+        super().__init__(_params(device, max_points, rank, nranks, 1.0, plane_threshold,
+                                 max_match_sqd))
+        self.x_ = StateIkfom()
+        self.P_ = np.eye(24)
+        self._map_src = None
+        self._scan_ref = None
+        self.last_stats = L.SlioIkfStats()
+
+    # --- accessors (esekfom.hpp:50-56)
+    def get_x(self) -> StateIkfom:
+        return self.x_
+
+    def get_P(self) -> np.ndarray:
+        return self.P_
+
+    def change_x(self, x: StateIkfom) -> None:
+        self.x_ = x
+
+    def change_P(self, P: np.ndarray) -> None:
+        self.P_ = np.array(P, dtype=np.float64).reshape(24, 24)
+
+    # --- plumbing
+    def _bind(self, feats_down_body: np.ndarray, ikdtree: KdTreeMap) -> int:
+        if self._map_src is not ikdtree:
+            L.check(self.lib.slio_map_share(self.h, ikdtree.h), "map_share")
+            self._map_src = ikdtree
+        pts = np.ascontiguousarray(np.asarray(feats_down_body, dtype=np.float32)[:, :3])
+        x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
+        L.check(self.lib.slio_scan_upload(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0]),
+                "scan_upload")
+        self._scan_ref = feats_down_body
+        return pts.shape[0]
+
+    def boxplus(self, x: StateIkfom, f: np.ndarray) -> StateIkfom:
+        out = L.SlioState()
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        xc = x.to_c()
+        L.check(self.lib.slio_state_boxplus(C.byref(xc), L.dptr(f), C.byref(out)), "boxplus")
+        return StateIkfom.from_c(out)
+
+    def boxminus(self, x1: StateIkfom, x2: StateIkfom) -> np.ndarray:
+        d = np.zeros(24)
+        a, b = x1.to_c(), x2.to_c()
+        L.check(self.lib.slio_state_boxminus(C.byref(a), C.byref(b), L.dptr(d)), "boxminus")
+        return d
+
+    def h_share_model(self, ekfom_data: DynShareData, feats_down_body: np.ndarray,
+                      ikdtree: KdTreeMap, Nearest_Points: dict | None,
+                      extrinsic_est: bool) -> None:
+        """One measurement pass (esekfom.hpp:106-227); search iff ekfom_data.converge."""
+        if feats_down_body is not self._scan_ref or self._map_src is not ikdtree:
+            self._bind(feats_down_body, ikdtree)
+        pose = L.SlioPose()
+        pose.rot[:] = list(self.x_.rot)
+        pose.pos[:] = list(self.x_.pos)
+        pose.rli[:] = list(self.x_.offset_R_L_I)
+        pose.tli[:] = list(self.x_.offset_T_L_I)
+        HTH = np.zeros(78)
+        HTh = np.zeros(12)
+        m = C.c_int64()
+        L.check(self.lib.slio_iterate(self.h, C.byref(pose), int(ekfom_data.converge),
+                                      int(extrinsic_est), L.dptr(HTH), L.dptr(HTh), C.byref(m)),
+                "h_share_model")
+        full = np.zeros((12, 12))
+        full[np.triu_indices(12)] = HTH
+        full = full + np.triu(full, 1).T
+        ekfom_data.HTH, ekfom_data.HTh, ekfom_data.m = full, HTh, int(m.value)
+        ekfom_data.valid = m.value >= 1
+        if Nearest_Points is not None:
+            Nearest_Points.update(self.nearest_points())
+
+    def nearest_points(self) -> dict:
+        b, e = C.c_int64(), C.c_int64()
+        L.check(self.lib.slio_shard_range(self.h, C.byref(b), C.byref(e)), "shard_range")
+        n = e.value - b.value
+        idx = np.zeros((n, 5), np.int32)
+        sqd = np.zeros((n, 5), np.float32)
+        sel = np.zeros(n, np.uint8)
+        L.check(self.lib.slio_get_neighbors(self.h, L.iptr(idx), L.fptr(sqd), L.u8ptr(sel)),
+                "get_neighbors")
+        return {"index": idx, "sq_dist": sqd, "selected": sel.astype(bool), "begin": b.value}
+
+    def planes(self) -> np.ndarray:
+        b, e = C.c_int64(), C.c_int64()
+        self.lib.slio_shard_range(self.h, C.byref(b), C.byref(e))
+        out = np.zeros((e.value - b.value, 4), np.float32)
+        L.check(self.lib.slio_get_planes(self.h, L.fptr(out)), "get_planes")
+        return out
+
+    def update_iterated_dyn_share_modified(self, R: float, feats_down_body: np.ndarray,
+                                           ikdtree: KdTreeMap, Nearest_Points: dict | None,
+                                           maximum_iter: int, extrinsic_est: bool,
+                                           mode: int = L.SLIO_MODE_REFERENCE,
+                                           reduce=None) -> None:
+        """esekfom.hpp:270-346 (host C++ driver slio_ikf_update)."""
+        self._bind(feats_down_body, ikdtree)
+        xc = self.x_.to_c()
+        P = np.ascontiguousarray(self.P_, dtype=np.float64).copy()
+        cb = reduce if reduce is not None else L.ALLREDUCE_FN()
+        st = L.SlioIkfStats()
+        L.check(self.lib.slio_ikf_update(self.h, C.byref(xc), L.dptr(P), float(R), int(maximum_iter),
+                                         int(extrinsic_est), int(mode), cb, None, C.byref(st)),
+                "update_iterated_dyn_share_modified")
+        self.x_ = StateIkfom.from_c(xc)
+        self.P_ = P.reshape(24, 24)
+        self.last_stats = st
+        if Nearest_Points is not None:
+            Nearest_Points.update(self.nearest_points())

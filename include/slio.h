@@ -1,0 +1,207 @@
+/*
+ * slio.h — C-ABI drop-in boundary of the MI355X IKF scan-matching core.
+ *
+ * The reference (zhan994/agi_lidar_slam, S-FAST_LIO) has no plugin API for this
+ * path; its seam is the C++ call
+ *
+ *   kf.update_iterated_dyn_share_modified(R, feats_down_body, ikdtree,
+ *                                         Nearest_Points, maximum_iter,
+ *                                         extrinsic_est)
+ *       src/S-FAST_LIO/include/esekfom.hpp:270-275
+ *       called from src/S-FAST_LIO/src/laserMapping.cpp:772-774
+ *       and        src/S-FAST_LIO/src/laserMapping_re.cpp:663-665
+ *
+ * and, inside it, one measurement pass
+ *
+ *   esekf::h_share_model(dyn_share_datastruct&, feats_down_body, ikdtree,
+ *                        Nearest_Points, extrinsic_est)
+ *       src/S-FAST_LIO/include/esekfom.hpp:106-227
+ *
+ * whose per-point work (body->world transform, ikd-Tree 5-NN
+ * KD_TREE::Nearest_Search ikd_Tree.cpp:370-402, esti_plane common_lib.h:102-134,
+ * residual + range gate, Jacobian row) and whose H^T H / H^T h products
+ * (esekfom.hpp:306-319) run here as HIP kernels on gfx950.  The 24x24 filter
+ * algebra stays on the host (slio_ikf_update below, host C++).
+ *
+ * Conventions: plain pointers and sizes, int status (0 ok, <0 error, never
+ * throws), one opaque handle per filter; a handle is not thread-safe.  All
+ * host buffers are caller-owned.  Errors: slio_last_error() returns a
+ * thread-local message for the last failing call on this thread.
+ */
+#ifndef SLIO_H
+#define SLIO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLIO_NUM_MATCH 5   /* NUM_MATCH_POINTS, common_lib.h:22 */
+#define SLIO_NPROD 91      /* 78 (H^T H upper triangle) + 12 (H^T h) + 1 (m) */
+#define SLIO_NHTH 78
+#define SLIO_NSUPER 8      /* fixed summation tree: 8 super-chunks of the scan */
+#define SLIO_CHUNK 128     /* scan points per reduction chunk (one workgroup) */
+
+enum {
+  SLIO_OK = 0,
+  SLIO_EINVAL = -1,    /* bad argument */
+  SLIO_ENOMEM = -2,    /* device or host allocation failed */
+  SLIO_EDEVICE = -3,   /* HIP runtime error */
+  SLIO_ECAPACITY = -4, /* scan larger than params.max_points */
+  SLIO_ESTATE = -5     /* call out of order (e.g. iterate before map upload) */
+};
+
+typedef struct slio_ctx* slio_handle;
+
+typedef struct slio_params {
+  int32_t device;          /* HIP device ordinal                              */
+  int32_t max_points;      /* scan capacity; reference caps at 100000
+                              (esekfom.hpp:23-29)                             */
+  int32_t rank;            /* this handle's shard of the scan points          */
+  int32_t nranks;          /* 1, 2, 4 or 8 (must divide SLIO_NSUPER)          */
+  float grid_cell;         /* map hash-grid cell edge in metres (0 -> 1.0)    */
+  float plane_threshold;   /* esti_plane threshold, 0.1f (esekfom.hpp:157)    */
+  float max_match_sqd;     /* 5th-NN sq.-distance gate, 5 (esekfom.hpp:147)   */
+  int32_t reserved;
+  int64_t max_grid_cells;  /* dense cell-table budget (0 -> 1<<29)            */
+} slio_params;
+
+/* Pose slice of state_ikfom used by the measurement model
+ * (use-ikfom.hpp:18-27).  Rotations are Sophus::SO3 unit quaternions stored
+ * (w, x, y, z); the kernel rotates points with the quaternion exactly as
+ * SO3::operator*(Vector3d) does (esekfom.hpp:128-129). */
+typedef struct slio_pose {
+  double rot[4];  /* x_.rot          */
+  double pos[3];  /* x_.pos          */
+  double rli[4];  /* x_.offset_R_L_I */
+  double tli[3];  /* x_.offset_T_L_I */
+} slio_pose;
+
+/* Full 24-D state_ikfom (use-ikfom.hpp:18-27); vector order of boxplus /
+ * boxminus (esekfom.hpp:59-73, 236-258): pos, rot, R_LI, T_LI, vel, bg, ba,
+ * grav. */
+typedef struct slio_state {
+  double pos[3];
+  double rot[4];
+  double rli[4];
+  double tli[3];
+  double vel[3];
+  double bg[3];
+  double ba[3];
+  double grav[3];
+} slio_state;
+
+/* ---- handle lifecycle --------------------------------------------------- */
+int slio_params_default(slio_params* p);
+int slio_create(slio_handle* out, const slio_params* p);
+int slio_destroy(slio_handle h);
+/* Use an external hipStream_t (e.g. torch's current stream) instead of the
+ * handle's own stream; NULL restores the handle's stream. */
+int slio_set_stream(slio_handle h, void* hip_stream);
+const char* slio_last_error(void);
+
+/* ---- map (replaces KD_TREE::Build, ikd_Tree.cpp:355-367, for a static map;
+ *      the search side replaces KD_TREE::Nearest_Search ikd_Tree.cpp:370) -- */
+/* Upload a map snapshot (host SoA float32, n points) and build the device
+ * grid index.  Neighbour indices reported later refer to positions in these
+ * arrays. */
+int slio_map_upload(slio_handle h, const float* x, const float* y,
+                    const float* z, int64_t n);
+/* Share src's read-only device map with h (same device; batched replay). */
+int slio_map_share(slio_handle h, slio_handle src);
+/* Grid diagnostics: dims[3], cell edge, number of map points. */
+int slio_map_info(slio_handle h, int32_t dims[3], float* cell, int64_t* n);
+
+/* ---- scan (feats_down_body, laserMapping.cpp:737-739) -------------------- */
+/* Upload the whole scan (host SoA float32, body frame).  With nranks > 1
+ * every rank uploads the full scan and processes its own point shard. */
+int slio_scan_upload(slio_handle h, const float* x, const float* y,
+                     const float* z, int64_t n);
+/* Point range [begin, end) this handle processes for the uploaded scan. */
+int slio_shard_range(slio_handle h, int64_t* begin, int64_t* end);
+
+/* ---- one h_share_model pass (esekfom.hpp:106-227) + reduction ----------- */
+/* Enqueue one measurement pass on the device.  do_search = ekfom_data.converge
+ * (esekfom.hpp:138): 1 re-runs the 5-NN search and the gate, 0 reuses the
+ * neighbours / plane / selection of the previous pass exactly like
+ * point_selected_surf does.  The pass leaves SLIO_NSUPER x SLIO_NPROD fp64
+ * super-chunk sums in the handle's device buffer (rows of super-chunks this
+ * rank does not own are zero, so a SUM all-reduce over ranks is an exact
+ * gather).  Returns the device pointer through d_super if non-NULL. */
+int slio_iterate_async(slio_handle h, const slio_pose* x, int do_search,
+                       int extrinsic_est, double** d_super);
+/* Make the handle write its super-chunk sums into a caller-owned device
+ * buffer of SLIO_NSUPER*SLIO_NPROD doubles (e.g. a torch tensor that an RCCL
+ * all-reduce then operates on); NULL restores the handle's own buffer. */
+int slio_set_super_buffer(slio_handle h, double* dev_buf);
+/* Copy the super-chunk sums to host (synchronises the stream). */
+int slio_super_download(slio_handle h, double super_out[SLIO_NSUPER * SLIO_NPROD]);
+/* Fixed-order sum of the super-chunk rows: H^T H upper triangle (row-major,
+ * i <= j), H^T h with h_i = -pd2 (esekfom.hpp:225), and m = effct_feat_num. */
+int slio_reduce_super(const double super_in[SLIO_NSUPER * SLIO_NPROD],
+                      double HTH[SLIO_NHTH], double HTh[12], int64_t* m);
+/* Convenience: iterate_async + download + reduce (single rank). */
+int slio_iterate(slio_handle h, const slio_pose* x, int do_search,
+                 int extrinsic_est, double HTH[SLIO_NHTH], double HTh[12],
+                 int64_t* m);
+
+/* ---- per-point results (Nearest_Points / point_selected_surf / normvec) -- */
+/* For the shard's points (n = end - begin): neighbour map indices (-1 if
+ * fewer than 5 map points exist), f32 squared distances ascending (the
+ * pointSearchSqDis of esekfom.hpp:135-141), final selection flag. */
+int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel);
+/* Plane (a, b, c, d) per point; (a,b,c) unit normal, d offset, or NaNs where
+ * esti_plane failed or the point was gated out before the fit. */
+int slio_get_planes(slio_handle h, float* abcd);
+/* Residual pd2 (normvec->points[i].intensity, esekfom.hpp:159-171) of the last
+ * pass for selected points, NaN otherwise. */
+int slio_get_residuals(slio_handle h, float* pd2);
+
+/* ---- kernel timing (HIP events on the handle's stream) ------------------- */
+#define SLIO_KERNEL_SEARCH 0   /* fused search pass (kNN + plane + Jacobian + chunk sums) */
+#define SLIO_KERNEL_REUSE 1    /* non-search pass                                          */
+#define SLIO_KERNEL_SUPER 2    /* super-chunk sums                                         */
+/* enable != 0 brackets every launch with hipEvents and accumulates elapsed
+ * device time per kernel kind; enabling resets the counters. */
+int slio_profile(slio_handle h, int enable);
+/* Accumulated device milliseconds and launch count of a kernel kind
+ * (synchronises the stream). */
+int slio_profile_read(slio_handle h, int kind, double* ms, int64_t* launches);
+
+/* ---- host IKF driver (update_iterated_dyn_share_modified, host C++) ------ */
+/* Optional cross-rank reduction hook: must SUM-all-reduce `count` doubles at
+ * device pointer dev_buf in place, ordered on `stream`. */
+typedef int (*slio_allreduce_fn)(void* ctx, double* dev_buf, int64_t count,
+                                 void* stream);
+
+typedef struct slio_ikf_stats {
+  int32_t passes;        /* h_share_model passes run                   */
+  int32_t searches;      /* passes with the kNN search                 */
+  int32_t valid_passes;  /* passes with effct_feat_num >= 1            */
+  int32_t converged;     /* dyn_share.converge at exit                 */
+  int64_t last_m;        /* effct_feat_num of the last pass            */
+  double device_ms;      /* wall time inside device passes (host clock)*/
+} slio_ikf_stats;
+
+#define SLIO_MODE_REFERENCE 0  /* esekfom.hpp:292-345 control flow       */
+#define SLIO_MODE_FIXED 1      /* exactly maximum_iter passes, kNN search
+                                  every pass, P update at the end        */
+
+/* Run the iterated update on state x (in/out) and covariance P (24x24
+ * row-major, in/out) with measurement noise R (LASER_POINT_COV,
+ * laserMapping.cpp:29).  reduce may be NULL for a single rank. */
+int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R,
+                    int maximum_iter, int extrinsic_est, int mode,
+                    slio_allreduce_fn reduce, void* reduce_ctx,
+                    slio_ikf_stats* stats);
+
+/* Manifold helpers exported for tests (esekfom.hpp:59-73, 236-258). */
+int slio_state_boxplus(const slio_state* x, const double dx[24], slio_state* out);
+int slio_state_boxminus(const slio_state* x1, const slio_state* x2, double dx[24]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SLIO_H */

@@ -1,0 +1,146 @@
+"""ctypes wrapper of oracle/_build/libslio_oracle.so (test infrastructure only).
+
+The oracle restates ikd-Tree kNN, esti_plane, h_share_model and the IKF
+update on the CPU (see slio_oracle.cpp for the reference file:line map).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libslio_oracle.so")
+
+_FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int32)
+_I64P = C.POINTER(C.c_int64)
+_U8P = C.POINTER(C.c_uint8)
+_lib = None
+
+
+def build() -> str:
+    src = os.path.join(HERE, "slio_oracle.cpp")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
+    return LIB
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        build()
+        lib = C.CDLL(LIB)
+        lib.orc_tree_build.restype = C.c_void_p
+        lib.orc_tree_build.argtypes = [_FP, _FP, _FP, C.c_int64]
+        lib.orc_tree_free.argtypes = [C.c_void_p]
+        lib.orc_knn.argtypes = [C.c_void_p, _FP, _FP, _FP, C.c_int64, C.c_int, _IP, _FP, C.c_int]
+        lib.orc_esti_plane.argtypes = [_FP, C.c_float, _FP]
+        lib.orc_body_to_world.argtypes = [_DP, _FP, _FP, _FP, C.c_int64, _FP, _FP, _FP]
+        lib.orc_pass.argtypes = [C.c_void_p, _DP, _FP, _FP, _FP, C.c_int64, C.c_int, C.c_int,
+                                 C.c_float, C.c_float, _IP, _FP, _FP, _U8P, _FP, _DP, _DP, C.c_int]
+        lib.orc_ikf_update.argtypes = [C.c_void_p, _FP, _FP, _FP, C.c_int64, _DP, _DP, C.c_double,
+                                       C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
+                                       C.c_int, _IP, _FP, _U8P, _I64P]
+        _lib = lib
+    return _lib
+
+
+def _f(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class Tree:
+    """Static restatement of KD_TREE::Build + Nearest_Search."""
+
+    def __init__(self, pts: np.ndarray):
+        self.lib = load()
+        self.pts = _f(pts)
+        self.x, self.y, self.z = (_f(self.pts[:, k]) for k in range(3))
+        self.t = self.lib.orc_tree_build(self.x.ctypes.data_as(_FP), self.y.ctypes.data_as(_FP),
+                                         self.z.ctypes.data_as(_FP), self.pts.shape[0])
+
+    def __del__(self):
+        if getattr(self, "t", None):
+            self.lib.orc_tree_free(self.t)
+            self.t = None
+
+    def knn(self, q: np.ndarray, k: int = 5, threads: int = 8):
+        qx, qy, qz = (_f(q[:, j]) for j in range(3))
+        n = q.shape[0]
+        idx = np.zeros((n, k), np.int32)
+        sqd = np.zeros((n, k), np.float32)
+        rc = self.lib.orc_knn(self.t, qx.ctypes.data_as(_FP), qy.ctypes.data_as(_FP),
+                              qz.ctypes.data_as(_FP), n, k, idx.ctypes.data_as(_IP),
+                              sqd.ctypes.data_as(_FP), threads)
+        assert rc == 0
+        return idx, sqd
+
+
+def esti_plane(nb: np.ndarray, threshold: float = 0.1):
+    nb = _f(nb).reshape(15)
+    out = np.zeros(4, np.float32)
+    ok = load().orc_esti_plane(nb.ctypes.data_as(_FP), threshold, out.ctypes.data_as(_FP))
+    return bool(ok), out
+
+
+def body_to_world(state26: np.ndarray, body: np.ndarray) -> np.ndarray:
+    s = np.ascontiguousarray(state26, dtype=np.float64)
+    bx, by, bz = (_f(body[:, j]) for j in range(3))
+    n = body.shape[0]
+    w = [np.zeros(n, np.float32) for _ in range(3)]
+    load().orc_body_to_world(s.ctypes.data_as(_DP), bx.ctypes.data_as(_FP), by.ctypes.data_as(_FP),
+                             bz.ctypes.data_as(_FP), n, *(a.ctypes.data_as(_FP) for a in w))
+    return np.stack(w, 1)
+
+
+class PassState:
+    """Per-point arrays carried across passes (Nearest_Points, point_selected_surf)."""
+
+    def __init__(self, n: int):
+        self.idx = np.full((n, 5), -1, np.int32)
+        self.sqd = np.full((n, 5), np.inf, np.float32)
+        self.plane = np.full((n, 4), np.nan, np.float32)
+        self.sel = np.zeros(n, np.uint8)
+        self.resid = np.full(n, np.nan, np.float32)
+
+
+def h_pass(tree: Tree, state26, body, ps: PassState, do_search: bool, extrinsic: bool = False,
+           plane_thr: float = 0.1, max_sqd: float = 5.0, threads: int = 8,
+           rows: np.ndarray | None = None) -> np.ndarray:
+    """One h_share_model pass; returns the 91 sequential sums.  If ``rows``
+    (n, 14) float64 is given it receives the per-point rows [h_x, -pd2, 1]."""
+    s = np.ascontiguousarray(state26, dtype=np.float64)
+    bx, by, bz = (_f(body[:, j]) for j in range(3))
+    out = np.zeros(91)
+    load().orc_pass(tree.t, s.ctypes.data_as(_DP), bx.ctypes.data_as(_FP), by.ctypes.data_as(_FP),
+                    bz.ctypes.data_as(_FP), body.shape[0], int(do_search), int(extrinsic),
+                    plane_thr, max_sqd, ps.idx.ctypes.data_as(_IP), ps.sqd.ctypes.data_as(_FP),
+                    ps.plane.ctypes.data_as(_FP), ps.sel.ctypes.data_as(_U8P),
+                    ps.resid.ctypes.data_as(_FP), out.ctypes.data_as(_DP),
+                    rows.ctypes.data_as(_DP) if rows is not None else None, threads)
+    return out
+
+
+def ikf_update(tree: Tree, body, state26, P, R=0.001, maximum_iter=4, extrinsic=False, mode=0,
+               plane_thr=0.1, max_sqd=5.0, reference_gain=1, threads=3):
+    """update_iterated_dyn_share_modified; returns (state26, P, stats, idx, sqd, sel)."""
+    s = np.ascontiguousarray(state26, dtype=np.float64).copy()
+    Pm = np.ascontiguousarray(P, dtype=np.float64).copy()
+    bx, by, bz = (_f(body[:, j]) for j in range(3))
+    n = body.shape[0]
+    idx = np.zeros((n, 5), np.int32)
+    sqd = np.zeros((n, 5), np.float32)
+    sel = np.zeros(n, np.uint8)
+    st = np.zeros(5, np.int64)
+    rc = load().orc_ikf_update(tree.t, bx.ctypes.data_as(_FP), by.ctypes.data_as(_FP),
+                               bz.ctypes.data_as(_FP), n, s.ctypes.data_as(_DP),
+                               Pm.ctypes.data_as(_DP), R, maximum_iter, int(extrinsic), mode,
+                               plane_thr, max_sqd, reference_gain, threads,
+                               idx.ctypes.data_as(_IP), sqd.ctypes.data_as(_FP),
+                               sel.ctypes.data_as(_U8P), st.ctypes.data_as(_I64P))
+    assert rc == 0, rc
+    return s, Pm, st, idx, sqd, sel
