@@ -36,8 +36,10 @@ class SlioParams(C.Structure):
         ("grid_cell", C.c_float),
         ("plane_threshold", C.c_float),
         ("max_match_sqd", C.c_float),
-        ("reserved", C.c_int32),
+        ("lanes_per_query", C.c_int32),
         ("max_grid_cells", C.c_int64),
+        ("search_radius", C.c_float),
+        ("reserved", C.c_int32),
     ]
 
 

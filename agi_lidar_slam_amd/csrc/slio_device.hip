@@ -42,13 +42,23 @@ void set_error(const std::string& msg) { g_err = msg; }
     }                                                                           \
   } while (0)
 
-constexpr int kLPQ = 8;                          // lanes per query
 constexpr int kBlock = 256;                      // threads per search workgroup
-constexpr int kQPP = kBlock / kLPQ;              // queries per pass (32)
-constexpr int kPasses = SLIO_CHUNK / kQPP;       // passes per chunk (4)
+constexpr int kDefaultLPQ = 2;                   // lanes per query (tuned on MI355X)
 constexpr uint64_t kInfKey = ~0ull;
 
-static_assert(SLIO_CHUNK % kQPP == 0, "chunk must be a multiple of queries/pass");
+#ifdef SLIO_ABL_STAMP
+// diagnostic build only: per-block phase timestamps (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_stamps[8192][8];
+#define STAMP(slot)                                                                \
+  do {                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192)                              \
+      g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+#else
+#define STAMP(slot) \
+  do {              \
+  } while (0)
+#endif
 
 __constant__ uint8_t c_pa[SLIO_NPROD];
 __constant__ uint8_t c_pb[SLIO_NPROD];
@@ -222,83 +232,309 @@ __device__ __forceinline__ bool residual_gate(const float (&abcd)[4], float wx, 
 }
 
 // ---------------------------------------------------------------- top-5
-__device__ __forceinline__ void insert5(uint64_t key, uint32_t pos, uint64_t (&k)[5],
-                                        uint32_t (&p)[5]) {
-  if (key < k[4]) {
-    k[4] = key;
-    p[4] = pos;
+// A per-lane sorted list of the 5 best candidates.  Key = (float bits of the
+// squared distance << 32) | map index, so one u64 compare orders by distance
+// then index (squared distances are >= +0, whose bit patterns sort like the
+// values).  p[] holds the candidates' positions in the cell-sorted map.
+struct Top5 {
+  uint64_t k[5];
+  uint32_t p[5];
+};
+
+__device__ __forceinline__ void top5_clear(Top5& t) {
 #pragma unroll
-    for (int j = 4; j > 0; --j) {
-      const bool sw = k[j] < k[j - 1];
-      const uint64_t ka = k[j - 1], kb = k[j];
-      const uint32_t pa = p[j - 1], pb = p[j];
-      k[j - 1] = sw ? kb : ka;
-      k[j] = sw ? ka : kb;
-      p[j - 1] = sw ? pb : pa;
-      p[j] = sw ? pa : pb;
-    }
+  for (int j = 0; j < 5; ++j) {
+    t.k[j] = kInfKey;
+    t.p[j] = 0;
   }
 }
 
-__device__ __forceinline__ void consider(const float4 c, uint32_t pos, float qx, float qy,
-                                         float qz, uint64_t (&k)[5], uint32_t (&p)[5]) {
-  const float ddx = qx - c.x, ddy = qy - c.y, ddz = qz - c.z;
-  const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;
-  const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c.w);
-  insert5(key, pos, k, p);
+// Branch-free insertion: slot j takes k[j-1] if key < k[j-1], key if
+// k[j-1] <= key < k[j], else keeps k[j].  All five slots update in parallel
+// (no serial compare-swap chain).
+__device__ __forceinline__ void top5_insert(Top5& t, uint64_t key, uint32_t pos) {
+  bool c[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) c[j] = key < t.k[j];
+#pragma unroll
+  for (int j = 4; j > 0; --j) {
+    t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
+    t.p[j] = c[j - 1] ? t.p[j - 1] : (c[j] ? pos : t.p[j]);
+  }
+  t.k[0] = c[0] ? key : t.k[0];
+  t.p[0] = c[0] ? pos : t.p[0];
 }
 
-// butterfly merge of the kLPQ per-lane lists of a query group
-__device__ __forceinline__ void group_merge(uint64_t (&k)[5], uint32_t (&p)[5]) {
+__device__ __forceinline__ void consider(Top5& t, const float4 c, uint32_t pos, float qx, float qy,
+                                         float qz) {
+  const float ddx = qx - c.x, ddy = qy - c.y, ddz = qz - c.z;
+  const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+  const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c.w);
+  if (key < t.k[4]) top5_insert(t, key, pos);
+}
+
+// butterfly merge of the LPQ per-lane lists of a query group (lanes of a
+// group are consecutive and aligned, so xor partners stay in the group)
+template <int LPQ>
+__device__ __forceinline__ void group_merge(Top5& t) {
 #pragma unroll
-  for (int m = 1; m < kLPQ; m <<= 1) {
+  for (int m = 1; m < LPQ; m <<= 1) {
     uint64_t ok[5];
     uint32_t op[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      ok[j] = __shfl_xor(k[j], m);
-      op[j] = __shfl_xor(p[j], m);
+      ok[j] = __shfl_xor(t.k[j], m);
+      op[j] = __shfl_xor(t.p[j], m);
     }
 #pragma unroll
-    for (int j = 0; j < 5; ++j) insert5(ok[j], op[j], k, p);
+    for (int j = 0; j < 5; ++j)
+      if (ok[j] < t.k[4]) top5_insert(t, ok[j], op[j]);
   }
 }
 
-// Scan all candidates of cube [c-r, c+r]^3 minus cube [c-rin, c+rin]^3
-// (rin < 0: nothing excluded), clamped to the grid; lanes stride over runs.
-__device__ void scan_region(const float4* __restrict__ pts,
-                            const uint32_t* __restrict__ start, const GridGeom& g, int cx,
-                            int cy, int cz, int r, int rin, int sub, float qx, float qy,
-                            float qz, uint64_t (&k)[5], uint32_t (&p)[5]) {
+// Conservative lower bound of the distance from coordinate q to the points
+// assigned to grid cell i along one axis (cell edges are known to +-tol).
+__device__ __forceinline__ float axis_gap(float q, int i, float o, float h, float tol) {
+  const float lo = o + (float)i * h - tol;
+  const float hi = o + (float)(i + 1) * h + tol;
+  return fmaxf(fmaxf(lo - q, q - hi), 0.0f);
+}
+
+// A "run" is a contiguous x-range of cells in one (y, z) row: contiguous
+// points in the cell-sorted map.  Runs are named by bits of a 64-bit mask:
+// bit rr (0..24) = row (dy, dz) = (rr % 5 - 2, rr / 5 - 2) of the 5x5 rows
+// around the query cell, bit 32 + rr = a second (right) segment of that row.
+// Search regions (all exact, see k_search_pass):
+//   mode 1: the 3x3x3 block (x in [cx-1, cx+1]);
+//   mode 2: cells of the 5x5x5 cube with box gap^2 <= lim, minus the 3x3x3 block;
+//   mode 3: cells of the 5x5x5 cube with box gap^2 <= lim (a sphere);
+//   mode 4: cells with lim0 < box gap^2 <= lim (the shell a grown sphere adds).
+struct RunCtx {
+  int cx, cy, cz;
+  float qx, qy, qz;
+  int mode;
+  float lim0, lim;
+};
+
+__device__ __forceinline__ float sq_gap(float q, int i, float o, const GridGeom& g) {
+  const float a = axis_gap(q, i, o, g.h, g.tol);
+  return a * a;
+}
+
+// rows of the 5x5 whose (y, z) gap is within lim and which lie in the grid
+__device__ __forceinline__ uint64_t sphere_rows(const GridGeom& g, const RunCtx& rc, float lim) {
+  float gy[5], gz[5];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) {
+    gy[d] = sq_gap(rc.qy, rc.cy - 2 + d, g.oy, g);
+    gz[d] = sq_gap(rc.qz, rc.cz - 2 + d, g.oz, g);
+  }
+  uint64_t m = 0;
+#pragma unroll
+  for (int rr = 0; rr < 25; ++rr) {
+    const int dy = rr % 5, dz = rr / 5;
+    const int yy = rc.cy - 2 + dy, zz = rc.cz - 2 + dz;
+    const bool in = yy >= 0 && yy < g.dy && zz >= 0 && zz < g.dz;
+    if (in && gy[dy] + gz[dz] <= lim) m |= 1ull << rr;
+  }
+  return m;
+}
+
+// contiguous x-range [lo, hi] around cx of the cells with gap^2 <= rem
+__device__ __forceinline__ void sphere_span(const GridGeom& g, const RunCtx& rc, float rem, int& lo,
+                                            int& hi) {
+  const float gm2 = sq_gap(rc.qx, rc.cx - 2, g.ox, g), gm1 = sq_gap(rc.qx, rc.cx - 1, g.ox, g);
+  const float gp1 = sq_gap(rc.qx, rc.cx + 1, g.ox, g), gp2 = sq_gap(rc.qx, rc.cx + 2, g.ox, g);
+  lo = (gm2 <= rem) ? rc.cx - 2 : (gm1 <= rem) ? rc.cx - 1 : rc.cx;
+  hi = (gp2 <= rem) ? rc.cx + 2 : (gp1 <= rem) ? rc.cx + 1 : rc.cx;
+  if (rem < 0.0f) {
+    lo = 1;
+    hi = 0;
+  }
+}
+
+__device__ __forceinline__ void run_range(const GridGeom& g, const RunCtx& rc, int bit, int& yy,
+                                          int& zz, int& xa, int& xb) {
+  const int rr = bit & 31;
+  const int dy = rr % 5, dz = rr / 5;
+  yy = rc.cy - 2 + dy;
+  zz = rc.cz - 2 + dz;
+  const bool right = bit >= 32;
+  if (rc.mode == 1) {
+    xa = rc.cx - 1;
+    xb = rc.cx + 1;
+  } else {
+    // recomputed rather than looked up: a runtime-indexed gy[]/gz[] would be
+    // lowered to scratch memory
+    const float gyz = sq_gap(rc.qy, yy, g.oy, g) + sq_gap(rc.qz, zz, g.oz, g);
+    int lo, hi;
+    sphere_span(g, rc, rc.lim - gyz, lo, hi);
+    if (rc.mode == 3) {
+      xa = lo;
+      xb = hi;
+    } else {
+      // exclude the cells an earlier pass already scanned: [cx-1, cx+1] of
+      // the inner rows (mode 2) or the smaller sphere's span (mode 4)
+      int lo0, hi0;
+      if (rc.mode == 2) {
+        const bool inner = dy >= 1 && dy <= 3 && dz >= 1 && dz <= 3;
+        lo0 = inner ? rc.cx - 1 : 1;
+        hi0 = inner ? rc.cx + 1 : 0;
+      } else {
+        sphere_span(g, rc, rc.lim0 - gyz, lo0, hi0);
+      }
+      if (lo0 > hi0) {  // nothing scanned before in this row
+        xa = right ? 1 : lo;
+        xb = right ? 0 : hi;
+      } else if (!right) {
+        xa = lo;
+        xb = min(hi, lo0 - 1);
+      } else {
+        xa = max(lo, hi0 + 1);
+        xb = hi;
+      }
+    }
+  }
+  xa = max(xa, 0);
+  xb = min(xb, g.dx - 1);
+  if (yy < 0 || yy >= g.dy || zz < 0 || zz >= g.dz) {
+    xa = 1;
+    xb = 0;
+  }
+}
+
+// Strided, software-pipelined sweep of a flattened candidate list made of up
+// to 9 contiguous runs (rs = run starts, pre = prefix lengths, T = total): the
+// U loads of step k+1 are issued before step k's candidates are consumed.
+template <int LPQ, int U>
+__device__ __forceinline__ void flat_addr(const uint32_t (&rs)[9], const uint32_t (&pre)[10],
+                                          uint32_t T, uint32_t t0, uint32_t (&a)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t tt = t0 + u * LPQ;
+    uint32_t ad = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+      if (tt >= pre[q]) ad = rs[q] + (tt - pre[q]);
+    a[u] = ad;
+  }
+  // slots past the end re-read slot 0's (valid) address: no branch per load
+#pragma unroll
+  for (int u = 1; u < U; ++u) a[u] = (t0 + u * LPQ < T) ? a[u] : a[0];
+}
+
+template <int LPQ, int U>
+__device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const uint32_t (&rs)[9],
+                                          const uint32_t (&pre)[10], uint32_t T, int sub,
+                                          float qx, float qy, float qz, Top5& t) {
+  uint32_t t0 = sub;
+  if (t0 >= T) return;
+  uint32_t a[U];
+  float4 c[U];
+  flat_addr<LPQ, U>(rs, pre, T, t0, a);
+#pragma unroll
+  for (int u = 0; u < U; ++u) c[u] = pts[a[u]];
+  for (;;) {
+    const uint32_t t1 = t0 + U * LPQ;
+    const bool more = t1 < T;
+    uint32_t an[U];
+    float4 cn[U];
+    if (more) {
+      flat_addr<LPQ, U>(rs, pre, T, t1, an);
+#pragma unroll
+      for (int u = 0; u < U; ++u) cn[u] = pts[an[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (t0 + u * LPQ < T) consider(t, c[u], a[u], qx, qy, qz);
+    if (!more) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = an[u];
+      c[u] = cn[u];
+    }
+    t0 = t1;
+  }
+}
+
+// Scan the runs of `mask` into the lane's list: run bounds are fetched 9 runs
+// at a time (their loads overlap), then the lanes of the group stride over
+// the flattened candidate list with U float4 loads in flight per lane.
+template <int LPQ, int U>
+__device__ __forceinline__ void scan_runs(const float4* __restrict__ pts, const uint32_t* __restrict__ start,
+                          const GridGeom& g, const RunCtx& rc, uint64_t mask, int sub, Top5& t) {
+  while (mask) {
+    uint32_t rs[9], pre[10];
+    pre[0] = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      uint32_t s = 0, e = 0;
+      if (mask) {
+        const int bit = __ffsll((unsigned long long)mask) - 1;
+        mask &= mask - 1;
+        int yy, zz, xa, xb;
+        run_range(g, rc, bit, yy, zz, xa, xb);
+        if (xa <= xb) {
+          const uint32_t rb = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
+          s = start[rb + xa];
+          e = start[rb + xb + 1];
+        }
+      }
+      rs[q] = s;
+      pre[q + 1] = pre[q] + (e - s);
+    }
+    const uint32_t T = pre[9];
+    scan_flat<LPQ, U>(pts, rs, pre, T, sub, rc.qx, rc.qy, rc.qz, t);
+  }
+}
+
+// Full grid-clamped cube [c-r, c+r]^3 (general fallback: queries outside the
+// grid, or a 5th neighbour beyond the 5x5x5 cube).
+template <int LPQ, int U>
+__device__ __forceinline__ void scan_cube(const float4* __restrict__ pts, const uint32_t* __restrict__ start,
+                          const GridGeom& g, int cx, int cy, int cz, int r, int sub, float qx,
+                          float qy, float qz, Top5& t) {
   const int z0 = max(cz - r, 0), z1 = min(cz + r, g.dz - 1);
   const int y0 = max(cy - r, 0), y1 = min(cy + r, g.dy - 1);
   const int xlo = max(cx - r, 0), xhi = min(cx + r, g.dx - 1);
-  if (xlo > xhi) return;
-  for (int zz = z0; zz <= z1; ++zz) {
-    for (int yy = y0; yy <= y1; ++yy) {
-      const bool inner_row = rin >= 0 && abs(zz - cz) <= rin && abs(yy - cy) <= rin;
-      const uint32_t rowbase = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
-      // up to two x segments
-      int sa0, sa1, sb0, sb1;
-      if (!inner_row) {
-        sa0 = xlo;
-        sa1 = xhi;
-        sb0 = 1;
-        sb1 = 0;
-      } else {
-        sa0 = xlo;
-        sa1 = min(cx - rin - 1, xhi);
-        sb0 = max(cx + rin + 1, xlo);
-        sb1 = xhi;
+  if (xlo > xhi || y0 > y1 || z0 > z1) return;
+  const int ny = y1 - y0 + 1;
+  const int nrun = ny * (z1 - z0 + 1);
+  for (int j0 = 0; j0 < nrun; j0 += 9) {
+    uint32_t rs[9], pre[10];
+    pre[0] = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const int j = j0 + q;
+      const bool ok = j < nrun;
+      const int jj = ok ? j : 0;
+      const int yy = y0 + jj % ny, zz = z0 + jj / ny;
+      const uint32_t rb = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
+      const uint32_t s = start[rb + xlo];
+      const uint32_t e = start[rb + xhi + 1];
+      rs[q] = s;
+      pre[q + 1] = pre[q] + (ok ? e - s : 0u);
+    }
+    const uint32_t T = pre[9];
+    for (uint32_t t0 = sub; t0 < T; t0 += U * LPQ) {
+      uint32_t a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t tt = t0 + u * LPQ;
+        uint32_t ad = 0;
+#pragma unroll
+        for (int q = 0; q < 9; ++q)
+          if (tt >= pre[q]) ad = rs[q] + (tt - pre[q]);
+        a[u] = ad;
       }
 #pragma unroll
-      for (int seg = 0; seg < 2; ++seg) {
-        const int a0 = seg ? sb0 : sa0, a1 = seg ? sb1 : sa1;
-        if (a0 > a1) continue;
-        const uint32_t s = start[rowbase + a0];
-        const uint32_t e = start[rowbase + a1 + 1];
-        for (uint32_t j = s + sub; j < e; j += kLPQ) consider(pts[j], j, qx, qy, qz, k, p);
-      }
+      for (int u = 1; u < U; ++u) a[u] = (t0 + u * LPQ < T) ? a[u] : a[0];
+      float4 c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) c[u] = pts[a[u]];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (t0 + u * LPQ < T) consider(t, c[u], a[u], qx, qy, qz);
     }
   }
 }
@@ -348,6 +584,7 @@ struct PassOut {
 struct PassCfg {
   float plane_thr;
   float max_sqd;
+  float radius_sq;  // sphere-first search radius^2 (0: 3x3x3 block first)
   int extrinsic;
   int64_t c_begin, c_end;  // global chunk range of this rank
 };
@@ -360,7 +597,10 @@ __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
   return c_begin + base + (b >> 3);
 }
 
-// fixed-order product phase: rows[SLIO_CHUNK][kRow] in LDS -> chunk partial
+// fixed-order product phase: rows[SLIO_CHUNK][kRow] in LDS -> chunk partial.
+// Thread (half, k) sums row[a_k] * row[b_k] over its rows with 4 interleaved
+// accumulators (rows r = 0,1,2,3 mod 4) to break the dependent fp64 add chain;
+// the accumulators and halves are then combined in a fixed order.
 template <int NT>
 __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], double (*part)[SLIO_NPROD],
                                                double* __restrict__ out) {
@@ -370,10 +610,16 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
   const int half = t >> 7, kk = t & 127;
   if (kk < SLIO_NPROD && half < kSplit) {
     const int a = c_pa[kk], b = c_pb[kk];
-    double s = 0.0;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     const int r0 = half * kRowsPer;
-    for (int r = r0; r < r0 + kRowsPer; ++r) s = s + rows[r][a] * rows[r][b];
-    part[half][kk] = s;
+#pragma unroll 2
+    for (int r = r0; r < r0 + kRowsPer; r += 4) {
+      s0 = s0 + rows[r][a] * rows[r][b];
+      s1 = s1 + rows[r + 1][a] * rows[r + 1][b];
+      s2 = s2 + rows[r + 2][a] * rows[r + 2][b];
+      s3 = s3 + rows[r + 3][a] * rows[r + 3][b];
+    }
+    part[half][kk] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
   if (t < SLIO_NPROD) {
@@ -384,148 +630,210 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_search_pass(const MapView map, const ScanDev scan,
-                                                        const PoseDev pose, const PassCfg cfg,
-                                                        const PassOut out) {
+template <int LPQ>
+constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
+
+// One h_share_model search pass over one 128-point chunk.
+// Phase 1 (kNN): LPQ lanes per scan point find the exact 5-NN; results go to
+// LDS.  Phase 2 (fit): one lane per point reloads the 5 neighbours (L2-hot),
+// runs esti_plane, the residual gate and the Jacobian row, and writes the
+// row to LDS.  Phase 3: fixed-order fp64 products -> chunk partial.
+template <int LPQ, int U, bool SPHERE>
+__global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
+    const MapView map, const ScanDev scan, const PoseDev pose, const PassCfg cfg,
+    const PassOut out) {
+  constexpr int NT = search_block<LPQ>();
+  constexpr int QPP = NT / LPQ;               // queries per kNN pass
+  constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
+  static_assert(SLIO_CHUNK % QPP == 0, "chunk must be a multiple of queries/pass");
+  static_assert(NT >= SLIO_CHUNK, "fit phase needs one lane per point");
   __shared__ double rows[SLIO_CHUNK][kRow];
-  __shared__ double part[kBlock / 128][SLIO_NPROD];
+  __shared__ double part[NT / 128][SLIO_NPROD];
+  __shared__ uint32_t nb_pos[SLIO_CHUNK][5];
+  __shared__ float nb_d5[SLIO_CHUNK];
+  __shared__ float4 qw[SLIO_CHUNK];
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
   const int tid = threadIdx.x;
-  const int sub = tid & (kLPQ - 1);
-  const int grp = tid / kLPQ;
+  const int sub = tid & (LPQ - 1);
+  const int grp = tid / LPQ;
   const GridGeom g = map.g;
   const float4* __restrict__ pts = map.pts;
   const uint32_t* __restrict__ start = map.start;
+  if (tid == 0) STAMP(0);
 
-  for (int pass = 0; pass < kPasses; ++pass) {
-    const int slot = pass * kQPP + grp;
+  // ---------------- phase 1: exact 5-NN
+  for (int pass = 0; pass < PASSES; ++pass) {
+    const int slot = pass * QPP + grp;
+    const int64_t i = chunk * SLIO_CHUNK + slot;
+    if (i >= scan.n) continue;
+    const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
+    float qx, qy, qz;
+    body_to_world(pose, bx, by, bz, qx, qy, qz);
+    Top5 t;
+    top5_clear(t);
+    const bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0;
+#if defined(SLIO_ABL_IO) || defined(SLIO_ABL_NOCAND)
+    // diagnostic: synthetic neighbours (the first 5 map points), no search
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      t.k[j] = ((uint64_t)__float_as_uint(0.1f * (j + 1)) << 32) | (uint64_t)j;
+      t.p[j] = j;
+    }
+#endif
+#if defined(SLIO_ABL_NOCAND)
+    if (finite) {
+      const int cx = cell_coord(qx, g.ox, g.inv_h);
+      const int cy = cell_coord(qy, g.oy, g.inv_h);
+      const int cz = cell_coord(qz, g.oz, g.inv_h);
+      uint32_t acc = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int yy = min(max(cy - 1 + q % 3, 0), g.dy - 1), zz = min(max(cz - 1 + q / 3, 0), g.dz - 1);
+        const uint32_t rb = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
+        acc += start[rb + min(max(cx - 1, 0), g.dx - 1)] ^ start[rb + min(cx + 2, g.dx)];
+      }
+      t.p[0] += (acc == 0x7fffffffu) ? 1u : 0u;
+    }
+#elif !defined(SLIO_ABL_IO)
+    if (finite) {
+      const int cx = cell_coord(qx, g.ox, g.inv_h);
+      const int cy = cell_coord(qy, g.oy, g.inv_h);
+      const int cz = cell_coord(qz, g.oz, g.inv_h);
+      const int ex = max(max(-cx, cx - (g.dx - 1)), 0);
+      const int ey = max(max(-cy, cy - (g.dy - 1)), 0);
+      const int ez = max(max(-cz, cz - (g.dz - 1)), 0);
+      int r = max(1, max(ex, max(ey, ez)));
+      bool done = false;
+      if (r == 1 && !SPHERE) {
+        // (1) the 3x3x3 block around the query cell: 9 runs, one batch
+        RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
+        scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
+        group_merge<LPQ>(t);
+        bool covers;
+        const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
+        const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+        done = covers || (t.k[4] != kInfKey && b1 > 0.0f && d5 < (b1 * b1) * 0.99999f);
+        if (!done && t.k[4] != kInfKey) {
+          // (2) exact refinement: every cell of the 5x5x5 cube whose
+          // conservative box gap is within the current 5th distance, minus
+          // the block already scanned (valid while that sphere stays inside
+          // the 5x5x5 cube; otherwise the general fallback takes over)
+          bool covers2;
+          const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, covers2);
+          if (covers2 || (b2 > 0.0f && d5 < (b2 * b2) * 0.99999f)) {
+            rc.mode = 2;
+            rc.lim = d5 * 1.00001f;
+            if (sub != 0) top5_clear(t);  // lane 0 keeps the merged list
+            const uint64_t rows = sphere_rows(g, rc, rc.lim);
+            scan_runs<LPQ, U>(pts, start, g, rc, rows | ((rows & 0x739c0ull) << 32), sub, t);
+            group_merge<LPQ>(t);
+            done = true;
+          }
+        }
+        r = 2;
+      } else if (r == 1) {
+        // sphere-first search: (1) cells of the 5x5x5 cube whose box gap^2 <=
+        // rho0^2, exact once 5 neighbours lie within rho0; (2) the shell out
+        // to the current 5th distance, exact while it stays inside the cube
+        RunCtx rc{cx, cy, cz, qx, qy, qz, 3, 0.0f, cfg.radius_sq * 1.00001f};
+        bool covers2;
+        const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, covers2);
+        const float cube2 = covers2 ? __int_as_float(0x7f800000) : b2 * b2 * 0.99999f;
+        uint64_t mask = sphere_rows(g, rc, rc.lim);
+        for (int step = 0; step < 2; ++step) {
+          scan_runs<LPQ, U>(pts, start, g, rc, mask, sub, t);
+          group_merge<LPQ>(t);
+          if (step == 1) {
+            done = true;
+            break;
+          }
+          const bool valid = t.k[4] != kInfKey;
+          const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+          done = valid && d5 <= cfg.radius_sq && d5 < cube2;
+          if (done || !valid || !(d5 < cube2)) break;
+          rc.mode = 4;
+          rc.lim0 = rc.lim;
+          rc.lim = fmaxf(d5 * 1.00001f, rc.lim0);
+          const uint64_t rows = sphere_rows(g, rc, rc.lim);
+          mask = rows | (rows << 32);
+          if (sub != 0) top5_clear(t);  // lane 0 keeps the merged list
+        }
+        r = 2;
+      }
+      // (3) general fallback: full cubes r, r+1, ... rescanned from scratch
+      for (; !done; ++r) {
+        top5_clear(t);
+        scan_cube<LPQ, U>(pts, start, g, cx, cy, cz, r, sub, qx, qy, qz, t);
+        group_merge<LPQ>(t);
+        bool covers;
+        const float b = outside_bound(g, cx, cy, cz, r, qx, qy, qz, covers);
+        const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+        done = covers || (t.k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
+      }
+    }
+#endif
+    // Nearest_Points / pointSearchSqDis for this point
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (j % LPQ == sub) {
+        const uint64_t mk = t.k[j];
+        out.nbr_idx[i * 5 + j] = (mk == kInfKey) ? -1 : (int32_t)(uint32_t)mk;
+        out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+                                                 : __uint_as_float((uint32_t)(mk >> 32));
+        nb_pos[slot][j] = t.p[j];
+      }
+    }
+    if (sub == 0) {
+      // kNN gate (esekfom.hpp:144-147): 5 neighbours and d5 <= 5
+      const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+      nb_d5[slot] = (t.k[4] != kInfKey) ? d5 : __int_as_float(0x7f800000);
+      qw[slot] = make_float4(qx, qy, qz, 0.0f);
+    }
+  }
+  if ((tid >> 6) < 4) STAMP(4 + (tid >> 6));  // per-wave end of the kNN phase
+  __syncthreads();
+  if (tid == 0) STAMP(1);
+
+  // ---------------- phase 2: plane fit, residual gate, Jacobian row
+  if (tid < SLIO_CHUNK) {
+    const int slot = tid;
     const int64_t i = chunk * SLIO_CHUNK + slot;
     double row[kRow];
 #pragma unroll
     for (int j = 0; j < kRow; ++j) row[j] = 0.0;
     if (i < scan.n) {
-      const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
-      float qx, qy, qz;
-      body_to_world(pose, bx, by, bz, qx, qy, qz);
-
-      uint64_t k[5];
-      uint32_t p[5];
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        k[j] = kInfKey;
-        p[j] = 0;
-      }
-      const bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0;
-      if (finite) {
-        const int cx = cell_coord(qx, g.ox, g.inv_h);
-        const int cy = cell_coord(qy, g.oy, g.inv_h);
-        const int cz = cell_coord(qz, g.oz, g.inv_h);
-        const int ex = max(max(-cx, cx - (g.dx - 1)), 0);
-        const int ey = max(max(-cy, cy - (g.dy - 1)), 0);
-        const int ez = max(max(-cz, cz - (g.dz - 1)), 0);
-        int r = max(1, max(ex, max(ey, ez)));
-        int rin = -1;
-        if (r == 1) {
-          // fast path: 3x3x3 block = 9 x-runs; issue the 18 run bounds first
-          uint32_t rs[9], rl[9];
-          const int xlo = max(cx - 1, 0), xhi = min(cx + 1, g.dx - 1);
-#pragma unroll
-          for (int q = 0; q < 9; ++q) {
-            const int yy = cy - 1 + (q % 3), zz = cz - 1 + (q / 3);
-            const bool ok = yy >= 0 && yy < g.dy && zz >= 0 && zz < g.dz && xlo <= xhi;
-            const uint32_t rb = ok ? ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx : 0u;
-            const uint32_t s = ok ? start[rb + xlo] : 0u;
-            const uint32_t e = ok ? start[rb + xhi + 1] : 0u;
-            rs[q] = s;
-            rl[q] = e - s;
-          }
-          uint32_t pre[10];
-          pre[0] = 0;
-#pragma unroll
-          for (int q = 0; q < 9; ++q) pre[q + 1] = pre[q] + rl[q];
-          const uint32_t T = pre[9];
-          for (uint32_t t0 = sub; t0 < T; t0 += 2 * kLPQ) {
-            const uint32_t t1 = t0 + kLPQ;
-            uint32_t a0 = 0, a1 = 0;
-#pragma unroll
-            for (int q = 0; q < 9; ++q) {
-              if (t0 >= pre[q]) a0 = rs[q] + (t0 - pre[q]);
-              if (t1 >= pre[q]) a1 = rs[q] + (t1 - pre[q]);
-            }
-            const float4 c0 = pts[a0];
-            float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (t1 < T) c1 = pts[a1];
-            consider(c0, a0, qx, qy, qz, k, p);
-            if (t1 < T) consider(c1, a1, qx, qy, qz, k, p);
-          }
-          group_merge(k, p);
-          rin = 1;
-          r = 2;
-          bool covers;
-          const float b = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
-          const float d5 = __uint_as_float((uint32_t)(k[4] >> 32));
-          const bool done = covers || (k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
-          if (!done && sub != 0) {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) k[j] = kInfKey;
-          }
-          if (done) r = -1;
-        }
-        // general rings (rare): expand until the 5th distance is provably final
-        while (r > 0) {
-          scan_region(pts, start, g, cx, cy, cz, r, rin, sub, qx, qy, qz, k, p);
-          group_merge(k, p);
-          bool covers;
-          const float b = outside_bound(g, cx, cy, cz, r, qx, qy, qz, covers);
-          const float d5 = __uint_as_float((uint32_t)(k[4] >> 32));
-          const bool done = covers || (k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
-          if (done) break;
-          if (sub != 0) {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) k[j] = kInfKey;
-          }
-          rin = r;
-          ++r;
-        }
-      }
-
-      // Nearest_Points / pointSearchSqDis for this point
-      if (sub < 5) {
-        uint64_t mk = k[0];
-#pragma unroll
-        for (int j = 1; j < 5; ++j) mk = (sub == j) ? k[j] : mk;
-        out.nbr_idx[i * 5 + sub] = (mk == kInfKey) ? -1 : (int32_t)(uint32_t)mk;
-        out.nbr_sqd[i * 5 + sub] =
-            (mk == kInfKey) ? __int_as_float(0x7f800000) : __uint_as_float((uint32_t)(mk >> 32));
-      }
-      // kNN gate (esekfom.hpp:144-147)
-      const float d5 = __uint_as_float((uint32_t)(k[4] >> 32));
-      bool sel = (k[4] != kInfKey) && !(d5 > cfg.max_sqd);
+      const float d5 = nb_d5[slot];
+      bool sel = !(d5 > cfg.max_sqd);   // +inf when fewer than 5 map points
       float abcd[4] = {__int_as_float(0x7fc00000), __int_as_float(0x7fc00000),
                        __int_as_float(0x7fc00000), __int_as_float(0x7fc00000)};
       float pd2 = __int_as_float(0x7fc00000);
+      const float4 q = qw[slot];
+      const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
       if (sel) {
         float nb[5][3];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-          const float4 c = pts[p[j]];
+          const float4 c = pts[nb_pos[slot][j]];
           nb[j][0] = c.x;
           nb[j][1] = c.y;
           nb[j][2] = c.z;
         }
         float pl[4];
+#ifdef SLIO_ABL_NOFIT
+        pl[0] = nb[0][0]; pl[1] = nb[1][1]; pl[2] = nb[2][2]; pl[3] = nb[3][0] + nb[4][1];
+        sel = true;
+#else
         sel = esti_plane_dev(nb, cfg.plane_thr, pl);
+#endif
         if (sel) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) abcd[j] = pl[j];
-          sel = residual_gate(abcd, qx, qy, qz, bx, by, bz, pd2);
+          sel = residual_gate(abcd, q.x, q.y, q.z, bx, by, bz, pd2);
         }
       }
-      if (sub == 0) {
-        out.plane[i] = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
-        out.sel[i] = sel ? 1 : 0;
-        out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
-      }
+      out.plane[i] = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
+      out.sel[i] = sel ? 1 : 0;
+      out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
       if (sel) {
         double h[12];
         jacobian_row(pose, bx, by, bz, abcd[0], abcd[1], abcd[2], cfg.extrinsic != 0, h);
@@ -535,13 +843,18 @@ __global__ __launch_bounds__(kBlock) void k_search_pass(const MapView map, const
         row[13] = 1.0;
       }
     }
-    // lanes of the group write the row cooperatively
 #pragma unroll
-    for (int j = 0; j < kRow; ++j)
-      if ((j & (kLPQ - 1)) == sub) rows[slot][j] = row[j];
+    for (int j = 0; j < kRow; ++j) rows[slot][j] = row[j];
   }
   __syncthreads();
-  chunk_products<kBlock>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
+  if (tid == 0) STAMP(2);
+  // ---------------- phase 3: fixed-order products
+#ifdef SLIO_ABL_NOPROD
+  if (tid < SLIO_NPROD) out.chunk_part[chunk * SLIO_NPROD + tid] = rows[tid][0];
+#else
+  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
+#endif
+  if (tid == 0) STAMP(3);
 }
 
 // Non-search pass: reuse neighbours/plane/selection (esekfom.hpp:138-150 with
@@ -584,20 +897,31 @@ __global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan, c
   chunk_products<SLIO_CHUNK>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
 }
 
-// super-chunk sums in fixed chunk order; rows of super-chunks this rank does
-// not own are written as zeros.
-__global__ __launch_bounds__(128) void k_super_sums(const double* __restrict__ chunk_part,
-                                                    int64_t C, int s_begin, int s_end,
-                                                    double* __restrict__ super_out) {
+// super-chunk sums in a fixed order: segment g of the 8 sums chunks
+// c0+g, c0+g+8, ... sequentially, then the 8 segment sums are added in order.
+// Rows of super-chunks this rank does not own are written as zeros.
+constexpr int kSuperSeg = 8;
+__global__ __launch_bounds__(SLIO_NPROD * kSuperSeg) void k_super_sums(
+    const double* __restrict__ chunk_part, int64_t C, int s_begin, int s_end,
+    double* __restrict__ super_out) {
+  __shared__ double part[kSuperSeg][SLIO_NPROD];
   const int s = blockIdx.x;
   const int t = threadIdx.x;
-  if (t >= SLIO_NPROD) return;
+  const int seg = t / SLIO_NPROD, kk = t % SLIO_NPROD;
   double acc = 0.0;
   if (s >= s_begin && s < s_end) {
     const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
-    for (int64_t c = c0; c < c1; ++c) acc = acc + chunk_part[c * SLIO_NPROD + t];
+#pragma unroll 4
+    for (int64_t c = c0 + seg; c < c1; c += kSuperSeg) acc = acc + chunk_part[c * SLIO_NPROD + kk];
   }
-  super_out[s * SLIO_NPROD + t] = acc;
+  part[seg][kk] = acc;
+  __syncthreads();
+  if (t < SLIO_NPROD) {
+    double v = part[0][t];
+#pragma unroll
+    for (int q = 1; q < kSuperSeg; ++q) v = v + part[q][t];
+    super_out[s * SLIO_NPROD + t] = v;
+  }
 }
 
 // ---------------------------------------------------------------- context
@@ -741,6 +1065,15 @@ void* internal_stream(slio_handle h) { return h ? (void*)h->c.stream : nullptr; 
 
 extern "C" {
 
+#ifdef SLIO_ABL_STAMP
+int slio_debug_stamps(unsigned long long* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * nblocks) ==
+                 hipSuccess
+             ? 0
+             : -3;
+}
+#endif
+
 const char* slio_last_error(void) { return g_err.c_str(); }
 
 int slio_params_default(slio_params* p) {
@@ -750,7 +1083,8 @@ int slio_params_default(slio_params* p) {
   p->max_points = 100000;
   p->rank = 0;
   p->nranks = 1;
-  p->grid_cell = 1.0f;
+  p->grid_cell = 1.25f;      // tuned on MI355X for 0.5 m map resolution
+  p->search_radius = 0.0f;   // 3x3x3 block first (tuned); > 0 selects the sphere search
   p->plane_threshold = 0.1f;
   p->max_match_sqd = 5.0f;
   p->max_grid_cells = (int64_t)1 << 29;
@@ -781,6 +1115,10 @@ int slio_create(slio_handle* out, const slio_params* p) {
   h->c.prm = *p;
   if (h->c.prm.grid_cell <= 0.0f) h->c.prm.grid_cell = 1.0f;
   if (h->c.prm.max_grid_cells <= 0) h->c.prm.max_grid_cells = (int64_t)1 << 29;
+  {
+    const int l = h->c.prm.lanes_per_query;
+    if (l != 1 && l != 2 && l != 4 && l != 8) h->c.prm.lanes_per_query = kDefaultLPQ;
+  }
   if (hipStreamCreateWithFlags(&h->c.own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     set_error("slio_create: hipStreamCreate failed");
@@ -1055,6 +1393,11 @@ int slio_iterate_async(slio_handle h, const slio_pose* x, int do_search, int ext
   PassCfg cfg;
   cfg.plane_thr = c.prm.plane_threshold;
   cfg.max_sqd = c.prm.max_match_sqd;
+  {
+    // the first sphere must sit inside the 5x5x5 cube: rho0 < 2h
+    const float rho = std::min(c.prm.search_radius, 1.99f * c.map->g.h);
+    cfg.radius_sq = rho > 0.0f ? rho * rho : 0.0f;
+  }
   cfg.extrinsic = extrinsic_est ? 1 : 0;
   cfg.c_begin = c0;
   cfg.c_end = c1;
@@ -1072,7 +1415,22 @@ int slio_iterate_async(slio_handle h, const slio_pose* x, int do_search, int ext
     }
     if (do_search) {
       const MapView mv{c.map->g, c.map->n, c.map->pts, c.map->start};
-      k_search_pass<<<(unsigned)nblk, kBlock, 0, c.stream>>>(mv, s, P, cfg, o);
+      const bool sph = cfg.radius_sq > 0.0f;
+      const unsigned nb = (unsigned)nblk;
+      switch (c.prm.lanes_per_query) {
+        case 1: sph ? k_search_pass<1, 4, true><<<nb, search_block<1>(), 0, c.stream>>>(mv, s, P, cfg, o)
+                    : k_search_pass<1, 4, false><<<nb, search_block<1>(), 0, c.stream>>>(mv, s, P, cfg, o);
+          break;
+        case 4: sph ? k_search_pass<4, 4, true><<<nb, search_block<4>(), 0, c.stream>>>(mv, s, P, cfg, o)
+                    : k_search_pass<4, 4, false><<<nb, search_block<4>(), 0, c.stream>>>(mv, s, P, cfg, o);
+          break;
+        case 8: sph ? k_search_pass<8, 4, true><<<nb, search_block<8>(), 0, c.stream>>>(mv, s, P, cfg, o)
+                    : k_search_pass<8, 4, false><<<nb, search_block<8>(), 0, c.stream>>>(mv, s, P, cfg, o);
+          break;
+        default: sph ? k_search_pass<2, 4, true><<<nb, search_block<2>(), 0, c.stream>>>(mv, s, P, cfg, o)
+                     : k_search_pass<2, 4, false><<<nb, search_block<2>(), 0, c.stream>>>(mv, s, P, cfg, o);
+          break;
+      }
     } else {
       k_reuse_pass<<<(unsigned)nblk, SLIO_CHUNK, 0, c.stream>>>(s, P, cfg, o);
     }
@@ -1087,7 +1445,7 @@ int slio_iterate_async(slio_handle h, const slio_pose* x, int do_search, int ext
     ev2 = prof_pair(c);
     (void)hipEventRecord(ev2.first, c.stream);
   }
-  k_super_sums<<<SLIO_NSUPER, 128, 0, c.stream>>>(c.chunk_part, C, c.prm.rank * per,
+  k_super_sums<<<SLIO_NSUPER, SLIO_NPROD * kSuperSeg, 0, c.stream>>>(c.chunk_part, C, c.prm.rank * per,
                                                    (c.prm.rank + 1) * per, c.d_super);
   if (c.prof) {
     (void)hipEventRecord(ev2.second, c.stream);

@@ -73,8 +73,10 @@ slio_pose pose_of(const slio_state& x) {
 }
 
 // One filter update from the pass sums; returns the 24x24 KH in KH and
-// updates x.  Follows esekfom.hpp:303-321.
-bool filter_step(const slio_state& x_prop, const double* P, double R, const double HTH[78],
+// updates x.  Follows esekfom.hpp:303-321.  Pinv = P_.inverse(): P_ does not
+// change inside the iteration loop, so the caller inverts it once per update
+// (the reference re-inverts the same matrix every pass, esekfom.hpp:311).
+bool filter_step(const slio_state& x_prop, const double* Pinv, double R, const double HTH[78],
                  const double HTh[12], slio_state& x, double KH[576], double dx[24]) {
   double dx_new[24];
   boxminus(x, x_prop, dx_new);
@@ -86,8 +88,6 @@ bool filter_step(const slio_state& x_prop, const double* P, double R, const doub
       H12[j * 12 + i] = HTH[k];
       ++k;
     }
-  double Pinv[576];
-  if (!invert<24>(P, Pinv)) return false;
   double A[576];
   for (int i = 0; i < 24; ++i)
     for (int j = 0; j < 24; ++j) {
@@ -154,6 +154,11 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
   double sup[SLIO_NSUPER * SLIO_NPROD];
   const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
   double dev_ms = 0.0;
+  double Pinv[576];
+  if (!invert<24>(P, Pinv)) {
+    set_error("slio_ikf_update: singular covariance");
+    return SLIO_EINVAL;
+  }
   for (int i = first; i < maximum_iter; ++i) {
     const bool search = (mode == SLIO_MODE_FIXED) ? true : converge;
     const slio_pose pose = pose_of(*x);
@@ -181,7 +186,7 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
       continue;
     }
     ++st.valid_passes;
-    if (!filter_step(x_prop, P, R, HTH, HTh, *x, KH, dx)) {
+    if (!filter_step(x_prop, Pinv, R, HTH, HTh, *x, KH, dx)) {
       set_error("slio_ikf_update: singular covariance");
       return SLIO_EINVAL;
     }

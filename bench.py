@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--map-points", type=int, default=10_000_000)
     ap.add_argument("--scan-points", type=int, default=100_000)
-    ap.add_argument("--cell", type=float, default=1.0)
+    ap.add_argument("--cell", type=float, default=1.25)
     ap.add_argument("--cpu-scans", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -60,11 +60,18 @@ typedef struct slio_params {
                               (esekfom.hpp:23-29)                             */
   int32_t rank;            /* this handle's shard of the scan points          */
   int32_t nranks;          /* 1, 2, 4 or 8 (must divide SLIO_NSUPER)          */
-  float grid_cell;         /* map hash-grid cell edge in metres (0 -> 1.0)    */
+  float grid_cell;         /* map grid cell edge in metres (default 1.25)     */
   float plane_threshold;   /* esti_plane threshold, 0.1f (esekfom.hpp:157)    */
   float max_match_sqd;     /* 5th-NN sq.-distance gate, 5 (esekfom.hpp:147)   */
-  int32_t reserved;
+  int32_t lanes_per_query; /* search lanes per scan point: 1, 2, 4, 8 (0 ->
+                              tuned default)                                  */
   int64_t max_grid_cells;  /* dense cell-table budget (0 -> 1<<29)            */
+  float search_radius;     /* first search sphere radius in metres (default 0:
+                              scan the 3x3x3 cell block first); capped at 1.99
+                              cells.
+                              Any value gives the exact 5-NN; it only tunes
+                              speed.                                           */
+  int32_t reserved;
 } slio_params;
 
 /* Pose slice of state_ikfom used by the measurement model

@@ -1,0 +1,22 @@
+# usage: bash scripts/gpu_round.sh <tag> [tests] [sweep] [bench] [prof]
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+tag=$1; shift
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${tag}_tests.log 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/${tag}_tests.log
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+    sweep)
+      timeout -k 10 600 python scripts/sweep_search.py > gpurun_out/${tag}_sweep.log 2>&1 || { echo "sweep failed"; tail -20 gpurun_out/${tag}_sweep.log; exit 3; }
+      cat gpurun_out/${tag}_sweep.log | grep -v amdgpu.ids ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 4; }
+      cat gpurun_out/${tag}_bench.json ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 5; }
+      find gpurun_out/${tag}_prof -name "*stats*" | head; for f in $(find gpurun_out/${tag}_prof -name "*kernel_stats.csv"); do head -8 $f; done ;;
+  esac
+done

@@ -1,0 +1,54 @@
+"""Drive the C2 search pass REPS times (for rocprofv3 PMC / ablation runs).
+Env: SLIO_LIB (library path), LPQ, CELL, REPS."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
+
+
+def main():
+    lib = L.load(os.environ.get("SLIO_LIB", L.LIB_PATH))
+    lpq = int(os.environ.get("LPQ", "2"))
+    cell = float(os.environ.get("CELL", "1.0"))
+    reps = int(os.environ.get("REPS", "20"))
+    mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
+    nscan = int(os.environ.get("NSCAN", "100000"))
+    fr.body = np.ascontiguousarray(fr.body[:nscan])
+    st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI])
+    pose = L.SlioPose()
+    pose.pos[:] = list(st[0:3]); pose.rot[:] = list(st[3:7])
+    pose.rli[:] = list(st[7:11]); pose.tli[:] = list(st[11:14])
+    p = L.SlioParams()
+    lib.slio_params_default(C.byref(p))
+    p.grid_cell, p.lanes_per_query = cell, lpq
+    p.search_radius = float(os.environ.get("RADIUS", "1.0"))
+    h = C.c_void_p()
+    L.check(lib.slio_create(C.byref(h), C.byref(p)), "create")
+    x, y, z = (np.ascontiguousarray(mp[:, k]) for k in range(3))
+    L.check(lib.slio_map_upload(h, L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")
+    bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
+    L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]), "scan")
+    HTH = np.zeros(78); HTh = np.zeros(12); m = C.c_int64()
+    for _ in range(3):
+        L.check(lib.slio_iterate(h, C.byref(pose), 1, 0, L.dptr(HTH), L.dptr(HTh), C.byref(m)), "it")
+    lib.slio_profile(h, 1)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        L.check(lib.slio_iterate(h, C.byref(pose), 1, 0, L.dptr(HTH), L.dptr(HTh), C.byref(m)), "it")
+    el = (time.perf_counter() - t0) / reps
+    ms = C.c_double(); n = C.c_int64()
+    lib.slio_profile_read(h, 0, C.byref(ms), C.byref(n))
+    print(json.dumps({"lib": os.path.basename(os.environ.get("SLIO_LIB", "libslio.so")), "lpq": lpq,
+                      "cell": cell, "radius": p.search_radius, "nscan": nscan, "search_us": ms.value / n.value * 1e3,
+                      "iter_wall_us": el * 1e6, "m": m.value}), flush=True)
+    lib.slio_destroy(h)
+
+
+if __name__ == "__main__":
+    main()

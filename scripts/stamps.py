@@ -1,0 +1,42 @@
+"""Per-block phase timing from the SLIO_ABL_STAMP diagnostic build."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
+
+lib = L.load(os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so"))
+lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
+    for nscan in [25000, 100000]:
+        mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
+        body = np.ascontiguousarray(fr.body[:nscan])
+        st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI])
+        pose = L.SlioPose()
+        pose.pos[:] = list(st[0:3]); pose.rot[:] = list(st[3:7])
+        pose.rli[:] = list(st[7:11]); pose.tli[:] = list(st[11:14])
+        p = L.SlioParams(); lib.slio_params_default(C.byref(p)); p.grid_cell = 1.25; p.lanes_per_query = lpq
+        h = C.c_void_p(); L.check(lib.slio_create(C.byref(h), C.byref(p)), "create")
+        x, y, z = (np.ascontiguousarray(mp[:, k]) for k in range(3))
+        L.check(lib.slio_map_upload(h, L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")
+        bx, by, bz = (np.ascontiguousarray(body[:, k]) for k in range(3))
+        L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), body.shape[0]), "scan")
+        HTH = np.zeros(78); HTh = np.zeros(12); m = C.c_int64()
+        for _ in range(5):
+            L.check(lib.slio_iterate(h, C.byref(pose), 1, 0, L.dptr(HTH), L.dptr(HTh), C.byref(m)), "it")
+        nb = (nscan + 127) // 128
+        buf = (C.c_ulonglong * (8 * nb))()
+        assert lib.slio_debug_stamps(buf, nb) == 0
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
+        t0 = a[:, 0].min()
+        us = (a - t0) / 100.0   # 100 MHz -> us
+        ph1 = us[:, 1] - us[:, 0]; ph2 = us[:, 2] - us[:, 1]; ph3 = us[:, 3] - us[:, 2]
+        wv = us[:, 4:8] - us[:, [0]]
+        print(f"lpq={lpq} n={nscan} blocks={nb}: kernel span {us[:, 3].max():.1f}us; start spread {us[:, 0].max():.1f}us")
+        for name, v in (("knn", ph1), ("fit", ph2), ("prod", ph3)):
+            print(f"  {name}: mean {v.mean():.2f} p50 {np.median(v):.2f} p90 {np.quantile(v, .9):.2f} max {v.max():.2f} us")
+        print(f"  wave kNN end: mean {wv.mean():.2f} max {wv.max():.2f}; per-block max-min wave {np.mean(wv.max(1) - wv.min(1)):.2f} us")
+        lib.slio_destroy(h)

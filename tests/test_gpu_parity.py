@@ -25,11 +25,14 @@ def L():
     return _lib
 
 
-def mk(L, n_max=100000, rank=0, nranks=1, cell=1.0, max_cells=0):
+def mk(L, n_max=100000, rank=0, nranks=1, cell=0.75, max_cells=0, radius=None, lpq=0):
     lib = L.load()
     p = L.SlioParams()
     lib.slio_params_default(C.byref(p))
     p.max_points, p.rank, p.nranks, p.grid_cell = n_max, rank, nranks, cell
+    if radius is not None:
+        p.search_radius = radius
+    p.lanes_per_query = lpq
     if max_cells:
         p.max_grid_cells = max_cells
     h = C.c_void_p()
@@ -122,14 +125,18 @@ def test_knn_golden_bitexact(L):
         L.load().slio_destroy(h)
 
 
-@pytest.mark.parametrize("cell,max_cells", [(0.37, 0), (1.0, 0), (2.5, 0), (1.0, 4096)])
-def test_knn_grid_geometry_invariant(L, oracle_mod, c1, cell, max_cells):
-    """Exactness must not depend on the cell edge or the cell-budget fallback."""
+@pytest.mark.parametrize("cell,max_cells,radius,lpq", [
+    (0.37, 0, None, 0), (1.0, 0, None, 0), (2.5, 0, None, 0), (1.0, 4096, None, 0),
+    (0.75, 0, 0.0, 0), (0.75, 0, 0.3, 0), (0.75, 0, 1.49, 0), (1.25, 0, 0.0, 2),
+    (0.75, 0, 1.0, 1), (0.75, 0, 1.0, 4), (0.75, 0, 1.0, 8)])
+def test_knn_grid_geometry_invariant(L, oracle_mod, c1, cell, max_cells, radius, lpq):
+    """Exactness must not depend on the cell edge, the cell-budget fallback,
+    the first-sphere radius or the lanes per query."""
     mp, fr, T = c1["avia"]
     st = state_of(fr)
     q = oracle_mod.body_to_world(st, fr.body)
     ridx, rsqd = T.knn(q, 5)
-    h = mk(L, cell=cell, max_cells=max_cells)
+    h = mk(L, cell=cell, max_cells=max_cells, radius=radius, lpq=lpq)
     try:
         upload_map(L, h, mp)
         upload_scan(L, h, fr.body)
