@@ -23,6 +23,7 @@ SLIO_MODE_FIXED = 1
 SLIO_KERNEL_SEARCH = 0
 SLIO_KERNEL_REUSE = 1
 SLIO_KERNEL_SUPER = 2
+SLIO_PROFILE_KEEP = 16
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ECAPACITY", -5: "ESTATE"}
 
@@ -39,7 +40,7 @@ class SlioParams(C.Structure):
         ("lanes_per_query", C.c_int32),
         ("max_grid_cells", C.c_int64),
         ("search_radius", C.c_float),
-        ("reserved", C.c_int32),
+        ("far_query_margin", C.c_float),
     ]
 
 
@@ -108,6 +109,11 @@ SIGNATURES = {
     "slio_profile": (C.c_int, [_P, C.c_int]),
     "slio_profile_read": (C.c_int, [_P, C.c_int, _DP, _I64P]),
     "slio_ikf_update": (
+        C.c_int,
+        [_P, C.POINTER(SlioState), _DP, C.c_double, C.c_int, C.c_int, C.c_int, ALLREDUCE_FN, _P,
+         C.POINTER(SlioIkfStats)],
+    ),
+    "slio_ikf_update_device": (
         C.c_int,
         [_P, C.POINTER(SlioState), _DP, C.c_double, C.c_int, C.c_int, C.c_int, ALLREDUCE_FN, _P,
          C.POINTER(SlioIkfStats)],

@@ -57,4 +57,18 @@ inline void rank_chunks(int64_t n, int rank, int nranks, int64_t* c0, int64_t* c
   *c1 = super_lo(C, (rank + 1) * per);
 }
 
+// Device-resident IKF control block (slio_ikf_update_device): the filter
+// state, covariance and the esekfom.hpp:292-345 control flags live in HBM so
+// a whole update runs without host round trips.
+struct IkfCtl {
+  slio_state x;      // x_ (current iterate)
+  slio_state xprop;  // x_propagated
+  double P[576];     // P_ (row-major)
+  double KH[576];    // K * H of the last valid pass
+  int32_t converge, t, done, search_now;
+  int32_t passes, searches, valid_passes, mode;
+  int64_t last_m;
+  int32_t singular, pad;
+};
+
 }  // namespace slio

@@ -14,12 +14,14 @@
 //     so 1/2/4/8 GPUs give bitwise-identical sums.
 // Built with -ffp-contract=off: every float/double expression is evaluated
 // exactly as written (the reference's x86-64 build has no FMA either).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -27,6 +29,21 @@
 
 #include "slio_common.hpp"
 #include "slio_plane.hpp"
+#include "slio_so3.hpp"
+
+// -DSLIO_SOLVE_STAMP: wall-clock stamps of the filter-step phases (diagnostic
+// builds only; read with slio_dbg_solve_stamps).
+#ifdef SLIO_SOLVE_STAMP
+__device__ unsigned long long g_sstamp[32];
+#define SSTAMP(k)                                     \
+  do {                                                \
+    if (threadIdx.x == 0) g_sstamp[k] = wall_clock64(); \
+  } while (0)
+#else
+#define SSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
 
 namespace slio {
 
@@ -132,6 +149,23 @@ struct PoseDev {
   double R[9];                          // rot.matrix(), row-major
   double RL[9];                         // offset_R_L_I.matrix(), row-major
 };
+
+__device__ __forceinline__ PoseDev pose_from_state(const slio_state& x) {
+  PoseDev P;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    P.rq[j] = x.rot[j];
+    P.lq[j] = x.rli[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    P.pos[j] = x.pos[j];
+    P.tli[j] = x.tli[j];
+  }
+  qmatrix(Quat{x.rot[0], x.rot[1], x.rot[2], x.rot[3]}, P.R);
+  qmatrix(Quat{x.rli[0], x.rli[1], x.rli[2], x.rli[3]}, P.RL);
+  return P;
+}
 
 // Sophus::SO3::operator*(Vector3d) = Eigen QuaternionBase::_transformVector:
 // uv = q.vec() x v; uv += uv; return v + q.w() * uv + q.vec() x uv;
@@ -581,12 +615,26 @@ struct PassOut {
   double* chunk_part;  // C * NPROD (global chunk index)
 };
 
+// far_query_margin: squared distance from the query to the grid's bounding box
+__device__ __forceinline__ bool far_outside(const GridGeom& g, float far_sq, float qx, float qy,
+                                            float qz) {
+  if (far_sq <= 0.0f) return false;
+  const float gx = fmaxf(fmaxf(g.ox - qx, qx - (g.ox + g.h * (float)g.dx)), 0.0f);
+  const float gy = fmaxf(fmaxf(g.oy - qy, qy - (g.oy + g.h * (float)g.dy)), 0.0f);
+  const float gz = fmaxf(fmaxf(g.oz - qz, qz - (g.oz + g.h * (float)g.dz)), 0.0f);
+  return gx * gx + gy * gy + gz * gz > far_sq;
+}
+
 struct PassCfg {
+  const IkfCtl* ctl;  // device-resident update: pose + pass selection from HBM (else null)
+  int want_search;    // with ctl: run only if ctl->search_now == want_search
   float plane_thr;
   float max_sqd;
   float radius_sq;  // sphere-first search radius^2 (0: 3x3x3 block first)
+  float far_sq;     // far_query_margin^2 (0: no cut)
   int extrinsic;
   int64_t c_begin, c_end;  // global chunk range of this rank
+  int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
 };
 
 __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
@@ -595,6 +643,293 @@ __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
   const int64_t xcd = b & 7, q = nblk >> 3, rr = nblk & 7;
   const int64_t base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
   return c_begin + base + (b >> 3);
+}
+
+// ---------------------------------------------------------------- filter step
+constexpr int kSolveThreads = 256;
+constexpr int kSuperSeg = 8;
+
+// LDS of the filter step.
+struct SolveLds {
+  double tot[SLIO_NPROD];
+  double M[144];
+  double K12[288];
+  double a[12][25];
+  double dxn[24], dx[24], Kh[24], f[12];
+  double KH[576];
+  double P[576];
+  double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums of this pass
+  slio_state x, xprop;                  // staged IkfCtl fields (one parallel sweep
+  int32_t fl[8];                        // in, one out: no serial HBM round trips)
+  int piv, s_final;
+};
+static_assert(offsetof(IkfCtl, xprop) == sizeof(slio_state), "IkfCtl: x, xprop adjacent");
+static_assert(offsetof(SolveLds, xprop) - offsetof(SolveLds, x) == sizeof(slio_state),
+              "SolveLds: x, xprop adjacent");
+static_assert(offsetof(IkfCtl, mode) - offsetof(IkfCtl, converge) == 7 * sizeof(int32_t),
+              "IkfCtl: 8 contiguous flags");
+constexpr int kStateD = sizeof(slio_state) / sizeof(double);
+// flag slots of IkfCtl::converge..mode
+enum { F_CONV, F_T, F_DONE, F_SEARCH, F_PASSES, F_SEARCHES, F_VALID, F_MODE };
+
+// Gauss-Jordan with partial pivoting on the 12 x 24 augmented [B | I], by
+// the first wavefront: lane j < 24 holds column j in registers and the
+// pivot row / factors are broadcast with readlane -- no workgroup barriers.
+// Operation order is exactly the host invert<12>'s (first maximum |a[r][c]|
+// as pivot, row c scaled by 1/pivot, every other row r with f = a[r][c] != 0
+// updated a[r][j] -= f * a[c][j]), so the inverse is bitwise the host's.
+// Returns (to all lanes of wave 0) false on an exactly singular pivot.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ bool gj12_wave(SolveLds& L) {
+  const int lane = threadIdx.x;  // wave 0 only
+  const bool col = lane < 24;
+  double v[12];
+#pragma unroll
+  for (int r = 0; r < 12; ++r) v[r] = col ? L.a[r][lane] : 0.0;
+#pragma unroll
+  for (int c = 0; c < 12; ++c) {
+    // pivot search in lane c's column (rows c..11, first maximum)
+    double best = fabs(v[c]);
+    int p = c;
+#pragma unroll
+    for (int r = c + 1; r < 12; ++r) {
+      const double a = fabs(v[r]);
+      if (a > best) {
+        best = a;
+        p = r;
+      }
+    }
+    p = __builtin_amdgcn_readlane(p, c);
+    best = readlane_d(best, c);
+    if (best == 0.0) return false;
+    // swap rows c and p
+    double vp = v[c];
+#pragma unroll
+    for (int r = c + 1; r < 12; ++r) vp = (r == p) ? v[r] : vp;
+#pragma unroll
+    for (int r = c + 1; r < 12; ++r) v[r] = (r == p) ? v[c] : v[r];
+    v[c] = vp;
+    // scale row c by 1 / pivot
+    const double inv = 1.0 / readlane_d(v[c], c);
+    v[c] *= inv;
+    // eliminate column c from every other row
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+      if (r == c) continue;
+      const double f = readlane_d(v[r], c);
+      if (f != 0.0) v[r] -= f * v[c];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 12; ++r)
+    if (col) L.a[r][lane] = v[r];
+  return true;
+}
+
+// x1 [-] x2 (esekfom.hpp:236-258) by two lanes: part 0 = the vector blocks
+// and the rotation, part 1 = the R_LI rotation.
+__device__ void state_boxminus_part(const slio_state& x1, const slio_state& x2, double d[24],
+                                    int part) {
+  if (part == 0) {
+    for (int i = 0; i < 3; ++i) {
+      d[i] = x1.pos[i] - x2.pos[i];
+      d[9 + i] = x1.tli[i] - x2.tli[i];
+      d[12 + i] = x1.vel[i] - x2.vel[i];
+      d[15 + i] = x1.bg[i] - x2.bg[i];
+      d[18 + i] = x1.ba[i] - x2.ba[i];
+      d[21 + i] = x1.grav[i] - x2.grav[i];
+    }
+    so3_boxminus(Quat{x1.rot[0], x1.rot[1], x1.rot[2], x1.rot[3]},
+                 Quat{x2.rot[0], x2.rot[1], x2.rot[2], x2.rot[3]}, d + 3);
+  } else {
+    so3_boxminus(Quat{x1.rli[0], x1.rli[1], x1.rli[2], x1.rli[3]},
+                 Quat{x2.rli[0], x2.rli[1], x2.rli[2], x2.rli[3]}, d + 6);
+  }
+}
+
+// x [+] f (esekfom.hpp:59-73) by two lanes: part 0 = vectors + rotation,
+// part 1 = R_LI.
+__device__ void state_boxplus_part(slio_state& x, const double f[24], int part) {
+  if (part == 0) {
+    for (int i = 0; i < 3; ++i) {
+      x.pos[i] = x.pos[i] + f[i];
+      x.tli[i] = x.tli[i] + f[9 + i];
+      x.vel[i] = x.vel[i] + f[12 + i];
+      x.bg[i] = x.bg[i] + f[15 + i];
+      x.ba[i] = x.ba[i] + f[18 + i];
+      x.grav[i] = x.grav[i] + f[21 + i];
+    }
+    const Quat r = qnormalized(qmul(Quat{x.rot[0], x.rot[1], x.rot[2], x.rot[3]}, so3_exp(f + 3)));
+    x.rot[0] = r.w; x.rot[1] = r.x; x.rot[2] = r.y; x.rot[3] = r.z;
+  } else {
+    const Quat l = qnormalized(qmul(Quat{x.rli[0], x.rli[1], x.rli[2], x.rli[3]}, so3_exp(f + 6)));
+    x.rli[0] = l.w; x.rli[1] = l.x; x.rli[2] = l.y; x.rli[3] = l.z;
+  }
+}
+
+// One filter step of update_iterated_dyn_share_modified on device by one
+// workgroup of NT threads, with the operation order of the host filter_step
+// (slio_ikf.cpp):
+//   M = H^T H / R, X = (I + M P[:12, :12])^-1  (12x12 Gauss-Jordan)
+//   K12 = P[:, :12] X  = K_front[:, :12] of esekfom.hpp:311 (push-through
+//   identity: (P^-1 + E^T M E)^-1 E^T = P E^T (I + M E P E^T)^-1)
+//   K h = K12 H^T h / R, K H = K12 M, dx = K h + (K H - I) dx_new,
+// then x [+] dx, the convergence logic of esekfom.hpp:323-344 and, on the
+// final pass, P = (I - K H) P.
+// L.sup holds the pass's super-chunk sums on entry (all threads of the
+// workgroup call this; ctl->done is uniform).
+template <int NT>
+__device__ void ikf_solve_block(IkfCtl* ctl, double R, int i, int maxit, SolveLds& L) {
+  static_assert(NT >= 128, "solve: one thread per sum");
+  const int t = threadIdx.x;
+  if (t < SLIO_NPROD) {
+    double v = L.sup[0][t];
+    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][t];
+    L.tot[t] = v;
+  }
+  {
+    const double* src = reinterpret_cast<const double*>(&ctl->x);
+    double* dst = reinterpret_cast<double*>(&L.x);
+    for (int e = t; e < 2 * kStateD; e += NT) dst[e] = src[e];
+  }
+  for (int e = t; e < 576; e += NT) L.P[e] = ctl->P[e];
+  if (t < 8) L.fl[t] = (&ctl->converge)[t];
+  __syncthreads();
+  SSTAMP(4);
+  const int64_t m = (int64_t)llround(L.tot[90]);
+  const bool valid = m >= 1;
+  if (valid) {
+    // the two parts on lanes of different wavefronts, so they run concurrently
+    if (t == NT - 1 || t == NT - 65) state_boxminus_part(L.x, L.xprop, L.dxn, t == NT - 1);
+    if (t < SLIO_NHTH) {
+      int ii = 0, kk = t;
+      while (kk >= 12 - ii) {
+        kk -= 12 - ii;
+        ++ii;
+      }
+      const int jj = ii + kk;
+      const double v = L.tot[t] / R;
+      L.M[ii * 12 + jj] = v;
+      L.M[jj * 12 + ii] = v;
+    }
+    __syncthreads();
+    for (int e = t; e < 288; e += NT) {
+      const int r = e / 24, j = e - r * 24;
+      if (j < 12) {
+        double s2 = 0.0;
+        for (int k = 0; k < 12; ++k) s2 += L.M[r * 12 + k] * L.P[k * 24 + j];
+        L.a[r][j] = (r == j ? 1.0 : 0.0) + s2;
+      } else {
+        L.a[r][j] = (j - 12 == r) ? 1.0 : 0.0;
+      }
+    }
+    __syncthreads();
+    SSTAMP(5);
+    if (t < 64) {
+      const bool ok = gj12_wave(L);
+      if (t == 0) L.piv = ok ? 1 : 0;
+    }
+    __syncthreads();
+    SSTAMP(6);
+    if (!L.piv) {
+      if (t == 0) {
+        ctl->singular = 1;
+        ctl->done = 1;
+      }
+      return;
+    }
+    for (int e = t; e < 288; e += NT) {
+      const int r = e / 12, cc = e - r * 12;
+      double s2 = 0.0;
+      for (int k = 0; k < 12; ++k) s2 += L.P[r * 24 + k] * L.a[k][12 + cc];
+      L.K12[e] = s2;
+    }
+    __syncthreads();
+    SSTAMP(7);
+    if (t < 24) {
+      double s2 = 0.0;
+      for (int j = 0; j < 12; ++j) s2 += L.K12[t * 12 + j] * L.tot[SLIO_NHTH + j];
+      L.Kh[t] = s2 / R;
+    }
+    for (int e = t; e < 576; e += NT) {
+      const int r = e / 24, cc = e - r * 24;
+      double v = 0.0;
+      if (cc < 12)
+        for (int j = 0; j < 12; ++j) v += L.K12[r * 12 + j] * L.M[j * 12 + cc];
+      L.KH[e] = v;
+      ctl->KH[e] = v;
+    }
+    __syncthreads();
+    if (t < 24) {
+      double s2 = 0.0;
+      for (int j = 0; j < 24; ++j) s2 += (L.KH[t * 24 + j] - (t == j ? 1.0 : 0.0)) * L.dxn[j];
+      L.dx[t] = L.Kh[t] + s2;
+    }
+    __syncthreads();
+    SSTAMP(8);
+  }
+  // any |dx| > epsi (esekfom.hpp:17, 325-331), wave 0 ballot
+  bool big = false;
+  if (t < 64) {
+    const bool b = valid && t < 24 && fabs(L.dx[t]) > 0.001;
+    big = __ballot(b) != 0;
+  }
+  if (t == 0) {
+    int32_t* f = L.fl;
+    f[F_PASSES] += 1;
+    f[F_SEARCHES] += f[F_SEARCH];
+    int fin = 0;
+    if (valid) {
+      f[F_VALID] += 1;
+      if (f[F_MODE] == SLIO_MODE_FIXED) {
+        fin = i == maxit - 1;
+        f[F_SEARCH] = 1;
+      } else {
+        const int conv = big ? 0 : 1;
+        f[F_CONV] = conv;
+        if (conv) f[F_T] += 1;
+        if (!f[F_T] && i == maxit - 2) f[F_CONV] = 1;
+        fin = (f[F_T] > 1 || i == maxit - 1);
+        f[F_SEARCH] = f[F_CONV];
+      }
+    } else if (i == maxit - 1) {
+      // reference: the loop ends without the P update; fixed mode applies
+      // the last valid pass's K H if there was one
+      fin = (f[F_MODE] == SLIO_MODE_FIXED && f[F_VALID] > 0);
+    }
+    if (fin || i == maxit - 1) f[F_DONE] = 1;
+    L.s_final = fin;
+    ctl->last_m = m;
+  }
+  __syncthreads();
+  SSTAMP(9);
+  const bool fin = L.s_final != 0;
+  if (fin && !valid)
+    for (int e = t; e < 576; e += NT) L.KH[e] = ctl->KH[e];  // last valid pass's K H
+  __syncthreads();
+  // x [+] dx on one lane, overlapped with P = (I - K H) P (esekfom.hpp:341-343)
+  if (valid && (t == NT - 1 || t == NT - 65)) state_boxplus_part(L.x, L.dx, t == NT - 1);
+  if (fin)
+    for (int e = t; e < 576; e += NT) {
+      const int r = e / 24, cc = e - r * 24;
+      double s2 = 0.0;
+      for (int q = 0; q < 24; ++q) s2 += ((r == q ? 1.0 : 0.0) - L.KH[r * 24 + q]) * L.P[q * 24 + cc];
+      ctl->P[e] = s2;
+    }
+  __syncthreads();
+  SSTAMP(10);
+  {
+    const double* src = reinterpret_cast<const double*>(&L.x);
+    double* dst = reinterpret_cast<double*>(&ctl->x);
+    for (int e = t; e < kStateD; e += NT) dst[e] = src[e];
+  }
+  if (t < 8) (&ctl->converge)[t] = L.fl[t];
+  SSTAMP(11);
 }
 
 // fixed-order product phase: rows[SLIO_CHUNK][kRow] in LDS -> chunk partial.
@@ -638,10 +973,15 @@ constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
 // LDS.  Phase 2 (fit): one lane per point reloads the 5 neighbours (L2-hot),
 // runs esti_plane, the residual gate and the Jacobian row, and writes the
 // row to LDS.  Phase 3: fixed-order fp64 products -> chunk partial.
-template <int LPQ, int U, bool SPHERE>
+template <int LPQ, int U, bool SPHERE, bool DEVPOSE>
 __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
-    const MapView map, const ScanDev scan, const PoseDev pose, const PassCfg cfg,
+    const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
     const PassOut out) {
+  // DEVPOSE: pose and pass selection come from the device-resident update
+  if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
+                  cfg.ctl->search_now != cfg.want_search))
+    return;
+  const PoseDev pose = DEVPOSE ? pose_from_state(cfg.ctl->x) : pose_arg;
   constexpr int NT = search_block<LPQ>();
   constexpr int QPP = NT / LPQ;               // queries per kNN pass
   constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
@@ -671,7 +1011,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     body_to_world(pose, bx, by, bz, qx, qy, qz);
     Top5 t;
     top5_clear(t);
-    const bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0;
+    const bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0 &&
+                        !far_outside(g, cfg.far_sq, qx, qy, qz);
 #if defined(SLIO_ABL_IO) || defined(SLIO_ABL_NOCAND)
     // diagnostic: synthetic neighbours (the first 5 map points), no search
 #pragma unroll
@@ -859,8 +1200,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
 
 // Non-search pass: reuse neighbours/plane/selection (esekfom.hpp:138-150 with
 // converge == false), one lane per point.
-__global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan, const PoseDev pose,
+template <bool DEVPOSE>
+__global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan,
+                                                           const PoseDev pose_arg,
                                                            const PassCfg cfg, const PassOut out) {
+  if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
+                  cfg.ctl->search_now != cfg.want_search))
+    return;
+  const PoseDev pose = DEVPOSE ? pose_from_state(cfg.ctl->x) : pose_arg;
   __shared__ double rows[SLIO_CHUNK][kRow];
   __shared__ double part[1][SLIO_NPROD];
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
@@ -900,14 +1247,21 @@ __global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan, c
 // super-chunk sums in a fixed order: segment g of the 8 sums chunks
 // c0+g, c0+g+8, ... sequentially, then the 8 segment sums are added in order.
 // Rows of super-chunks this rank does not own are written as zeros.
-constexpr int kSuperSeg = 8;
+// ctl != null (single-rank device-resident update): the last of the 8 blocks
+// to finish (threadfence reduction: agent-scope release + counter, acquire
+// in the last block) runs the filter step on the 8 rows, so a pass plus its
+// filter step is two launches.
 __global__ __launch_bounds__(SLIO_NPROD * kSuperSeg) void k_super_sums(
     const double* __restrict__ chunk_part, int64_t C, int s_begin, int s_end,
-    double* __restrict__ super_out) {
+    double* super_out, IkfCtl* ctl, uint32_t* count, double R, int iter, int maxit) {
+  constexpr int NT = SLIO_NPROD * kSuperSeg;
   __shared__ double part[kSuperSeg][SLIO_NPROD];
+  __shared__ SolveLds L;
+  __shared__ int last;
   const int s = blockIdx.x;
   const int t = threadIdx.x;
   const int seg = t / SLIO_NPROD, kk = t % SLIO_NPROD;
+  if (ctl) SSTAMP(0);
   double acc = 0.0;
   if (s >= s_begin && s < s_end) {
     const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
@@ -921,7 +1275,38 @@ __global__ __launch_bounds__(SLIO_NPROD * kSuperSeg) void k_super_sums(
 #pragma unroll
     for (int q = 1; q < kSuperSeg; ++q) v = v + part[q][t];
     super_out[s * SLIO_NPROD + t] = v;
+    L.sup[s][t] = v;
   }
+  if (!ctl) return;
+  SSTAMP(1);
+  __threadfence();
+  __syncthreads();
+  if (t == 0) last = atomicAdd(count, 1u) == (uint32_t)(SLIO_NSUPER - 1);
+  __syncthreads();
+  if (!last) return;
+  SSTAMP(2);
+  __threadfence();
+  if (t == 0) *count = 0;
+  for (int e = t; e < SLIO_NSUPER * SLIO_NPROD; e += NT) {
+    const int q = e / SLIO_NPROD;
+    if (q != s) L.sup[q][e - q * SLIO_NPROD] = super_out[e];
+  }
+  __syncthreads();
+  SSTAMP(3);
+  if (ctl->done) return;
+  ikf_solve_block<NT>(ctl, R, iter, maxit, L);
+}
+
+// ---------------------------------------------------------------- device IKF
+// Filter step after the multi-rank all-reduce: super sums from HBM.
+__global__ __launch_bounds__(kSolveThreads) void k_ikf_solve(IkfCtl* ctl, const double* sup,
+                                                             double R, int i, int maxit) {
+  __shared__ SolveLds L;
+  if (ctl->done) return;
+  for (int e = threadIdx.x; e < SLIO_NSUPER * SLIO_NPROD; e += kSolveThreads)
+    L.sup[e / SLIO_NPROD][e % SLIO_NPROD] = sup[e];
+  __syncthreads();
+  ikf_solve_block<kSolveThreads>(ctl, R, i, maxit, L);
 }
 
 // ---------------------------------------------------------------- context
@@ -943,10 +1328,15 @@ struct Ctx {
   double* chunk_part = nullptr;
   double* d_super = nullptr;
   double* d_super_own = nullptr;
+  uint32_t* count = nullptr;  // k_super_sums last-block counter (zero between launches)
+  IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
+  IkfCtl* h_ctl = nullptr;  // pinned staging copy
+  hipEvent_t done_ev = nullptr;  // end of a device-resident update (polled)
   double* h_super = nullptr;  // pinned
   bool searched = false;
   // profiling: event pairs pending per kind, accumulated time
   bool prof = false;
+  int prof_mask = 0;  // bit k: time kernel kind k
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[3];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   double prof_ms[3] = {0, 0, 0};
@@ -1042,6 +1432,135 @@ static void free_scan(Ctx* c) {
   c->chunk_part = nullptr;
 }
 
+// Enqueue one measurement pass (+ super-chunk sums) on the handle's stream.
+// Host mode: pose P by value, search iff which == 1.  Device mode (ctl != 0):
+// the pose and the search/reuse choice come from the control block in HBM;
+// which == 2 launches both kernels (each exits unless selected).
+// Wait for everything enqueued on the handle's stream by polling an event: a
+// blocking stream sync sleeps and wakes ~10-20 us late, a large share of a
+// ~60 us IKF iteration.
+static hipError_t wait_stream(Ctx& c) {
+  hipError_t e;
+  if (!c.done_ev && (e = hipEventCreateWithFlags(&c.done_ev, hipEventDisableTiming))) return e;
+  if ((e = hipEventRecord(c.done_ev, c.stream))) return e;
+  while ((e = hipEventQuery(c.done_ev)) == hipErrorNotReady) {
+  }
+  return e;
+}
+
+// Fused filter step of a single-rank device-resident update.
+struct SolveArgs {
+  int on;        // run the filter step in the pass epilogue
+  int pass_idx;  // ctl->passes this pass belongs to
+  int iter, maxit;
+  double R;
+};
+
+static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
+                        int extrinsic_est, const SolveArgs* sa = nullptr) {
+  if (!c.map) {
+    set_error("slio pass: no map uploaded");
+    return SLIO_ESTATE;
+  }
+  if (!c.bx && c.n > 0) {
+    set_error("slio pass: no scan uploaded");
+    return SLIO_ESTATE;
+  }
+  if (which == 0 && !c.searched) {
+    set_error("slio pass: reuse pass before any search pass");
+    return SLIO_ESTATE;
+  }
+  const int64_t C = num_chunks(c.n);
+  int64_t c0, c1;
+  rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
+  PassCfg cfg;
+  cfg.ctl = ctl;
+  cfg.want_search = 1;
+  cfg.plane_thr = c.prm.plane_threshold;
+  cfg.max_sqd = c.prm.max_match_sqd;
+  {
+    // the first sphere must sit inside the 5x5x5 cube: rho0 < 2h
+    const float rho = std::min(c.prm.search_radius, 1.99f * c.map->g.h);
+    cfg.radius_sq = rho > 0.0f ? rho * rho : 0.0f;
+  }
+  cfg.far_sq = c.prm.far_query_margin > 0.0f ? c.prm.far_query_margin * c.prm.far_query_margin : 0.0f;
+  cfg.extrinsic = extrinsic_est ? 1 : 0;
+  cfg.c_begin = c0;
+  cfg.c_end = c1;
+  const int per = SLIO_NSUPER / c.prm.nranks;
+  cfg.pass_idx = sa ? sa->pass_idx : 0;
+  PassOut o{c.nbr_idx, c.nbr_sqd, c.plane, c.sel, c.resid, c.chunk_part};
+  ScanDev s{c.bx, c.by, c.bz, c.n};
+  const PoseDev P = Parg ? *Parg : PoseDev{};
+  const int64_t nblk = c1 - c0;
+  if (c.prof && (c.pending[0].size() + c.pending[1].size()) > 256) prof_drain(c);
+  const bool run_search = which != 0, run_reuse = which != 1;
+  // Profiled launches carry their start/stop events inside the dispatch
+  // packet (hipExtLaunchKernelGGL): no separate marker packets, so timing
+  // does not open gaps between the dependent kernels.
+  auto timing = [&](int kind) {
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (c.prof && (c.prof_mask & (1 << kind))) {
+      ev = prof_pair(c);
+      c.pending[kind].push_back(ev);
+    }
+    return ev;
+  };
+  if (nblk > 0 && run_search) {
+    const auto ev = timing(SLIO_KERNEL_SEARCH);
+    const MapView mv{c.map->g, c.map->n, c.map->pts, c.map->start};
+    const bool sph = cfg.radius_sq > 0.0f;
+    const dim3 nb((unsigned)nblk);
+#define SLIO_LAUNCH(L, SPH, DEV)                                                                   \
+  hipExtLaunchKernelGGL(k_search_pass<L, 4, SPH, DEV>, nb, dim3(search_block<L>()), 0, c.stream, \
+                        ev.first, ev.second, 0, mv, s, P, cfg, o)
+#define SLIO_LAUNCH2(L, SPH) \
+  do {                        \
+    if (ctl)                  \
+      SLIO_LAUNCH(L, SPH, true); \
+    else                      \
+      SLIO_LAUNCH(L, SPH, false); \
+  } while (0)
+    switch (c.prm.lanes_per_query * 2 + (sph ? 1 : 0)) {
+      case 2: SLIO_LAUNCH2(1, false); break;
+      case 3: SLIO_LAUNCH2(1, true); break;
+      case 8: SLIO_LAUNCH2(4, false); break;
+      case 9: SLIO_LAUNCH2(4, true); break;
+      case 16: SLIO_LAUNCH2(8, false); break;
+      case 17: SLIO_LAUNCH2(8, true); break;
+      case 5: SLIO_LAUNCH2(2, true); break;
+      default: SLIO_LAUNCH2(2, false); break;
+    }
+#undef SLIO_LAUNCH2
+#undef SLIO_LAUNCH
+  }
+  if (nblk > 0 && run_reuse) {
+    const auto ev = timing(SLIO_KERNEL_REUSE);
+    PassCfg rcfg = cfg;
+    rcfg.want_search = 0;
+    const dim3 nb((unsigned)nblk), bs(SLIO_CHUNK);
+    if (ctl)
+      hipExtLaunchKernelGGL(k_reuse_pass<true>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
+                            rcfg, o);
+    else
+      hipExtLaunchKernelGGL(k_reuse_pass<false>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
+                            rcfg, o);
+  }
+  {
+    const auto ev = timing(SLIO_KERNEL_SUPER);
+    // single-rank device-resident update: + filter step in the last block
+    const bool fuse = sa && sa->on;
+    hipExtLaunchKernelGGL(k_super_sums, dim3(SLIO_NSUPER), dim3(SLIO_NPROD * kSuperSeg), 0,
+                          c.stream, ev.first, ev.second, 0, (const double*)c.chunk_part, C,
+                          c.prm.rank * per, (c.prm.rank + 1) * per, c.d_super,
+                          fuse ? ctl : (IkfCtl*)nullptr, c.count, fuse ? sa->R : 0.0,
+                          fuse ? sa->iter : 0, fuse ? sa->maxit : 0);
+  }
+  SLIO_HIP(hipGetLastError());
+  if (which != 0) c.searched = true;
+  return SLIO_OK;
+}
+
 }  // namespace slio
 
 using namespace slio;
@@ -1088,6 +1607,7 @@ int slio_params_default(slio_params* p) {
   p->plane_threshold = 0.1f;
   p->max_match_sqd = 5.0f;
   p->max_grid_cells = (int64_t)1 << 29;
+  p->far_query_margin = 100.0f;
   return SLIO_OK;
 }
 
@@ -1100,6 +1620,10 @@ int slio_create(slio_handle* out, const slio_params* p) {
   if (p->max_points <= 0 || p->nranks <= 0 || (SLIO_NSUPER % p->nranks) != 0 || p->rank < 0 ||
       p->rank >= p->nranks) {
     set_error("slio_create: bad max_points / rank / nranks");
+    return SLIO_EINVAL;
+  }
+  if (!(p->far_query_margin >= 0.0f) || !(p->search_radius >= 0.0f)) {
+    set_error("slio_create: far_query_margin / search_radius must be >= 0");
     return SLIO_EINVAL;
   }
   int ndev = 0;
@@ -1126,7 +1650,9 @@ int slio_create(slio_handle* out, const slio_params* p) {
   }
   h->c.stream = h->c.own_stream;
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
-      hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess) {
+      hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
+      hipMalloc(&h->c.count, sizeof(uint32_t) * 4) != hipSuccess ||
+      hipMemset(h->c.count, 0, sizeof(uint32_t) * 4) != hipSuccess) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
     return SLIO_ENOMEM;
@@ -1147,6 +1673,10 @@ int slio_destroy(slio_handle h) {
     (void)hipEventDestroy(p.second);
   }
   (void)hipFree(h->c.d_super_own);
+  (void)hipFree(h->c.count);
+  (void)hipFree(h->c.ctl);
+  (void)hipHostFree(h->c.h_ctl);
+  if (h->c.done_ev) (void)hipEventDestroy(h->c.done_ev);
   (void)hipHostFree(h->c.h_super);
   h->c.map.reset();
   if (h->c.own_stream) (void)hipStreamDestroy(h->c.own_stream);
@@ -1375,85 +1905,73 @@ int slio_iterate_async(slio_handle h, const slio_pose* x, int do_search, int ext
     set_error("slio_iterate_async: null pose");
     return SLIO_EINVAL;
   }
-  if (!c.map) {
-    set_error("slio_iterate_async: no map uploaded");
-    return SLIO_ESTATE;
-  }
-  if (!c.bx && c.n > 0) {
-    set_error("slio_iterate_async: no scan uploaded");
-    return SLIO_ESTATE;
-  }
-  if (!do_search && !c.searched) {
-    set_error("slio_iterate_async: reuse pass before any search pass");
-    return SLIO_ESTATE;
-  }
-  const int64_t C = num_chunks(c.n);
-  int64_t c0, c1;
-  rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
-  PassCfg cfg;
-  cfg.plane_thr = c.prm.plane_threshold;
-  cfg.max_sqd = c.prm.max_match_sqd;
-  {
-    // the first sphere must sit inside the 5x5x5 cube: rho0 < 2h
-    const float rho = std::min(c.prm.search_radius, 1.99f * c.map->g.h);
-    cfg.radius_sq = rho > 0.0f ? rho * rho : 0.0f;
-  }
-  cfg.extrinsic = extrinsic_est ? 1 : 0;
-  cfg.c_begin = c0;
-  cfg.c_end = c1;
-  PassOut o{c.nbr_idx, c.nbr_sqd, c.plane, c.sel, c.resid, c.chunk_part};
-  ScanDev s{c.bx, c.by, c.bz, c.n};
   const PoseDev P = make_pose(x);
-  const int64_t nblk = c1 - c0;
-  if (c.prof && (c.pending[0].size() + c.pending[1].size()) > 256) prof_drain(c);
-  if (nblk > 0) {
-    const int kind = do_search ? SLIO_KERNEL_SEARCH : SLIO_KERNEL_REUSE;
-    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (c.prof) {
-      ev = prof_pair(c);
-      (void)hipEventRecord(ev.first, c.stream);
-    }
-    if (do_search) {
-      const MapView mv{c.map->g, c.map->n, c.map->pts, c.map->start};
-      const bool sph = cfg.radius_sq > 0.0f;
-      const unsigned nb = (unsigned)nblk;
-      switch (c.prm.lanes_per_query) {
-        case 1: sph ? k_search_pass<1, 4, true><<<nb, search_block<1>(), 0, c.stream>>>(mv, s, P, cfg, o)
-                    : k_search_pass<1, 4, false><<<nb, search_block<1>(), 0, c.stream>>>(mv, s, P, cfg, o);
-          break;
-        case 4: sph ? k_search_pass<4, 4, true><<<nb, search_block<4>(), 0, c.stream>>>(mv, s, P, cfg, o)
-                    : k_search_pass<4, 4, false><<<nb, search_block<4>(), 0, c.stream>>>(mv, s, P, cfg, o);
-          break;
-        case 8: sph ? k_search_pass<8, 4, true><<<nb, search_block<8>(), 0, c.stream>>>(mv, s, P, cfg, o)
-                    : k_search_pass<8, 4, false><<<nb, search_block<8>(), 0, c.stream>>>(mv, s, P, cfg, o);
-          break;
-        default: sph ? k_search_pass<2, 4, true><<<nb, search_block<2>(), 0, c.stream>>>(mv, s, P, cfg, o)
-                     : k_search_pass<2, 4, false><<<nb, search_block<2>(), 0, c.stream>>>(mv, s, P, cfg, o);
-          break;
+  const int rc = enqueue_pass(c, &P, nullptr, do_search ? 1 : 0, extrinsic_est);
+  if (rc) return rc;
+  if (d_super) *d_super = c.d_super;
+  return SLIO_OK;
+}
+
+int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R,
+                           int maximum_iter, int extrinsic_est, int mode,
+                           slio_allreduce_fn reduce, void* reduce_ctx, slio_ikf_stats* stats) {
+  SLIO_CHECK_H(h);
+  if (!x || !P || !(R > 0.0) || maximum_iter < 1 ||
+      (mode != SLIO_MODE_REFERENCE && mode != SLIO_MODE_FIXED)) {
+    set_error("slio_ikf_update_device: bad arguments");
+    return SLIO_EINVAL;
+  }
+  Ctx& c = h->c;
+  if (!c.ctl) {
+    SLIO_HIP(hipMalloc(&c.ctl, sizeof(IkfCtl)));
+    SLIO_HIP(hipHostMalloc(&c.h_ctl, sizeof(IkfCtl)));
+  }
+  IkfCtl& hc = *c.h_ctl;
+  hc.x = *x;
+  hc.xprop = *x;
+  std::memcpy(hc.P, P, sizeof(double) * 576);
+  hc.converge = 1;
+  hc.t = 0;
+  hc.done = 0;
+  hc.search_now = 1;
+  hc.passes = hc.searches = hc.valid_passes = 0;
+  hc.mode = mode;
+  hc.last_m = 0;
+  hc.singular = 0;
+  SLIO_HIP(hipMemcpyAsync(c.ctl, c.h_ctl, sizeof(IkfCtl), hipMemcpyHostToDevice, c.stream));
+  const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
+  for (int i = first; i < maximum_iter; ++i) {
+    // single rank: the filter step runs in the pass kernel's last block;
+    // multi-rank: pass -> all-reduce of the super sums -> k_ikf_solve
+    const SolveArgs sa{reduce ? 0 : 1, i - first, i, maximum_iter, R};
+    int rc = enqueue_pass(c, nullptr, c.ctl, mode == SLIO_MODE_FIXED ? 1 : 2, extrinsic_est, &sa);
+    if (rc) return rc;
+    if (reduce) {
+      rc = reduce(reduce_ctx, c.d_super, (int64_t)SLIO_NSUPER * SLIO_NPROD, (void*)c.stream);
+      if (rc) {
+        set_error("slio_ikf_update_device: reduce callback failed");
+        return SLIO_EDEVICE;
       }
-    } else {
-      k_reuse_pass<<<(unsigned)nblk, SLIO_CHUNK, 0, c.stream>>>(s, P, cfg, o);
+      k_ikf_solve<<<1, kSolveThreads, 0, c.stream>>>(c.ctl, c.d_super, R, i, maximum_iter);
     }
-    if (c.prof) {
-      (void)hipEventRecord(ev.second, c.stream);
-      c.pending[kind].push_back(ev);
-    }
-  }
-  const int per = SLIO_NSUPER / c.prm.nranks;
-  std::pair<hipEvent_t, hipEvent_t> ev2{nullptr, nullptr};
-  if (c.prof) {
-    ev2 = prof_pair(c);
-    (void)hipEventRecord(ev2.first, c.stream);
-  }
-  k_super_sums<<<SLIO_NSUPER, SLIO_NPROD * kSuperSeg, 0, c.stream>>>(c.chunk_part, C, c.prm.rank * per,
-                                                   (c.prm.rank + 1) * per, c.d_super);
-  if (c.prof) {
-    (void)hipEventRecord(ev2.second, c.stream);
-    c.pending[SLIO_KERNEL_SUPER].push_back(ev2);
   }
   SLIO_HIP(hipGetLastError());
-  if (do_search) c.searched = true;
-  if (d_super) *d_super = c.d_super;
+  SLIO_HIP(hipMemcpyAsync(c.h_ctl, c.ctl, sizeof(IkfCtl), hipMemcpyDeviceToHost, c.stream));
+  SLIO_HIP(wait_stream(c));
+  if (c.h_ctl->singular) {
+    set_error("slio_ikf_update_device: singular covariance");
+    return SLIO_EINVAL;
+  }
+  *x = c.h_ctl->x;
+  std::memcpy(P, c.h_ctl->P, sizeof(double) * 576);
+  if (stats) {
+    stats->passes = c.h_ctl->passes;
+    stats->searches = c.h_ctl->searches;
+    stats->valid_passes = c.h_ctl->valid_passes;
+    stats->converged = c.h_ctl->converge;
+    stats->last_m = c.h_ctl->last_m;
+    stats->device_ms = 0.0;
+  }
   return SLIO_OK;
 }
 
@@ -1467,11 +1985,15 @@ int slio_profile(slio_handle h, int enable) {
   SLIO_CHECK_H(h);
   Ctx& c = h->c;
   prof_drain(c);
-  c.prof = enable != 0;
-  for (int k = 0; k < 3; ++k) {
-    c.prof_ms[k] = 0.0;
-    c.prof_n[k] = 0;
-  }
+  const bool keep = (enable & SLIO_PROFILE_KEEP) != 0;
+  const int sel = enable & ~SLIO_PROFILE_KEEP;
+  c.prof_mask = (sel == 1) ? 7 : ((sel >> 1) & 7);
+  c.prof = c.prof_mask != 0;
+  if (!keep)
+    for (int k = 0; k < 3; ++k) {
+      c.prof_ms[k] = 0.0;
+      c.prof_n[k] = 0;
+    }
   return SLIO_OK;
 }
 
@@ -1494,7 +2016,7 @@ int slio_super_download(slio_handle h, double* super_out) {
   Ctx& c = h->c;
   SLIO_HIP(hipMemcpyAsync(c.h_super, c.d_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD,
                           hipMemcpyDeviceToHost, c.stream));
-  SLIO_HIP(hipStreamSynchronize(c.stream));
+  SLIO_HIP(wait_stream(c));
   if (super_out) std::memcpy(super_out, c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD);
   return SLIO_OK;
 }
@@ -1562,3 +2084,9 @@ int slio_get_residuals(slio_handle h, float* pd2) {
 }
 
 }  // extern "C"
+
+#ifdef SLIO_SOLVE_STAMP
+extern "C" int slio_dbg_solve_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamp), sizeof(g_sstamp)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -6,7 +6,8 @@
 // gain K of the reference is never formed:
 //   K * h       = K_front[:, :12] * (H^T h) / R
 //   (K * H)[:, :12] = K_front[:, :12] * (H^T H) / R
-// which is algebraically identical to esekfom.hpp:306-319.  The control flow
+// and K_front[:, :12] comes from a 12x12 inverse (see filter_step): all
+// algebraically identical to esekfom.hpp:306-319.  The control flow
 // (passes i = -1 .. maximum_iter-1, re-search only after a converged pass or
 // forced at i == maximum_iter-2, skip on effct_feat_num < 1, final
 // P = (I - KH) P) follows esekfom.hpp:292-345 line for line.
@@ -72,40 +73,51 @@ slio_pose pose_of(const slio_state& x) {
   return p;
 }
 
-// One filter update from the pass sums; returns the 24x24 KH in KH and
-// updates x.  Follows esekfom.hpp:303-321.  Pinv = P_.inverse(): P_ does not
-// change inside the iteration loop, so the caller inverts it once per update
-// (the reference re-inverts the same matrix every pass, esekfom.hpp:311).
-bool filter_step(const slio_state& x_prop, const double* Pinv, double R, const double HTH[78],
+// One filter update from the pass sums (esekfom.hpp:303-321), updating x and
+// returning K H and dx.  K_front[:, :12] = (H^T H / R + P^-1)^-1 [:, :12] is
+// evaluated with the push-through identity
+//   (P^-1 + E^T M E)^-1 E^T = P E^T (I + M E P E^T)^-1,  M = H^T H / R,
+// i.e. K12 = P[:, :12] (I + M P11)^-1: one 12x12 inverse, no P^-1 (the
+// reference inverts two 24x24 matrices per pass, esekfom.hpp:311).  The
+// device kernel k_ikf_solve uses exactly this operation order.
+bool filter_step(const slio_state& x_prop, const double* P, double R, const double HTH[78],
                  const double HTh[12], slio_state& x, double KH[576], double dx[24]) {
   double dx_new[24];
   boxminus(x, x_prop, dx_new);
-  double H12[144];
+  double M[144];
   int k = 0;
   for (int i = 0; i < 12; ++i)
     for (int j = i; j < 12; ++j) {
-      H12[i * 12 + j] = HTH[k];
-      H12[j * 12 + i] = HTH[k];
+      const double v = HTH[k] / R;
+      M[i * 12 + j] = v;
+      M[j * 12 + i] = v;
       ++k;
     }
-  double A[576];
-  for (int i = 0; i < 24; ++i)
-    for (int j = 0; j < 24; ++j) {
-      const double hth = (i < 12 && j < 12) ? H12[i * 12 + j] : 0.0;
-      A[i * 24 + j] = hth / R + Pinv[i * 24 + j];
+  double B[144], X[144];
+  for (int r = 0; r < 12; ++r)
+    for (int j = 0; j < 12; ++j) {
+      double s = 0.0;
+      for (int q = 0; q < 12; ++q) s += M[r * 12 + q] * P[q * 24 + j];
+      B[r * 12 + j] = (r == j ? 1.0 : 0.0) + s;
     }
-  double Kf[576];
-  if (!invert<24>(A, Kf)) return false;
-  std::memset(KH, 0, sizeof(double) * 576);
-  double Kh[24];
-  for (int i = 0; i < 24; ++i) {
-    double s = 0.0;
-    for (int j = 0; j < 12; ++j) s += Kf[i * 24 + j] * HTh[j];
-    Kh[i] = s / R;
+  if (!invert<12>(B, X)) return false;
+  double K12[288];
+  for (int r = 0; r < 24; ++r)
     for (int c = 0; c < 12; ++c) {
-      double t = 0.0;
-      for (int j = 0; j < 12; ++j) t += Kf[i * 24 + j] * H12[j * 12 + c];
-      KH[i * 24 + c] = t / R;
+      double s = 0.0;
+      for (int q = 0; q < 12; ++q) s += P[r * 24 + q] * X[q * 12 + c];
+      K12[r * 12 + c] = s;
+    }
+  double Kh[24];
+  for (int r = 0; r < 24; ++r) {
+    double s = 0.0;
+    for (int j = 0; j < 12; ++j) s += K12[r * 12 + j] * HTh[j];
+    Kh[r] = s / R;
+    for (int c = 0; c < 24; ++c) {
+      double v = 0.0;
+      if (c < 12)
+        for (int j = 0; j < 12; ++j) v += K12[r * 12 + j] * M[j * 12 + c];
+      KH[r * 24 + c] = v;
     }
   }
   for (int i = 0; i < 24; ++i) {
@@ -154,11 +166,6 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
   double sup[SLIO_NSUPER * SLIO_NPROD];
   const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
   double dev_ms = 0.0;
-  double Pinv[576];
-  if (!invert<24>(P, Pinv)) {
-    set_error("slio_ikf_update: singular covariance");
-    return SLIO_EINVAL;
-  }
   for (int i = first; i < maximum_iter; ++i) {
     const bool search = (mode == SLIO_MODE_FIXED) ? true : converge;
     const slio_pose pose = pose_of(*x);
@@ -186,7 +193,7 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
       continue;
     }
     ++st.valid_passes;
-    if (!filter_step(x_prop, Pinv, R, HTH, HTh, *x, KH, dx)) {
+    if (!filter_step(x_prop, P, R, HTH, HTh, *x, KH, dx)) {
       set_error("slio_ikf_update: singular covariance");
       return SLIO_EINVAL;
     }

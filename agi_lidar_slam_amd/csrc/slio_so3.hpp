@@ -14,13 +14,21 @@
 
 #include <cmath>
 
+#ifndef SLIO_HD
+#if defined(__HIPCC__)
+#define SLIO_HD __host__ __device__
+#else
+#define SLIO_HD
+#endif
+#endif
+
 namespace slio {
 
 struct Quat {
   double w = 1.0, x = 0.0, y = 0.0, z = 0.0;
 };
 
-inline Quat qmul(const Quat& a, const Quat& b) {
+SLIO_HD inline Quat qmul(const Quat& a, const Quat& b) {
   Quat r;
   r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
   r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
@@ -29,13 +37,13 @@ inline Quat qmul(const Quat& a, const Quat& b) {
   return r;
 }
 
-inline Quat qnormalized(const Quat& q) {
-  const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+SLIO_HD inline Quat qnormalized(const Quat& q) {
+  const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
   return Quat{q.w / n, q.x / n, q.y / n, q.z / n};
 }
 
 // row-major 3x3
-inline void qmatrix(const Quat& q, double R[9]) {
+SLIO_HD inline void qmatrix(const Quat& q, double R[9]) {
   const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
   const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
   const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
@@ -51,63 +59,74 @@ inline void qmatrix(const Quat& q, double R[9]) {
   R[8] = 1.0 - (txx + tyy);
 }
 
-inline Quat qfrom_matrix(const double m[9]) {
-  auto M = [&](int r, int c) { return m[r * 3 + c]; };
+// Eigen Quaternion(Matrix3) (Quaternion.h quaternionbase_assign_impl): trace
+// branch, else i = argmax diagonal, j = (i+1)%3, k = (j+1)%3 -- written out per
+// i so no local array is indexed at run time (that lowers to GPU scratch).
+SLIO_HD inline Quat qfrom_matrix(const double m[9]) {
+  const double m00 = m[0], m01 = m[1], m02 = m[2];
+  const double m10 = m[3], m11 = m[4], m12 = m[5];
+  const double m20 = m[6], m21 = m[7], m22 = m[8];
   Quat q;
-  double t = M(0, 0) + M(1, 1) + M(2, 2);
+  double t = m00 + m11 + m22;
   if (t > 0.0) {
-    t = std::sqrt(t + 1.0);
+    t = sqrt(t + 1.0);
     q.w = 0.5 * t;
     t = 0.5 / t;
-    q.x = (M(2, 1) - M(1, 2)) * t;
-    q.y = (M(0, 2) - M(2, 0)) * t;
-    q.z = (M(1, 0) - M(0, 1)) * t;
-  } else {
-    int i = 0;
-    if (M(1, 1) > M(0, 0)) i = 1;
-    if (M(2, 2) > M(i, i)) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    t = std::sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
-    double v[3];
-    v[i] = 0.5 * t;
+    q.x = (m21 - m12) * t;
+    q.y = (m02 - m20) * t;
+    q.z = (m10 - m01) * t;
+  } else if (!(m11 > m00) && !(m22 > m00)) {  // i = 0, j = 1, k = 2
+    t = sqrt(m00 - m11 - m22 + 1.0);
+    q.x = 0.5 * t;
     t = 0.5 / t;
-    q.w = (M(k, j) - M(j, k)) * t;
-    v[j] = (M(j, i) + M(i, j)) * t;
-    v[k] = (M(k, i) + M(i, k)) * t;
-    q.x = v[0];
-    q.y = v[1];
-    q.z = v[2];
+    q.w = (m21 - m12) * t;
+    q.y = (m10 + m01) * t;
+    q.z = (m20 + m02) * t;
+  } else if ((m11 > m00) && !(m22 > m11)) {  // i = 1, j = 2, k = 0
+    t = sqrt(m11 - m22 - m00 + 1.0);
+    q.y = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (m02 - m20) * t;
+    q.z = (m21 + m12) * t;
+    q.x = (m01 + m10) * t;
+  } else {  // i = 2, j = 0, k = 1
+    t = sqrt(m22 - m00 - m11 + 1.0);
+    q.z = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (m10 - m01) * t;
+    q.x = (m02 + m20) * t;
+    q.y = (m12 + m21) * t;
   }
   return q;
 }
 
 constexpr double kSmallEps = 1e-10;
 
-inline Quat so3_exp(const double om[3]) {
-  const double theta = std::sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+SLIO_HD inline Quat so3_exp(const double om[3]) {
+  const double theta = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
   const double half = 0.5 * theta;
   double imag;
-  const double real = std::cos(half);
+  const double real = cos(half);
   if (theta < kSmallEps) {
     const double t2 = theta * theta;
     const double t4 = t2 * t2;
     imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;
   } else {
-    imag = std::sin(half) / theta;
+    imag = sin(half) / theta;
   }
   return qnormalized(Quat{real, imag * om[0], imag * om[1], imag * om[2]});
 }
 
-inline void so3_log(const Quat& q, double out[3]) {
-  const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z);
+SLIO_HD inline void so3_log(const Quat& q, double out[3]) {
+  const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z);
   const double w = q.w;
   double f;
   if (n < kSmallEps) {
     f = 2.0 / w - 2.0 * (n * n) / (w * (w * w));
-  } else if (std::fabs(w) < kSmallEps) {
+  } else if (fabs(w) < kSmallEps) {
     f = (w > 0 ? M_PI : -M_PI) / n;
   } else {
-    f = 2.0 * std::atan(n / w) / n;
+    f = 2.0 * atan(n / w) / n;
   }
   out[0] = f * q.x;
   out[1] = f * q.y;
@@ -115,7 +134,7 @@ inline void so3_log(const Quat& q, double out[3]) {
 }
 
 // SO3(a.matrix()^T * b.matrix()).log()  (esekfom.hpp:242-246)
-inline void so3_boxminus(const Quat& b, const Quat& a, double out[3]) {
+SLIO_HD inline void so3_boxminus(const Quat& b, const Quat& a, double out[3]) {
   double Ra[9], Rb[9], M[9];
   qmatrix(a, Ra);
   qmatrix(b, Rb);
@@ -131,6 +150,7 @@ inline void so3_boxminus(const Quat& b, const Quat& a, double out[3]) {
 // on an exactly singular pivot.
 template <int N>
 inline bool invert(const double* A, double* out) {
+  using std::fabs;
   double a[N][2 * N];
   for (int i = 0; i < N; ++i)
     for (int j = 0; j < N; ++j) {
@@ -139,10 +159,10 @@ inline bool invert(const double* A, double* out) {
     }
   for (int c = 0; c < N; ++c) {
     int p = c;
-    double best = std::fabs(a[c][c]);
+    double best = fabs(a[c][c]);
     for (int r = c + 1; r < N; ++r)
-      if (std::fabs(a[r][c]) > best) {
-        best = std::fabs(a[r][c]);
+      if (fabs(a[r][c]) > best) {
+        best = fabs(a[r][c]);
         p = r;
       }
     if (best == 0.0) return false;

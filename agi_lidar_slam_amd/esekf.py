@@ -226,15 +226,18 @@ class Esekf(_Handle):
                                            ikdtree: KdTreeMap, Nearest_Points: dict | None,
                                            maximum_iter: int, extrinsic_est: bool,
                                            mode: int = L.SLIO_MODE_REFERENCE,
-                                           reduce=None) -> None:
-        """esekfom.hpp:270-346 (host C++ driver slio_ikf_update)."""
+                                           reduce=None, device_loop: bool = True) -> None:
+        """esekfom.hpp:270-346.  device_loop=True: slio_ikf_update_device (state,
+        covariance and control flow resident in HBM, one host sync per update);
+        False: slio_ikf_update (host C++ 24x24 algebra after every pass)."""
         self._bind(feats_down_body, ikdtree)
         xc = self.x_.to_c()
         P = np.ascontiguousarray(self.P_, dtype=np.float64).copy()
         cb = reduce if reduce is not None else L.ALLREDUCE_FN()
         st = L.SlioIkfStats()
-        L.check(self.lib.slio_ikf_update(self.h, C.byref(xc), L.dptr(P), float(R), int(maximum_iter),
-                                         int(extrinsic_est), int(mode), cb, None, C.byref(st)),
+        fn = self.lib.slio_ikf_update_device if device_loop else self.lib.slio_ikf_update
+        L.check(fn(self.h, C.byref(xc), L.dptr(P), float(R), int(maximum_iter),
+                   int(extrinsic_est), int(mode), cb, None, C.byref(st)),
                 "update_iterated_dyn_share_modified")
         self.x_ = StateIkfom.from_c(xc)
         self.P_ = P.reshape(24, 24)

@@ -50,7 +50,7 @@ def cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--map-points", type=int, default=10_000_000)
@@ -59,6 +59,13 @@ def main():
     ap.add_argument("--cpu-scans", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP events on the search kernel (roofline fields null)")
+    ap.add_argument("--timing-every", type=int, default=5,
+                    help="time the search kernel (HIP events) on every k-th timed step; events "
+                         "cost ~5 us of idle per launch, so sampling keeps them out of most steps")
+    ap.add_argument("--host-loop", action="store_true",
+                    help="run the 24x24 step on the host after every pass (slio_ikf_update)")
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "search_traffic.json"))
     args = ap.parse_args()
@@ -125,27 +132,42 @@ def main():
     P0 = np.eye(24) * 1e-2
     stats = L.SlioIkfStats()
 
+    xs0 = L.SlioState()
+    xs0.pos[:] = list(st0[0:3])
+    xs0.rot[:] = list(st0[3:7])
+    xs0.rli[:] = list(st0[7:11])
+    xs0.tli[:] = list(st0[11:14])
+    xs0.grav[:] = list(st0[23:26])
+    xs = L.SlioState()
+    P = np.empty_like(P0)
+    P_ptr, xs_ref, st_ref = L.dptr(P), C.byref(xs), C.byref(stats)
+    fn = lib.slio_ikf_update if args.host_loop else lib.slio_ikf_update_device
+
     def step():
-        xs = L.SlioState()
-        xs.pos[:] = list(st0[0:3])
-        xs.rot[:] = list(st0[3:7])
-        xs.rli[:] = list(st0[7:11])
-        xs.tli[:] = list(st0[11:14])
-        xs.grav[:] = list(st0[23:26])
-        P = P0.copy()
-        L.check(lib.slio_ikf_update(h, C.byref(xs), L.dptr(P), 0.001, args.iters, 0,
-                                    L.SLIO_MODE_FIXED, reduce_cb, None, C.byref(stats)), "ikf")
+        # every step restarts from the same prior (same work per step)
+        C.memmove(C.addressof(xs), C.addressof(xs0), C.sizeof(xs))
+        P[...] = P0
+        rc = fn(h, xs_ref, P_ptr, 0.001, args.iters, 0, L.SLIO_MODE_FIXED, reduce_cb, None, st_ref)
+        if rc:
+            L.check(rc, "ikf")
         return xs
 
     for _ in range(args.warmup):
         step()
-    lib.slio_profile(h, 1)
+    lib.slio_profile(h, 0)  # reset totals
+    search_bit = 1 << (L.SLIO_KERNEL_SEARCH + 1)
+    every = max(1, args.timing_every)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        timed = not args.no_kernel_timing and k % every == 0
+        if timed:  # events on the search pass only, on this step's launches
+            lib.slio_profile(h, search_bit | L.SLIO_PROFILE_KEEP)
         xs = step()
+        if timed:
+            lib.slio_profile(h, L.SLIO_PROFILE_KEEP)  # pause, keep totals
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -153,9 +175,6 @@ def main():
     ms = C.c_double()
     nl = C.c_int64()
     lib.slio_profile_read(h, L.SLIO_KERNEL_SEARCH, C.byref(ms), C.byref(nl))
-    ms_super = C.c_double()
-    nl_super = C.c_int64()
-    lib.slio_profile_read(h, L.SLIO_KERNEL_SUPER, C.byref(ms_super), C.byref(nl_super))
     lib.slio_profile(h, 0)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{dev}")
@@ -220,6 +239,7 @@ def main():
             "map_points": args.map_points,
             "scan_points": args.scan_points,
             "iterations_per_step": args.iters,
+            "ikf_loop": "host" if args.host_loop else "device-resident",
             "grid_cell_m": args.cell,
             "parallelism": (f"scan points sharded x{world}, map replicated, one RCCL all-reduce "
                             "of 8x91 fp64 per iteration" if world > 1 else "single GPU"),
@@ -236,7 +256,7 @@ def main():
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_us": avg_kernel_s * 1e6,
             "launches": int(nl.value),
-            "super_sums_avg_us": (ms_super.value / max(nl_super.value, 1)) * 1e3,
+            "timing": f"HIP events in the dispatch packet, search launches of 1 in {every} timed steps",
         },
         "cpu_baseline": cpu,
     }

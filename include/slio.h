@@ -71,7 +71,13 @@ typedef struct slio_params {
                               cells.
                               Any value gives the exact 5-NN; it only tunes
                               speed.                                           */
-  int32_t reserved;
+  float far_query_margin;  /* scan points farther than this (metres) outside
+                              the map grid's bounding box get no neighbours
+                              (index -1, never selected) instead of an exact
+                              but unbounded far search; default 100.  They
+                              cannot pass the max_match_sqd gate anyway, so
+                              only Nearest_Points differs from ikd-Tree.
+                              0 disables the cut (exact everywhere).          */
 } slio_params;
 
 /* Pose slice of state_ikfom used by the measurement model
@@ -168,9 +174,15 @@ int slio_get_residuals(slio_handle h, float* pd2);
 /* ---- kernel timing (HIP events on the handle's stream) ------------------- */
 #define SLIO_KERNEL_SEARCH 0   /* fused search pass (kNN + plane + Jacobian + chunk sums) */
 #define SLIO_KERNEL_REUSE 1    /* non-search pass                                          */
-#define SLIO_KERNEL_SUPER 2    /* super-chunk sums                                         */
-/* enable != 0 brackets every launch with hipEvents and accumulates elapsed
- * device time per kernel kind; enabling resets the counters. */
+#define SLIO_KERNEL_SUPER 2    /* super-chunk sums (+ fused filter step)                   */
+#define SLIO_PROFILE_KEEP 16   /* flag: keep the accumulated totals                         */
+/* enable == 1 times every launch of every kind (start/stop hipEvents carried
+ * in the dispatch packet) and accumulates elapsed device time per kind;
+ * otherwise only the kinds whose bit 1 << (kind + 1) is set are timed (e.g.
+ * 1 << (SLIO_KERNEL_SEARCH + 1) = 2 times the search pass alone).  Without
+ * SLIO_PROFILE_KEEP any call resets the totals; with it, the call only
+ * changes what is timed (SLIO_PROFILE_KEEP alone pauses), so timing can be
+ * sampled over a subset of launches.  0 disables and resets. */
 int slio_profile(slio_handle h, int enable);
 /* Accumulated device milliseconds and launch count of a kernel kind
  * (synchronises the stream). */
@@ -202,6 +214,17 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R,
                     int maximum_iter, int extrinsic_est, int mode,
                     slio_allreduce_fn reduce, void* reduce_ctx,
                     slio_ikf_stats* stats);
+
+/* Same update, device-resident: state, covariance and the control flags of
+ * esekfom.hpp:292-345 live in HBM and a one-wavefront kernel performs the
+ * 24x24 step after each pass (same operation order as slio_ikf_update), so
+ * the passes are enqueued back to back with no host round trip; the host
+ * synchronises once at the end.  `reduce` (if any) is called once per pass at
+ * enqueue time and must enqueue a stream-ordered SUM all-reduce. */
+int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R,
+                           int maximum_iter, int extrinsic_est, int mode,
+                           slio_allreduce_fn reduce, void* reduce_ctx,
+                           slio_ikf_stats* stats);
 
 /* Manifold helpers exported for tests (esekfom.hpp:59-73, 236-258). */
 int slio_state_boxplus(const slio_state* x, const double dx[24], slio_state* out);

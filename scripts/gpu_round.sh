@@ -13,10 +13,13 @@ for step in "$@"; do
       timeout -k 10 600 python scripts/sweep_search.py > gpurun_out/${tag}_sweep.log 2>&1 || { echo "sweep failed"; tail -20 gpurun_out/${tag}_sweep.log; exit 3; }
       cat gpurun_out/${tag}_sweep.log | grep -v amdgpu.ids ;;
     bench)
-      timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 4; }
+      timeout -k 10 600 python bench.py --steps 100 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 4; }
       cat gpurun_out/${tag}_bench.json ;;
+    benchh)
+      timeout -k 10 600 python bench.py --steps 100 --warmup 5 --host-loop --no-cpu-baseline > gpurun_out/${tag}_benchh.json 2> gpurun_out/${tag}_benchh.err || { echo "benchh failed"; tail -20 gpurun_out/${tag}_benchh.err; exit 4; }
+      cat gpurun_out/${tag}_benchh.json ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 5; }
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 5; }
       find gpurun_out/${tag}_prof -name "*stats*" | head; for f in $(find gpurun_out/${tag}_prof -name "*kernel_stats.csv"); do head -8 $f; done ;;
   esac
 done

@@ -53,6 +53,7 @@ def test_params_default(lib):
     assert lib.slio_params_default(C.byref(p)) == 0
     assert p.max_points == 100000 and p.nranks == 1
     assert abs(p.plane_threshold - 0.1) < 1e-7 and p.max_match_sqd == 5.0
+    assert p.far_query_margin == 100.0 and p.search_radius == 0.0
 
 
 def test_bad_arguments_fail_loudly(lib):
@@ -64,6 +65,10 @@ def test_bad_arguments_fail_loudly(lib):
     p.nranks = 3
     assert lib.slio_create(C.byref(h), C.byref(p)) == -1
     assert b"nranks" in lib.slio_last_error()
+    p.nranks = 1
+    p.far_query_margin = -1.0
+    assert lib.slio_create(C.byref(h), C.byref(p)) == -1
+    assert b"far_query_margin" in lib.slio_last_error()
     assert lib.slio_iterate_async(None, None, 1, 0, None) == -1
 
 

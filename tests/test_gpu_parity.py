@@ -25,7 +25,7 @@ def L():
     return _lib
 
 
-def mk(L, n_max=100000, rank=0, nranks=1, cell=0.75, max_cells=0, radius=None, lpq=0):
+def mk(L, n_max=100000, rank=0, nranks=1, cell=0.75, max_cells=0, radius=None, lpq=0, far=None):
     lib = L.load()
     p = L.SlioParams()
     lib.slio_params_default(C.byref(p))
@@ -33,6 +33,8 @@ def mk(L, n_max=100000, rank=0, nranks=1, cell=0.75, max_cells=0, radius=None, l
     if radius is not None:
         p.search_radius = radius
     p.lanes_per_query = lpq
+    if far is not None:
+        p.far_query_margin = far
     if max_cells:
         p.max_grid_cells = max_cells
     h = C.c_void_p()
@@ -113,7 +115,7 @@ def assert_sums_close(got, ref):
 # ------------------------------------------------------------------ kNN
 def test_knn_golden_bitexact(L):
     z = np.load(os.path.join(GOLD, "knn_golden.npz"))
-    h = mk(L)
+    h = mk(L, far=0.0)   # exact everywhere: the golden set has far-away queries
     try:
         upload_map(L, h, z["map"])
         assert upload_scan(L, h, z["query"]) == 0
@@ -187,8 +189,10 @@ def rot_err(q1, q2):
     return 2 * np.arccos(min(1.0, abs(float(np.dot(q1, q2)) / np.linalg.norm(q1) / np.linalg.norm(q2))))
 
 
-@pytest.mark.parametrize("pat,maxit,mode", [("vlp16", 3, 0), ("avia", 4, 0), ("avia", 4, 1)])
-def test_ikf_update_vs_oracle(L, oracle_mod, c1, pat, maxit, mode):
+@pytest.mark.parametrize("pat,maxit,mode,device_loop", [
+    ("vlp16", 3, 0, True), ("avia", 4, 0, True), ("avia", 4, 1, True),
+    ("vlp16", 3, 0, False), ("avia", 4, 1, False)])
+def test_ikf_update_vs_oracle(L, oracle_mod, c1, pat, maxit, mode, device_loop):
     from agi_lidar_slam_amd.esekf import Esekf, KdTreeMap, StateIkfom
     mp, fr, T = c1[pat]
     st = state_of(fr)
@@ -201,7 +205,8 @@ def test_ikf_update_vs_oracle(L, oracle_mod, c1, pat, maxit, mode):
     kf.change_x(StateIkfom.from_array(st))
     kf.change_P(P0)
     nearest = {}
-    kf.update_iterated_dyn_share_modified(0.001, fr.body, kd, nearest, maxit, False, mode=mode)
+    kf.update_iterated_dyn_share_modified(0.001, fr.body, kd, nearest, maxit, False, mode=mode,
+                                          device_loop=device_loop)
     x = kf.get_x().to_array()
     assert np.abs(x[0:3] - s_ref[0:3]).max() < TOL_POS
     assert rot_err(x[3:7], s_ref[3:7]) < TOL_ROT
@@ -221,9 +226,12 @@ def test_ikf_update_vs_oracle(L, oracle_mod, c1, pat, maxit, mode):
 
 
 # ------------------------------------------------------------------ edges
-def test_edge_cases(L):
+@pytest.mark.parametrize("far", [0.0, None])
+def test_edge_cases(L, far):
+    """far=0: exact everywhere (ikd-Tree semantics); default far_query_margin
+    (100 m): the query ~1.4e6 m outside the map gets no neighbours."""
     lib = L.load()
-    h = mk(L, n_max=1000)
+    h = mk(L, n_max=1000, far=far)
     try:
         # reuse before any search -> ESTATE; iterate before map -> ESTATE
         assert upload_scan(L, h, np.zeros((4, 3), np.float32)) == 0
@@ -237,8 +245,11 @@ def test_edge_cases(L):
         s = iterate(L, h, IDENT, True)
         assert s[90] == 0
         idx, sqd, sel, pl, rs = results(L, h, 4)
-        assert (idx[[0, 1, 3], :3] >= 0).all() and (idx[:, 3:] == -1).all()
+        near = [0, 1, 3] if far == 0.0 else [0, 1]
+        assert (idx[near, :3] >= 0).all() and (idx[:, 3:] == -1).all()
         assert (idx[2] == -1).all() and not sel.any()
+        if far != 0.0:
+            assert (idx[3] == -1).all()
         assert list(idx[0, :3]) == [0, 1, 2]
         # capacity
         assert upload_scan(L, h, np.zeros((1001, 3), np.float32)) == -4
@@ -312,3 +323,30 @@ def test_full_size_c2_properties(L, oracle_mod):
         np.testing.assert_array_equal(s, s2)
     finally:
         L.load().slio_destroy(h)
+
+
+@pytest.mark.parametrize("mode,ext", [(0, False), (1, False), (0, True)])
+def test_device_loop_matches_host_loop(L, c1, mode, ext):
+    """slio_ikf_update_device (24x24 step on device) vs slio_ikf_update (host):
+    same operation order; only libm sin/cos/atan may differ by an ulp."""
+    from agi_lidar_slam_amd.esekf import Esekf, KdTreeMap, StateIkfom
+    mp, fr, _ = c1["avia"]
+    st = state_of(fr)
+    kd = KdTreeMap()
+    kd.Build(mp)
+    out = []
+    for dev in (False, True):
+        kf = Esekf()
+        kf.change_x(StateIkfom.from_array(st))
+        kf.change_P(np.eye(24) * 1e-2)
+        kf.update_iterated_dyn_share_modified(0.001, fr.body, kd, None, 4, ext, mode=mode,
+                                              device_loop=dev)
+        s = kf.last_stats
+        out.append((kf.get_x().to_array(), kf.get_P().copy(),
+                    (s.passes, s.searches, s.valid_passes, s.converged, s.last_m)))
+        kf.close()
+    (x0, P0, s0), (x1, P1, s1) = out
+    assert s0 == s1
+    np.testing.assert_allclose(x1, x0, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(P1, P0, rtol=0, atol=1e-9 * np.abs(P0).max())
+    kd.close()
