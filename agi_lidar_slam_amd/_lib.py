@@ -77,6 +77,27 @@ class SlioIkfStats(C.Structure):
     ]
 
 
+class SlioLioParams(C.Structure):
+    """slio_lio_params (include/slio_frontend.h)."""
+    _fields_ = [
+        ("device", C.c_int32),
+        ("n_scan", C.c_int32),
+        ("horizon_scan", C.c_int32),
+        ("downsample_rate", C.c_int32),
+        ("lidar_min_range", C.c_float),
+        ("lidar_max_range", C.c_float),
+        ("edge_threshold", C.c_float),
+        ("surf_threshold", C.c_float),
+        ("surf_leaf_size", C.c_float),
+        ("max_points", C.c_int32),
+        ("reserved", C.c_int32 * 4),
+    ]
+
+
+class SlioLioCounts(C.Structure):
+    _fields_ = [("n_extracted", C.c_int64), ("n_corner", C.c_int64), ("n_surface", C.c_int64)]
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
 
 _P = C.c_void_p
@@ -85,8 +106,9 @@ _DP = C.POINTER(C.c_double)
 _IP = C.POINTER(C.c_int32)
 _I64P = C.POINTER(C.c_int64)
 _U8P = C.POINTER(C.c_uint8)
+_U16P = C.POINTER(C.c_uint16)
 
-# name -> (restype, argtypes); every symbol include/slio.h declares
+# name -> (restype, argtypes); every symbol include/*.h declares
 SIGNATURES = {
     "slio_params_default": (C.c_int, [C.POINTER(SlioParams)]),
     "slio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioParams)]),
@@ -120,6 +142,20 @@ SIGNATURES = {
     ),
     "slio_state_boxplus": (C.c_int, [C.POINTER(SlioState), _DP, C.POINTER(SlioState)]),
     "slio_state_boxminus": (C.c_int, [C.POINTER(SlioState), C.POINTER(SlioState), _DP]),
+    # include/slio_frontend.h (LIO-SAM front-end)
+    "slio_lio_params_default": (C.c_int, [C.POINTER(SlioLioParams)]),
+    "slio_lio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioLioParams)]),
+    "slio_lio_destroy": (C.c_int, [_P]),
+    "slio_lio_set_stream": (C.c_int, [_P, _P]),
+    "slio_lio_set_deskew": (C.c_int, [_P, _DP, _DP, _DP, _DP, C.c_int32, C.c_double, C.c_int32]),
+    "slio_lio_upload": (C.c_int, [_P, _FP, _FP, _FP, _FP, _U16P, _FP, C.c_int64]),
+    "slio_lio_run_async": (C.c_int, [_P]),
+    "slio_lio_run": (C.c_int, [_P, C.POINTER(SlioLioCounts)]),
+    "slio_lio_get_counts": (C.c_int, [_P, C.POINTER(SlioLioCounts)]),
+    "slio_lio_get_range_image": (C.c_int, [_P, _FP, _IP]),
+    "slio_lio_get_cloud_info": (C.c_int, [_P, _IP, _IP, _IP, _FP, _FP]),
+    "slio_lio_get_features": (C.c_int, [_P, _FP, _U8P, _IP]),
+    "slio_lio_get_clouds": (C.c_int, [_P, _FP, _FP]),
 }
 
 _lib = None
@@ -168,3 +204,7 @@ def iptr(a: np.ndarray):
 
 def u8ptr(a: np.ndarray):
     return a.ctypes.data_as(_U8P)
+
+
+def u16ptr(a: np.ndarray):
+    return a.ctypes.data_as(_U16P)

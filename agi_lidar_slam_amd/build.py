@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libslio.so")
 
-SOURCES = ["slio_device.hip", "slio_ikf.cpp"]
+SOURCES = ["slio_device.hip", "slio_ikf.cpp", "slio_lio.hip"]
 HEADERS = ["slio_common.hpp", "slio_plane.hpp", "slio_so3.hpp"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -37,7 +37,7 @@ def _stale() -> bool:
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "slio.h"))
+    deps += [os.path.join(ROOT, "include", h) for h in ("slio.h", "slio_frontend.h")]
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 

@@ -1,0 +1,1331 @@
+// slio_lio.hip -- LIO-SAM front-end on gfx950.
+//
+// One scan = 7 launches on the handle's stream:
+//   memset(cell owners)            reset of rangeMat (imageProjection.cpp:146)
+//   k_lio_claim   per point        projectPointCloud filters (:614-636); the
+//                                  cell goes to the smallest point index
+//                                  (atomicMin) = "first point wins" (:638)
+//   k_lio_fill    block per ring   rangeMat / fullCloud for the winners, with
+//                                  deskewPoint (:565-604) relative to the first
+//                                  valid point; per-ring valid counts
+//   k_lio_extract block per ring   cloudExtraction (:656-678): ring offsets,
+//                                  start/endRingIndex, in-ring stream compaction
+//   k_lio_smooth  per point        calculateSmoothness (featureExtraction.cpp
+//                                  :108-131) + markOccludedPoints (:137-177) in
+//                                  pull form (each flag computed by its owner)
+//   k_lio_features block per ring  extractFeatures (:183-296): per sector a
+//                                  bitonic sort, the greedy edge / flat picks on
+//                                  one wavefront (ballot over 64 candidates),
+//                                  surface collection and the per-ring
+//                                  pcl::VoxelGrid (sorted voxel keys + centroids)
+//   k_lio_concat  block per ring   ring-ordered cloud_corner / cloud_surface
+// Rings are independent in extractFeatures (suppression reaches 5 points, the
+// gap between rings' candidate ranges is 10), sectors within a ring are not,
+// so a ring is one workgroup and its 6 sectors run in order.
+//
+// Deterministic choices where the reference is implementation-defined match
+// oracle/frontend_oracle.cpp: float trig as correctly
+// rounded values (double evaluation), sort ties by point index, smoothness
+// entries the reference never initialises are never picked.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "slio_common.hpp"
+#include "slio_frontend.h"
+
+namespace slio {
+namespace lio {
+
+#define LIO_HIP(call)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      set_error(std::string(#call) + ": " + hipGetErrorString(e_));            \
+      return SLIO_EDEVICE;                                                     \
+    }                                                                          \
+  } while (0)
+
+constexpr int kMaxImu = 2000;          // queueLength (imageProjection.cpp:35)
+constexpr int kCornerPerRing = 6 * 20;  // 6 sectors x 20 corners (featureExtraction.cpp:209)
+constexpr uint32_t kNone = 0xffffffffu;
+
+struct Geo {
+  int n_scan, horizon, ds;
+  float min_r, max_r;
+  float ang_res_x;
+  int64_t cells;
+};
+
+struct In {
+  const float *x, *y, *z, *in;
+  const uint16_t* ring;
+  const float* time;
+  int64_t n;
+};
+
+struct Deskew {
+  const double *t, *rx, *ry, *rz;
+  int cur;  // imuPointerCur
+  double t0;  // timeScanCur
+  int on;
+};
+
+// ---------------------------------------------------------------- math
+__device__ __forceinline__ float fcos(float a) { return (float)cos((double)a); }
+__device__ __forceinline__ float fsin(float a) { return (float)sin((double)a); }
+__device__ __forceinline__ float fatan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+
+struct Aff {
+  float m[3][4];
+};
+
+// pcl::getTransformation(0, 0, 0, roll, pitch, yaw) (pcl/common/impl/eigen.hpp)
+__device__ Aff get_rot(float roll, float pitch, float yaw) {
+  const float A = fcos(yaw), B = fsin(yaw), C = fcos(pitch), D = fsin(pitch), E = fcos(roll),
+              F = fsin(roll), DE = D * E, DF = D * F;
+  Aff t;
+  t.m[0][0] = A * C;
+  t.m[0][1] = A * DF - B * E;
+  t.m[0][2] = B * F + A * DE;
+  t.m[0][3] = 0.0f;
+  t.m[1][0] = B * C;
+  t.m[1][1] = A * E + B * DF;
+  t.m[1][2] = B * DE - A * F;
+  t.m[1][3] = 0.0f;
+  t.m[2][0] = -D;
+  t.m[2][1] = C * F;
+  t.m[2][2] = C * E;
+  t.m[2][3] = 0.0f;
+  return t;
+}
+
+__device__ __forceinline__ float cof(const Aff& a, int i1, int i2, int j1, int j2) {
+  return a.m[i1][j1] * a.m[i2][j2] - a.m[i1][j2] * a.m[i2][j1];
+}
+
+// Eigen Transform<float,3,Affine>::inverse(): 3x3 cofactor inverse, t' = -(R^-1 t)
+__device__ Aff inverse(const Aff& a) {
+  // cofactor_3x3<i, j>: i1 = (i+1)%3, i2 = (i+2)%3, j1 = (j+1)%3, j2 = (j+2)%3
+  const float c00 = cof(a, 1, 2, 1, 2), c10 = cof(a, 2, 0, 1, 2), c20 = cof(a, 0, 1, 1, 2);
+  const float det = (c00 * a.m[0][0] + c10 * a.m[1][0]) + c20 * a.m[2][0];
+  const float invdet = 1.0f / det;
+  Aff r;
+  r.m[0][0] = c00 * invdet;
+  r.m[0][1] = c10 * invdet;
+  r.m[0][2] = c20 * invdet;
+  r.m[1][0] = cof(a, 1, 2, 2, 0) * invdet;  // cofactor<0,1>
+  r.m[1][1] = cof(a, 2, 0, 2, 0) * invdet;  // cofactor<1,1>
+  r.m[1][2] = cof(a, 0, 1, 2, 0) * invdet;  // cofactor<2,1>
+  r.m[2][0] = cof(a, 1, 2, 0, 1) * invdet;  // cofactor<0,2>
+  r.m[2][1] = cof(a, 2, 0, 0, 1) * invdet;  // cofactor<1,2>
+  r.m[2][2] = cof(a, 0, 1, 0, 1) * invdet;  // cofactor<2,2>
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    r.m[i][3] = -((r.m[i][0] * a.m[0][3] + r.m[i][1] * a.m[1][3]) + r.m[i][2] * a.m[2][3]);
+  return r;
+}
+
+__device__ Aff compose(const Aff& l, const Aff& r) {
+  Aff o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      o.m[i][j] = (l.m[i][0] * r.m[0][j] + l.m[i][1] * r.m[1][j]) + l.m[i][2] * r.m[2][j];
+    o.m[i][3] = ((l.m[i][0] * r.m[0][3] + l.m[i][1] * r.m[1][3]) + l.m[i][2] * r.m[2][3]) + l.m[i][3];
+  }
+  return o;
+}
+
+// findRotation (imageProjection.cpp:492-529)
+__device__ void find_rotation(const Deskew& d, double pointTime, float& ox, float& oy, float& oz) {
+  int f = 0;
+  while (f < d.cur) {
+    if (pointTime < d.t[f]) break;
+    ++f;
+  }
+  if (pointTime > d.t[f] || f == 0) {
+    ox = (float)d.rx[f];
+    oy = (float)d.ry[f];
+    oz = (float)d.rz[f];
+  } else {
+    const int b = f - 1;
+    const double rf = (pointTime - d.t[b]) / (d.t[f] - d.t[b]);
+    const double rb = (d.t[f] - pointTime) / (d.t[f] - d.t[b]);
+    ox = (float)(d.rx[f] * rf + d.rx[b] * rb);
+    oy = (float)(d.ry[f] * rf + d.ry[b] * rb);
+    oz = (float)(d.rz[f] * rf + d.rz[b] * rb);
+  }
+}
+
+__device__ __forceinline__ float point_range(float x, float y, float z) {
+  return sqrtf(x * x + y * y + z * z);  // pointDistance, utility.h:382-384
+}
+
+// ---------------------------------------------------------------- block helpers
+// exclusive scan of one int per thread over the block; returns the total
+template <int NT>
+__device__ int block_exclusive_scan(int v, int* scratch /* NT/64 + 1 */, int& excl) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) scratch[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    int s = 0;
+    for (int q = 0; q < NT / 64; ++q) {
+      const int c = scratch[q];
+      scratch[q] = s;
+      s += c;
+    }
+    scratch[NT / 64] = s;
+  }
+  __syncthreads();
+  excl = scratch[w] + x - v;
+  const int total = scratch[NT / 64];
+  __syncthreads();
+  return total;
+}
+
+// in-LDS bitonic sort of P (power of two) 64-bit keys, ascending
+template <int NT>
+__device__ void bitonic_sort(uint64_t* key, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += NT) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint64_t a = key[i], b = key[l];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Bitonic sort of P <= 2 * NT keys (P a power of two >= 64), ascending.
+// Thread t holds indices t and t + NT; stages whose partner distance j <= 32
+// stay inside a wavefront (register shuffles), only j >= 64 goes through LDS.
+template <int NT>
+__device__ void bitonic_sort_shfl(uint64_t* key, int P) {
+  const int t = threadIdx.x;
+  const int i0 = t, i1 = t + NT;
+  const bool h0 = i0 < P, h1 = i1 < P;
+  uint64_t v0 = h0 ? key[i0] : 0, v1 = h1 ? key[i1] : 0;
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        if (h0) key[i0] = v0;
+        if (h1) key[i1] = v1;
+        __syncthreads();
+        if (h0) {
+          const uint64_t p = key[i0 ^ j];
+          const bool up = (i0 & k) == 0, lower = (i0 & j) == 0;
+          v0 = (lower == up) ? (v0 < p ? v0 : p) : (v0 < p ? p : v0);
+        }
+        if (h1) {
+          const uint64_t p = key[i1 ^ j];
+          const bool up = (i1 & k) == 0, lower = (i1 & j) == 0;
+          v1 = (lower == up) ? (v1 < p ? v1 : p) : (v1 < p ? p : v1);
+        }
+        __syncthreads();
+      } else {
+        const uint64_t p0 = __shfl_xor(v0, j, 64);
+        const uint64_t p1 = __shfl_xor(v1, j, 64);
+        {
+          const bool up = (i0 & k) == 0, lower = (i0 & j) == 0;
+          v0 = (lower == up) ? (v0 < p0 ? v0 : p0) : (v0 < p0 ? p0 : v0);
+        }
+        {
+          const bool up = (i1 & k) == 0, lower = (i1 & j) == 0;
+          v1 = (lower == up) ? (v1 < p1 ? v1 : p1) : (v1 < p1 ? p1 : v1);
+        }
+      }
+    }
+  }
+  if (h0) key[i0] = v0;
+  if (h1) key[i1] = v1;
+  __syncthreads();
+}
+
+// Independent bitonic sorts of the cap-sized segments of key[0, total)
+// (cap a power of two >= 64, total a multiple of cap): the network's k never
+// exceeds cap, so partners stay inside a segment.  Thread t holds slots
+// t + s * NT; partner distances j <= 32 use register shuffles.
+template <int NT>
+__device__ void seg_bitonic_shfl(uint64_t* key, int total, int cap) {
+  constexpr int S = 4;  // slots per thread (total <= S * NT)
+  const int t = threadIdx.x;
+  uint64_t v[S];
+  bool h[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int i = t + s * NT;
+    h[s] = i < total;
+    v[s] = h[s] ? key[i] : ~0ull;
+  }
+  for (int k = 2; k <= cap; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          if (h[s]) key[t + s * NT] = v[s];
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int i = t + s * NT;
+          if (h[s]) {
+            const uint64_t p = key[i ^ j];
+            const bool up = (i & (cap - 1) & k) == 0, lower = (i & j) == 0;  // direction from the in-segment offset
+            v[s] = (lower == up) ? (v[s] < p ? v[s] : p) : (v[s] < p ? p : v[s]);
+          }
+        }
+        __syncthreads();
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int i = t + s * NT;
+          const uint64_t p = __shfl_xor(v[s], j, 64);
+          const bool up = (i & (cap - 1) & k) == 0, lower = (i & j) == 0;  // direction from the in-segment offset
+          v[s] = (lower == up) ? (v[s] < p ? v[s] : p) : (v[s] < p ? p : v[s]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (h[s]) key[t + s * NT] = v[s];
+  __syncthreads();
+}
+
+__device__ __forceinline__ int pow2ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ __launch_bounds__(256) void k_lio_claim(In in, Geo g, uint32_t* owner,
+                                                   uint32_t* block_first) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool ok = i < in.n;
+  int64_t c = 0;
+  if (ok) {
+    const float px = in.x[i], py = in.y[i], pz = in.z[i];
+    const float range = point_range(px, py, pz);
+    const int row = in.ring[i];
+    ok = !(range < g.min_r || range > g.max_r) && row >= 0 && row < g.n_scan && row % g.ds == 0;
+    if (ok) {
+      const float horizonAngle = (float)((double)(fatan2(px, py) * 180.0f) / M_PI);
+      int col = (int)(-round(((double)horizonAngle - 90.0) / (double)g.ang_res_x) +
+                      (double)(g.horizon / 2));
+      if (col >= g.horizon) col -= g.horizon;
+      ok = col >= 0 && col < g.horizon;
+      c = col + (int64_t)row * g.horizon;
+    }
+  }
+#ifndef SLIO_ABL_NOATOMIC
+  if (ok) atomicMin(&owner[c], (uint32_t)i);
+#else
+  if (ok && c < 0) owner[0] = 0;  // diagnostic: no cell atomics
+#endif
+  // first valid point (deskew reference): the block minimum goes to its own
+  // slot (same-address device atomics serialise: 2k of them cost ~20 us)
+  __shared__ uint32_t wmin[4];
+  uint32_t v = ok ? (uint32_t)i : kNone;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) block_first[blockIdx.x] = min(min(wmin[0], wmin[1]), min(wmin[2], wmin[3]));
+}
+
+constexpr int kRowThreads = 1024;
+constexpr int kFillSplit = 8;     // blocks per ring in k_lio_fill (deskew trig on all CUs)
+constexpr int kFillThreads = 256;
+constexpr int kImuLds = 512;      // deskew table entries staged in LDS (larger tables stay in HBM)
+
+__device__ __forceinline__ void fsincos(float a, float& s, float& c) {
+  double sd, cd;
+  sincos((double)a, &sd, &cd);
+  s = (float)sd;
+  c = (float)cd;
+}
+
+// pcl::getTransformation(0, 0, 0, roll, pitch, yaw) with paired sin/cos
+__device__ Aff get_rot_sc(float roll, float pitch, float yaw) {
+  float A, B, C, D, E, F;
+  fsincos(yaw, B, A);
+  fsincos(pitch, D, C);
+  fsincos(roll, F, E);
+  const float DE = D * E, DF = D * F;
+  Aff t;
+  t.m[0][0] = A * C;
+  t.m[0][1] = A * DF - B * E;
+  t.m[0][2] = B * F + A * DE;
+  t.m[0][3] = 0.0f;
+  t.m[1][0] = B * C;
+  t.m[1][1] = A * E + B * DF;
+  t.m[1][2] = B * DE - A * F;
+  t.m[1][3] = 0.0f;
+  t.m[2][0] = -D;
+  t.m[2][1] = C * F;
+  t.m[2][2] = C * E;
+  t.m[2][3] = 0.0f;
+  return t;
+}
+
+// grid (n_scan, kFillSplit): block (r, s) fills columns [s H / S, (s + 1) H / S) of ring r
+__global__ __launch_bounds__(kFillThreads) void k_lio_fill(In in, Geo g, const uint32_t* owner,
+                                                           const uint32_t* block_first, int nfirst,
+                                                           Deskew d, float* range_mat,
+                                                           float4* full, int32_t* row_part) {
+  __shared__ Aff startInv;
+  __shared__ int scratch[kFillThreads / 64 + 1];
+  __shared__ uint32_t wmin[kFillThreads / 64];
+  __shared__ double tb[4][kImuLds];
+  const int r = blockIdx.x, sp = blockIdx.y;
+  const int t = threadIdx.x;
+  const bool desk = d.on && d.cur > 0;
+  if (desk) {
+    if (d.cur < kImuLds) {
+      for (int q = t; q <= d.cur; q += kFillThreads) {
+        tb[0][q] = d.t[q];
+        tb[1][q] = d.rx[q];
+        tb[2][q] = d.ry[q];
+        tb[3][q] = d.rz[q];
+      }
+    }
+    uint32_t v = kNone;
+    for (int q = t; q < nfirst; q += kFillThreads) v = min(v, block_first[q]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if ((t & 63) == 0) wmin[t >> 6] = v;
+    __syncthreads();
+    if (d.cur < kImuLds) {
+      d.t = tb[0];
+      d.rx = tb[1];
+      d.ry = tb[2];
+      d.rz = tb[3];
+    }
+    if (t == 0) {
+      uint32_t f = wmin[0];
+      for (int q = 1; q < kFillThreads / 64; ++q) f = min(f, wmin[q]);
+      float rx = 0.f, ry = 0.f, rz = 0.f;
+      if (f != kNone) find_rotation(d, d.t0 + (double)in.time[f], rx, ry, rz);
+      startInv = inverse(get_rot_sc(rx, ry, rz));
+    }
+    __syncthreads();
+  }
+  const int c0 = (int)((int64_t)g.horizon * sp / kFillSplit);
+  const int c1 = (int)((int64_t)g.horizon * (sp + 1) / kFillSplit);
+  int cnt = 0;
+  for (int col = c0 + t; col < c1; col += kFillThreads) {
+    const int64_t c = col + (int64_t)r * g.horizon;
+    const uint32_t o = owner[c];
+    if (o == kNone) {
+      range_mat[c] = FLT_MAX;
+      continue;
+    }
+    const float px = in.x[o], py = in.y[o], pz = in.z[o];
+    float ox = px, oy = py, oz = pz;
+    if (desk) {
+      float rx, ry, rz;
+      find_rotation(d, d.t0 + (double)in.time[o], rx, ry, rz);
+      const Aff bt = compose(startInv, get_rot_sc(rx, ry, rz));
+      ox = bt.m[0][0] * px + bt.m[0][1] * py + bt.m[0][2] * pz + bt.m[0][3];
+      oy = bt.m[1][0] * px + bt.m[1][1] * py + bt.m[1][2] * pz + bt.m[1][3];
+      oz = bt.m[2][0] * px + bt.m[2][1] * py + bt.m[2][2] * pz + bt.m[2][3];
+    }
+    range_mat[c] = point_range(px, py, pz);
+    full[c] = make_float4(ox, oy, oz, in.in[o]);
+    ++cnt;
+  }
+  int excl;
+  const int total = block_exclusive_scan<kFillThreads>(cnt, scratch, excl);
+  if (t == 0) row_part[r * kFillSplit + sp] = total;
+}
+
+struct CloudInfo {
+  int32_t* start_ring;
+  int32_t* end_ring;
+  int32_t* col_ind;
+  float* prange;
+  float4* xyzi;
+  int32_t* n_ext;
+};
+
+__global__ __launch_bounds__(kRowThreads) void k_lio_extract(Geo g, const float* range_mat,
+                                                             const float4* full,
+                                                             const int32_t* row_count, CloudInfo ci) {
+  __shared__ int scratch[kRowThreads / 64 + 1];
+  const int r = blockIdx.x;
+  const int t = threadIdx.x;
+  int part = 0;  // ring offset = sum of the partial counts of rings < r
+  for (int q = t; q < r * kFillSplit; q += kRowThreads) part += row_count[q];
+  int excl;
+  const int off = block_exclusive_scan<kRowThreads>(part, scratch, excl);
+  if (t == 0) {
+    int cnt = 0;
+    for (int q = 0; q < kFillSplit; ++q) cnt += row_count[r * kFillSplit + q];
+    ci.start_ring[r] = off - 1 + 5;
+    ci.end_ring[r] = off + cnt - 1 - 5;
+    if (r == g.n_scan - 1) *ci.n_ext = off + cnt;
+  }
+  // thread t owns the contiguous columns [t * per, (t + 1) * per)
+  const int per = (g.horizon + kRowThreads - 1) / kRowThreads;
+  const int c0 = t * per, c1 = min(c0 + per, g.horizon);
+  int cnt = 0;
+  for (int col = c0; col < c1; ++col) cnt += range_mat[col + (int64_t)r * g.horizon] != FLT_MAX;
+  block_exclusive_scan<kRowThreads>(cnt, scratch, excl);
+  int k = off + excl;
+  for (int col = c0; col < c1; ++col) {
+    const int64_t c = col + (int64_t)r * g.horizon;
+    const float rg = range_mat[c];
+    if (rg != FLT_MAX) {
+      ci.col_ind[k] = col;
+      ci.prange[k] = rg;
+      ci.xyzi[k] = full[c];
+      ++k;
+    }
+  }
+}
+
+// calculateSmoothness + markOccludedPoints, pull form: flag i is set iff some
+// j of the reference loop (:138-176) would set it.
+__device__ __forceinline__ bool occ_a(const float* r, const int32_t* col, int j) {
+  const int cd = abs(col[j + 1] - col[j]);
+  return cd < 10 && (double)(r[j] - r[j + 1]) > 0.3;
+}
+__device__ __forceinline__ bool occ_b(const float* r, const int32_t* col, int j) {
+  const int cd = abs(col[j + 1] - col[j]);
+  return cd < 10 && !((double)(r[j] - r[j + 1]) > 0.3) && (double)(r[j + 1] - r[j]) > 0.3;
+}
+
+__global__ __launch_bounds__(256) void k_lio_smooth(const float* __restrict__ r,
+                                                    const int32_t* __restrict__ col,
+                                                    const int32_t* n_ext, float* curvature,
+                                                    uint8_t* picked, int32_t* label) {
+  const int n = *n_ext;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float curv = 0.0f;
+  int pk = 1;  // entries the reference never initialises: never picked
+  if (i >= 5 && i < n - 5) {
+    const float diffRange = r[i - 5] + r[i - 4] + r[i - 3] + r[i - 2] + r[i - 1] - r[i] * 10 +
+                            r[i + 1] + r[i + 2] + r[i + 3] + r[i + 4] + r[i + 5];
+    curv = diffRange * diffRange;
+    pk = 0;
+    const int jmax = n - 7;  // loop i < cloudSize - 6
+    for (int j = max(i, 5); j <= min(i + 5, jmax); ++j)
+      if (occ_a(r, col, j)) pk = 1;
+    for (int j = max(i - 6, 5); j <= min(i - 1, jmax); ++j)
+      if (occ_b(r, col, j)) pk = 1;
+    if (i <= jmax) {
+      const float diff1 = fabsf(r[i - 1] - r[i]);
+      const float diff2 = fabsf(r[i + 1] - r[i]);
+      if ((double)diff1 > 0.02 * (double)r[i] && (double)diff2 > 0.02 * (double)r[i]) pk = 1;
+    }
+  }
+  curvature[i] = curv;
+  picked[i] = (uint8_t)pk;
+  label[i] = 0;  // k_lio_features writes the rings' [start, end]
+}
+
+struct FeatOut {
+  int32_t* label;          // n_ext
+  float4* corner_stage;    // n_scan * kCornerPerRing
+  int32_t* corner_count;   // n_scan
+  float4* surf_stage;      // n_ext (ring r at its first extracted index)
+  int32_t* surf_count;     // n_scan
+};
+
+struct FeatCfg {
+  float edge_thr, surf_thr, leaf;
+  int sort_cap;   // power of two >= max sector length
+  int ring_cap;   // >= ring span incl. 5-point margins
+  int vox_cap;    // power of two >= max ring length
+};
+
+constexpr int kFeatThreads = 1024;
+
+// -DSLIO_LIO_STAMP: wall-clock phase stamps of k_lio_features per ring
+#ifdef SLIO_LIO_STAMP
+__device__ unsigned long long g_lstamp[256 * 8];  // [ring][slot]
+#define LSTAMP(k)                                                             \
+  do {                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_lstamp[blockIdx.x * 8 + (k)] = wall_clock64(); \
+  } while (0)
+// accumulate the time since the last LSTAMP_T0 into slot k (k = 6, 7)
+#define LSTAMP_T0() unsigned long long lst0_ = wall_clock64()
+#define LSTAMP_ACC(k)                                                          \
+  do {                                                                         \
+    const unsigned long long n_ = wall_clock64();                              \
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_lstamp[blockIdx.x * 8 + (k)] += n_ - lst0_; \
+    lst0_ = n_;                                                                \
+  } while (0)
+#else
+#define LSTAMP_T0() \
+  do {              \
+  } while (0)
+#define LSTAMP_ACC(k) \
+  do {                \
+  } while (0)
+#define LSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+// one ring per workgroup
+__global__ __launch_bounds__(kFeatThreads) void k_lio_features(
+    const CloudInfo ci, const float* __restrict__ curvature, const uint8_t* __restrict__ picked0,
+    FeatCfg cfg, FeatOut out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // dynamic LDS: keys[max(sort_cap, vox_cap)] (sector sort, then voxel sort),
+  // then per ring position: curvature, column, surface list, flag, label
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);  // sector segments, then voxel keys
+  uint64_t* skeys = keys + max(6 * cfg.sort_cap, cfg.vox_cap);  // sorted sector segments
+  float4* vp = reinterpret_cast<float4*>(skeys + 6 * cfg.sort_cap);  // vox_cap
+  float* curv = reinterpret_cast<float*>(vp + cfg.vox_cap);
+  int32_t* col = reinterpret_cast<int32_t*>(curv + cfg.ring_cap);
+  int32_t* slist = col + cfg.ring_cap;
+  // flags and labels are written by one lane and read by the others of the
+  // same wavefront: volatile LDS accesses, issued in program order
+  volatile uint8_t* flag = reinterpret_cast<volatile uint8_t*>(slist + cfg.ring_cap);
+  volatile int8_t* lab = reinterpret_cast<volatile int8_t*>(flag + cfg.ring_cap);
+  uint8_t* reach = reinterpret_cast<uint8_t*>(const_cast<int8_t*>(lab) + cfg.ring_cap);
+  __shared__ int s_nsurf, s_ncorner;
+  __shared__ int corner_pos[kCornerPerRing];
+  __shared__ int scratch[kFeatThreads / 64 + 1];
+  __shared__ float s_min[3], s_max[3];
+  __shared__ int s_overflow, s_minb[3], s_mul[3];
+
+  const int r = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = *ci.n_ext;
+  const int start = ci.start_ring[r], end = ci.end_ring[r];
+  const int base = max(start - 5, 0);
+  const int span_end = min(end + 5, n - 1);  // last index touched
+  LSTAMP(0);
+  int ncorner = 0;  // wavefront 0 counter (uniform)
+  for (int q = base + t; q <= span_end; q += kFeatThreads) {
+    curv[q - base] = curvature[q];
+    col[q - base] = ci.col_ind[q];
+    flag[q - base] = picked0[q];
+    lab[q - base] = 0;
+  }
+  __syncthreads();
+
+  // suppression reach (featureExtraction.cpp:220-237, 247-262): points ind+l,
+  // l = 1..5 (and -1..-5), are flagged while consecutive columns differ by
+  // <= 10, so a pick flags the contiguous range [ind - reachL, ind + reachR]
+  for (int q = base + t; q <= span_end; q += kFeatThreads) {
+    int rr = 0, rl = 0;
+    for (int l = 1; l <= 5 && q + l <= span_end; ++l) {
+      if (abs(col[q + l - base] - col[q + l - 1 - base]) > 10) break;
+      rr = l;
+    }
+    for (int l = 1; l <= 5 && q - l >= base; ++l) {
+      if (abs(col[q - l - base] - col[q - l + 1 - base]) > 10) break;
+      rl = l;
+    }
+    reach[q - base] = (uint8_t)(rl | (rr << 4));
+  }
+  __syncthreads();
+  LSTAMP(1);
+
+  // ---- std::sort(sp, ep) of all 6 sectors at once (the sorts depend only
+  // on the smoothness values, not on the picks): sector j occupies the
+  // segment [j * sort_cap, (j + 1) * sort_cap) of `keys`, padded with ~0, and
+  // a bitonic network with k <= sort_cap sorts every segment independently.
+  // Keys are unique (value, index) pairs, so ties fall to the lower index.
+  __shared__ int s_sp[6], s_ep[6];
+  if (t < 6) {
+    s_sp[t] = (start * (6 - t) + end * t) / 6;
+    s_ep[t] = (start * (5 - t) + end * (t + 1)) / 6 - 1;
+  }
+  __syncthreads();
+  const int cap = cfg.sort_cap;
+  for (int q = t; q < 6 * cap; q += kFeatThreads) {
+    const int j = q / cap, o = q - j * cap;
+    const int k = s_sp[j] + o;
+    uint64_t kk = ~0ull;
+    if (s_sp[j] < s_ep[j] && k < s_ep[j]) {
+      const float v = (k >= 5 && k < n - 5) ? curv[k - base] : 0.0f;
+      kk = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)k;
+    }
+    keys[q] = kk;
+  }
+  __syncthreads();
+  LSTAMP_T0();
+  // rank sort inside each segment (an LDS-broadcast compare loop beat the
+  // shuffle bitonic network here: 15 vs 21 us on a 2048-point ring)
+  for (int q = t; q < 6 * cap; q += kFeatThreads) {
+    const int j = q / cap, o = q - j * cap;
+    const int len = s_ep[j] - s_sp[j];
+    if (o >= len) continue;
+    const uint64_t me = keys[q];
+    const uint64_t* ks = keys + j * cap;
+    int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+    int i2 = 0;
+    for (; i2 + 4 <= len; i2 += 4) {
+      r0 += ks[i2] < me;
+      r1 += ks[i2 + 1] < me;
+      r2 += ks[i2 + 2] < me;
+      r3 += ks[i2 + 3] < me;
+    }
+    for (; i2 < len; ++i2) r0 += ks[i2] < me;
+    skeys[j * cap + (r0 + r1) + (r2 + r3)] = me;
+  }
+  __syncthreads();
+  LSTAMP_ACC(6);
+  // ---- greedy picks, sector by sector on wavefront 0 (no block barriers).
+  // A 64-candidate chunk is loaded once; inside it the picks only update
+  // register eligibility (a pick clears the candidates inside its reach
+  // range), and the chunk's labels and flags are written to LDS once the
+  // chunk is done, before the next chunk reads them.
+  if (w == 0) {
+    for (int j = 0; j < 6; j++) {
+      const int sp = s_sp[j], ep = s_ep[j];
+      if (sp >= ep) continue;
+      const uint64_t* sk = skeys + j * cap;
+      auto ind_at = [&](int k) -> int { return k == ep ? ep : (int)(uint32_t)sk[k - sp]; };
+      // edges: k = ep .. sp, at most 20 (:205-238).  [sp, ep) is sorted by
+      // curvature, so below the first sorted value <= edgeThreshold nothing
+      // is eligible: the scan stops there (k = ep, outside the sort, first).
+      int picks = 0;
+      bool stop = false;
+      for (int top = ep; top >= sp && !stop; top -= 64) {
+        const int k = top - lane;
+        int ind = 0, lo = 0, hi = -1;
+        bool el = false, tail = false, mine = false;
+        if (k >= sp) {
+          ind = ind_at(k);
+          const int bb = ind - base;
+          const int rc = reach[bb];
+          lo = ind - (rc & 15);
+          hi = ind + (rc >> 4);
+          const float cv = curv[bb];
+          el = !flag[bb] && cv > cfg.edge_thr;
+          tail = k < ep && !(cv > cfg.edge_thr);
+        }
+        const bool last_chunk = __ballot(tail) != 0;
+        uint64_t msk = __ballot(el);
+        while (msk) {
+          const int l = __ffsll((long long)msk) - 1;
+          if (++picks > 20) {
+            stop = true;
+            break;
+          }
+          const int lol = __builtin_amdgcn_readlane(lo, l);
+          const int hil = __builtin_amdgcn_readlane(hi, l);
+          if (lane == l) {
+            mine = true;
+            corner_pos[ncorner + picks - 1] = ind;
+          }
+          el = el && lane > l && !(ind >= lol && ind <= hil);
+          msk = __ballot(el);
+        }
+        if (mine) {
+          lab[ind - base] = 1;
+          for (int q = lo; q <= hi; ++q) flag[q - base] = 1;
+        }
+        if (last_chunk) break;
+      }
+      ncorner += min(picks, 20);
+      // flats: k = sp .. ep (:239-263).  Ascending curvature: the scan stops
+      // after the first sorted value >= surfThreshold; k = ep is examined last.
+      bool done_sorted = false;
+      for (int bot = sp; bot < ep && !done_sorted; bot += 64) {
+        const int k = bot + lane;
+        int ind = 0, lo = 0, hi = -1;
+        bool el = false, tail = false, mine = false;
+        if (k < ep) {
+          ind = ind_at(k);
+          const int bb = ind - base;
+          const int rc = reach[bb];
+          lo = ind - (rc & 15);
+          hi = ind + (rc >> 4);
+          const float cv = curv[bb];
+          el = !flag[bb] && cv < cfg.surf_thr;
+          tail = !(cv < cfg.surf_thr);
+        }
+        done_sorted = __ballot(tail) != 0;
+        uint64_t msk = __ballot(el);
+        while (msk) {
+          const int l = __ffsll((long long)msk) - 1;
+          const int lol = __builtin_amdgcn_readlane(lo, l);
+          const int hil = __builtin_amdgcn_readlane(hi, l);
+          mine |= lane == l;
+          el = el && lane > l && !(ind >= lol && ind <= hil);
+          msk = __ballot(el);
+        }
+        if (mine) {
+          lab[ind - base] = -1;
+          for (int q = lo; q <= hi; ++q) flag[q - base] = 1;
+        }
+      }
+      {  // k = ep (outside the sorted range)
+        const int bb = ep - base;
+        if (!flag[bb] && curv[bb] < cfg.surf_thr) {
+          const int rc = reach[bb];
+          const int lol = ep - (rc & 15), hil = ep + (rc >> 4);
+          if (lane == 0) lab[bb] = -1;
+          if (lane <= hil - lol) flag[lol + lane - base] = 1;
+        }
+      }
+    }
+    LSTAMP_ACC(7);
+    if (t == 0) s_ncorner = ncorner;
+  }
+  __syncthreads();
+  // surfaceCloudScan (:265-269): sector positions k in [sp, ep] with label
+  // <= 0, in position order -- one block-wide compaction over the ring
+  {
+    const int per = (end - start + 1 + kFeatThreads - 1) / kFeatThreads;
+    const int q0 = start + t * per, q1 = min(q0 + per, end + 1);
+    auto in_sector = [&](int k) {
+      bool in = false;
+#pragma unroll
+      for (int jj = 0; jj < 6; ++jj) in |= s_sp[jj] < s_ep[jj] && k >= s_sp[jj] && k <= s_ep[jj];
+      return in;
+    };
+    int cnt = 0;
+    for (int k = q0; k < q1; ++k) cnt += in_sector(k) && lab[k - base] <= 0;
+    int excl;
+    const int total = block_exclusive_scan<kFeatThreads>(cnt, scratch, excl);
+    for (int k = q0; k < q1; ++k)
+      if (in_sector(k) && lab[k - base] <= 0) slist[excl++] = k;
+    if (t == 0) s_nsurf = total;
+  }
+  __syncthreads();
+  LSTAMP(2);
+
+  // ---- corners of this ring (pick order)
+  const int nc = s_ncorner;
+  for (int q = t; q < nc; q += kFeatThreads) {
+    const int p = corner_pos[q];  // a ring position by construction
+    out.corner_stage[(int64_t)r * kCornerPerRing + q] = ci.xyzi[(p >= start && p <= end) ? p : start];
+  }
+  for (int q = base + t; q <= span_end; q += kFeatThreads)
+    if (q >= start && q <= end) out.label[q] = lab[q - base];
+  if (t == 0) out.corner_count[r] = nc;
+
+  // ---- pcl::VoxelGrid(leaf) on surfaceCloudScan
+  const int m = s_nsurf;
+  float4* dst = out.surf_stage + (start - 4);  // ring's first extracted index
+  if (m == 0) {
+    if (t == 0) out.surf_count[r] = 0;
+    return;
+  }
+  {
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int q = t; q < m; q += kFeatThreads) {
+      const float4 p = ci.xyzi[slist[q]];
+      mn[0] = fminf(mn[0], p.x);
+      mn[1] = fminf(mn[1], p.y);
+      mn[2] = fminf(mn[2], p.z);
+      mx[0] = fmaxf(mx[0], p.x);
+      mx[1] = fmaxf(mx[1], p.y);
+      mx[2] = fmaxf(mx[2], p.z);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+        mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+      }
+    }
+    __shared__ float wmn[kFeatThreads / 64][3], wmx[kFeatThreads / 64][3];
+    if (lane == 0)
+      for (int a = 0; a < 3; ++a) {
+        wmn[w][a] = mn[a];
+        wmx[w][a] = mx[a];
+      }
+    __syncthreads();
+    if (t == 0) {
+      for (int a = 0; a < 3; ++a) {
+        float a0 = wmn[0][a], a1 = wmx[0][a];
+        for (int q = 1; q < kFeatThreads / 64; ++q) {
+          a0 = fminf(a0, wmn[q][a]);
+          a1 = fmaxf(a1, wmx[q][a]);
+        }
+        s_min[a] = a0;
+        s_max[a] = a1;
+      }
+      const float inv = 1.0f / cfg.leaf;
+      const int64_t dx = (int64_t)((s_max[0] - s_min[0]) * inv) + 1;
+      const int64_t dy = (int64_t)((s_max[1] - s_min[1]) * inv) + 1;
+      const int64_t dz = (int64_t)((s_max[2] - s_min[2]) * inv) + 1;
+      s_overflow = dx * dy * dz > (int64_t)2147483647;
+      int divb[3];
+      for (int a = 0; a < 3; ++a) {
+        s_minb[a] = (int)floorf(s_min[a] * inv);
+        divb[a] = (int)floorf(s_max[a] * inv) - s_minb[a] + 1;
+      }
+      s_mul[0] = 1;
+      s_mul[1] = divb[0];
+      s_mul[2] = divb[0] * divb[1];
+    }
+    __syncthreads();
+  }
+  if (s_overflow) {  // PCL: "Integer indices would overflow", output = input
+    for (int q = t; q < m; q += kFeatThreads) dst[q] = ci.xyzi[slist[q]];
+    if (t == 0) out.surf_count[r] = m;
+    return;
+  }
+  const float inv = 1.0f / cfg.leaf;
+  const int P = max(pow2ceil(m), 64);
+  for (int q = t; q < P; q += kFeatThreads) {
+    uint64_t kk = ~0ull;
+    if (q < m) {
+      const float4 p = ci.xyzi[slist[q]];
+      const int i0 = (int)(floorf(p.x * inv) - (float)s_minb[0]);
+      const int i1 = (int)(floorf(p.y * inv) - (float)s_minb[1]);
+      const int i2 = (int)(floorf(p.z * inv) - (float)s_minb[2]);
+      const uint32_t idx = (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
+      kk = ((uint64_t)idx << 32) | (uint32_t)q;
+    }
+    keys[q] = kk;
+  }
+  __syncthreads();
+  LSTAMP(3);
+  if (P <= 2 * kFeatThreads)
+    bitonic_sort_shfl<kFeatThreads>(keys, P);
+  else
+    bitonic_sort<kFeatThreads>(keys, P);
+  LSTAMP(4);
+  // stage the points in sorted order in LDS: the per-voxel folds below read LDS
+  for (int q = t; q < m; q += kFeatThreads) vp[q] = ci.xyzi[slist[(uint32_t)keys[q]]];
+  __syncthreads();
+  // voxel runs: a thread per run start, centroid in point order
+  const int per = (m + kFeatThreads - 1) / kFeatThreads;
+  const int q0 = t * per, q1 = min(q0 + per, m);
+  int starts = 0;
+  for (int q = q0; q < q1; ++q) starts += (q == 0) || ((keys[q] >> 32) != (keys[q - 1] >> 32));
+  int excl;
+  const int nvox = block_exclusive_scan<kFeatThreads>(starts, scratch, excl);
+  int o = excl;
+  for (int q = q0; q < q1; ++q) {
+    if (!((q == 0) || ((keys[q] >> 32) != (keys[q - 1] >> 32)))) continue;
+    const uint32_t id = (uint32_t)(keys[q] >> 32);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int e = q;
+    for (; e < m && (uint32_t)(keys[e] >> 32) == id; ++e) {
+      const float4 p = vp[e];
+      s0 += p.x;
+      s1 += p.y;
+      s2 += p.z;
+      s3 += p.w;
+    }
+    const float cnt = (float)(e - q);
+    dst[o++] = make_float4(s0 / cnt, s1 / cnt, s2 / cnt, s3 / cnt);
+  }
+  if (t == 0) out.surf_count[r] = nvox;
+  LSTAMP(5);
+}
+
+__global__ __launch_bounds__(256) void k_lio_concat(int n_scan, const int32_t* start_ring,
+                                                    FeatOut f, float4* corner, float4* surface,
+                                                    int64_t* counts /* n_corner, n_surface */) {
+  __shared__ int s_co, s_so;
+  const int r = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int co = 0, so = 0;
+    for (int q = 0; q < r; ++q) {
+      co += f.corner_count[q];
+      so += f.surf_count[q];
+    }
+    s_co = co;
+    s_so = so;
+    if (r == n_scan - 1) {
+      counts[0] = co + f.corner_count[r];
+      counts[1] = so + f.surf_count[r];
+    }
+  }
+  __syncthreads();
+  const int nc = f.corner_count[r], ns = f.surf_count[r];
+  for (int q = threadIdx.x; q < nc; q += 256)
+    corner[s_co + q] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
+  const float4* src = f.surf_stage + (start_ring[r] - 4);
+  for (int q = threadIdx.x; q < ns; q += 256) surface[s_so + q] = src[q];
+}
+
+}  // namespace lio
+}  // namespace slio
+
+using namespace slio;
+using namespace slio::lio;
+
+struct slio_lio {
+  slio_lio_params prm{};
+  Geo g{};
+  hipStream_t own = nullptr, stream = nullptr;
+  int64_t cap = 0, cells = 0;
+  // input
+  float *x = nullptr, *y = nullptr, *z = nullptr, *in = nullptr, *time = nullptr;
+  uint16_t* ring = nullptr;
+  int64_t n = 0;
+  // deskew
+  double *it = nullptr, *rx = nullptr, *ry = nullptr, *rz = nullptr;
+  int n_imu = 0;
+  double t0 = 0.0;
+  int deskew = 0;
+  // projection
+  uint32_t* owner = nullptr;  // cells + 1
+  float* range_mat = nullptr;
+  float4* full = nullptr;
+  int32_t* row_count = nullptr;     // n_scan * kFillSplit partial counts
+  uint32_t* block_first = nullptr;  // per claim block: smallest valid point index
+  // cloud_info
+  int32_t *start_ring = nullptr, *end_ring = nullptr, *col_ind = nullptr, *n_ext = nullptr;
+  float* prange = nullptr;
+  float4* xyzi = nullptr;
+  // features
+  float* curvature = nullptr;
+  uint8_t* picked0 = nullptr;
+  int32_t* label = nullptr;
+  float4* corner_stage = nullptr;
+  int32_t* corner_count = nullptr;
+  float4* surf_stage = nullptr;
+  int32_t* surf_count = nullptr;
+  float4* corner = nullptr;
+  float4* surface = nullptr;
+  int64_t* counts = nullptr;  // device: n_corner, n_surface
+  int64_t* h_counts = nullptr;  // pinned: n_ext, n_corner, n_surface
+  FeatCfg fc{};
+  size_t feat_smem = 0;
+  bool ran = false;
+};
+
+namespace {
+
+void lio_free(slio_lio* h) {
+  void* dev[] = {h->x, h->y, h->z, h->in, h->time, h->ring, h->it, h->rx, h->ry, h->rz,
+                 h->owner, h->range_mat, h->full, h->row_count, h->block_first,
+                 h->start_ring, h->end_ring,
+                 h->col_ind, h->n_ext, h->prange, h->xyzi, h->curvature, h->picked0, h->label,
+                 h->corner_stage, h->corner_count, h->surf_stage, h->surf_count, h->corner,
+                 h->surface, h->counts};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  if (h->h_counts) (void)hipHostFree(h->h_counts);
+  if (h->own) (void)hipStreamDestroy(h->own);
+}
+
+#define LIO_CHECK_H(h)                    \
+  do {                                    \
+    if (!(h)) {                           \
+      set_error("null slio_lio handle");  \
+      return SLIO_EINVAL;                 \
+    }                                     \
+    LIO_HIP(hipSetDevice((h)->prm.device)); \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int slio_lio_params_default(slio_lio_params* p) {
+  if (!p) return SLIO_EINVAL;
+  std::memset(p, 0, sizeof(*p));
+  p->n_scan = 16;
+  p->horizon_scan = 1800;
+  p->downsample_rate = 1;
+  p->lidar_min_range = 1.0f;
+  p->lidar_max_range = 1000.0f;
+  p->edge_threshold = 1.0f;
+  p->surf_threshold = 0.1f;
+  p->surf_leaf_size = 0.4f;
+  return SLIO_OK;
+}
+
+int slio_lio_create(slio_lio_handle* out, const slio_lio_params* p) {
+  if (!out || !p) {
+    set_error("slio_lio_create: null argument");
+    return SLIO_EINVAL;
+  }
+  *out = nullptr;
+  if (p->n_scan <= 0 || p->horizon_scan <= 0 || p->horizon_scan > 65536 || p->downsample_rate <= 0 ||
+      !(p->surf_leaf_size > 0.0f) || p->max_points < 0 || p->n_scan > 65535) {
+    set_error("slio_lio_create: bad n_scan / horizon_scan / downsample_rate / leaf / max_points");
+    return SLIO_EINVAL;
+  }
+  int ndev = 0;
+  LIO_HIP(hipGetDeviceCount(&ndev));
+  if (p->device < 0 || p->device >= ndev) {
+    set_error("slio_lio_create: no such HIP device");
+    return SLIO_EDEVICE;
+  }
+  LIO_HIP(hipSetDevice(p->device));
+  auto* h = new slio_lio();
+  h->prm = *p;
+  h->cells = (int64_t)p->n_scan * p->horizon_scan;
+  h->cap = p->max_points > 0 ? p->max_points : h->cells;
+  h->g = Geo{p->n_scan, p->horizon_scan, p->downsample_rate, p->lidar_min_range,
+             p->lidar_max_range, (float)(360.0 / float(p->horizon_scan)), h->cells};
+  const int64_t C = h->cells, N = h->cap;
+  hipError_t e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
+  h->stream = h->own;
+#define A(ptr, bytes) \
+  if (!e) e = hipMalloc(reinterpret_cast<void**>(&(ptr)), (bytes))
+  A(h->x, 4 * N);
+  A(h->y, 4 * N);
+  A(h->z, 4 * N);
+  A(h->in, 4 * N);
+  A(h->time, 4 * N);
+  A(h->ring, 2 * N);
+  A(h->it, 8 * kMaxImu);
+  A(h->rx, 8 * kMaxImu);
+  A(h->ry, 8 * kMaxImu);
+  A(h->rz, 8 * kMaxImu);
+  A(h->owner, 4 * (C + 1));
+  A(h->range_mat, 4 * C);
+  A(h->full, 16 * C);
+  A(h->row_count, 4 * p->n_scan * kFillSplit);
+  A(h->block_first, 4 * ((N + 255) / 256 + 1));
+  A(h->start_ring, 4 * p->n_scan);
+  A(h->end_ring, 4 * p->n_scan);
+  A(h->col_ind, 4 * C);
+  A(h->n_ext, 4);
+  A(h->prange, 4 * C);
+  A(h->xyzi, 16 * C);
+  A(h->curvature, 4 * C);
+  A(h->picked0, C);
+  A(h->label, 4 * C);
+  A(h->corner_stage, 16 * (int64_t)p->n_scan * kCornerPerRing);
+  A(h->corner_count, 4 * p->n_scan);
+  A(h->surf_stage, 16 * C);
+  A(h->surf_count, 4 * p->n_scan);
+  A(h->corner, 16 * (int64_t)p->n_scan * kCornerPerRing);
+  A(h->surface, 16 * C);
+  A(h->counts, 16);
+#undef A
+  if (!e) e = hipHostMalloc(reinterpret_cast<void**>(&h->h_counts), 3 * sizeof(int64_t));
+  if (e) {
+    set_error(std::string("slio_lio_create: ") + hipGetErrorString(e));
+    lio_free(h);
+    delete h;
+    return SLIO_ENOMEM;
+  }
+  const int H = p->horizon_scan;
+  h->fc.edge_thr = p->edge_threshold;
+  h->fc.surf_thr = p->surf_threshold;
+  h->fc.leaf = p->surf_leaf_size;
+  h->fc.sort_cap = 64;
+  while (h->fc.sort_cap < H / 6 + 2) h->fc.sort_cap <<= 1;
+  h->fc.vox_cap = 64;
+  while (h->fc.vox_cap < H) h->fc.vox_cap <<= 1;
+  h->fc.ring_cap = H + 16;
+  const int kcap = std::max(6 * h->fc.sort_cap, h->fc.vox_cap);
+  h->feat_smem = 8 * (size_t)(kcap + 6 * h->fc.sort_cap) + 16 * (size_t)h->fc.vox_cap +
+                 (4 + 4 + 4 + 1 + 1 + 1) * (size_t)h->fc.ring_cap + 16;
+  if (6 * h->fc.sort_cap > 4 * kFeatThreads) {
+    set_error("slio_lio_create: horizon_scan too large for the sector sort");
+    lio_free(h);
+    delete h;
+    return SLIO_EINVAL;
+  }
+  if (h->feat_smem > 160 * 1024 - 2048) {
+    set_error("slio_lio_create: horizon_scan too large for the per-ring LDS layout");
+    lio_free(h);
+    delete h;
+    return SLIO_EINVAL;
+  }
+  if (h->feat_smem > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)k_lio_features, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)h->feat_smem);
+  *out = h;
+  return SLIO_OK;
+}
+
+int slio_lio_destroy(slio_lio_handle h) {
+  if (!h) return SLIO_OK;
+  (void)hipSetDevice(h->prm.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  lio_free(h);
+  delete h;
+  return SLIO_OK;
+}
+
+int slio_lio_set_stream(slio_lio_handle h, void* stream) {
+  LIO_CHECK_H(h);
+  h->stream = stream ? (hipStream_t)stream : h->own;
+  return SLIO_OK;
+}
+
+int slio_lio_set_deskew(slio_lio_handle h, const double* imu_time, const double* rot_x,
+                        const double* rot_y, const double* rot_z, int32_t n_imu,
+                        double time_scan_cur, int32_t enabled) {
+  LIO_CHECK_H(h);
+  if (enabled && (n_imu < 1 || n_imu > kMaxImu || !imu_time || !rot_x || !rot_y || !rot_z)) {
+    set_error("slio_lio_set_deskew: need 1 <= n_imu <= 2000 and all four tables");
+    return SLIO_EINVAL;
+  }
+  h->deskew = enabled ? 1 : 0;
+  h->n_imu = enabled ? n_imu : 0;
+  h->t0 = time_scan_cur;
+  if (enabled) {
+    LIO_HIP(hipMemcpyAsync(h->it, imu_time, 8 * n_imu, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->rx, rot_x, 8 * n_imu, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->ry, rot_y, 8 * n_imu, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->rz, rot_z, 8 * n_imu, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipStreamSynchronize(h->stream));  // host tables may be freed on return
+  }
+  return SLIO_OK;
+}
+
+int slio_lio_upload(slio_lio_handle h, const float* x, const float* y, const float* z,
+                    const float* intensity, const uint16_t* ring, const float* time, int64_t n) {
+  LIO_CHECK_H(h);
+  if (n < 0 || (n > 0 && (!x || !y || !z || !intensity || !ring || !time))) {
+    set_error("slio_lio_upload: bad arguments");
+    return SLIO_EINVAL;
+  }
+  if (n > h->cap || n >= (int64_t)kNone) {
+    set_error("slio_lio_upload: scan exceeds max_points");
+    return SLIO_ECAPACITY;
+  }
+  h->n = n;
+  if (n > 0) {
+    LIO_HIP(hipMemcpyAsync(h->x, x, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->y, y, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->z, z, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->in, intensity, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->ring, ring, 2 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->time, time, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipStreamSynchronize(h->stream));
+  }
+  h->ran = false;
+  return SLIO_OK;
+}
+
+int slio_lio_run_async(slio_lio_handle h) {
+  LIO_CHECK_H(h);
+  const Geo& g = h->g;
+  const int R = g.n_scan;
+  LIO_HIP(hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream));
+  const In in{h->x, h->y, h->z, h->in, h->ring, h->time, h->n};
+  const int nclaim = (int)((h->n + 255) / 256);
+  if (h->n > 0)
+    k_lio_claim<<<nclaim, 256, 0, h->stream>>>(in, g, h->owner, h->block_first);
+  const Deskew d{h->it, h->rx, h->ry, h->rz, h->n_imu - 1, h->t0, h->deskew};
+  k_lio_fill<<<dim3(R, kFillSplit), kFillThreads, 0, h->stream>>>(
+      in, g, h->owner, h->block_first, nclaim, d, h->range_mat, h->full, h->row_count);
+  const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->prange, h->xyzi, h->n_ext};
+  k_lio_extract<<<R, kRowThreads, 0, h->stream>>>(g, h->range_mat, h->full, h->row_count, ci);
+  k_lio_smooth<<<(unsigned)((g.cells + 255) / 256), 256, 0, h->stream>>>(
+      h->prange, h->col_ind, h->n_ext, h->curvature, h->picked0, h->label);
+  const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count};
+  k_lio_features<<<R, kFeatThreads, h->feat_smem, h->stream>>>(ci, h->curvature, h->picked0,
+                                                                 h->fc, fo);
+  k_lio_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
+  LIO_HIP(hipGetLastError());
+  h->ran = true;
+  return SLIO_OK;
+}
+
+int slio_lio_get_counts(slio_lio_handle h, slio_lio_counts* c) {
+  LIO_CHECK_H(h);
+  if (!h->ran) {
+    set_error("slio_lio: no scan processed");
+    return SLIO_ESTATE;
+  }
+  int32_t ne = 0;
+  LIO_HIP(hipMemcpyAsync(h->h_counts + 1, h->counts, 16, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipMemcpyAsync(&ne, h->n_ext, 4, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  h->h_counts[0] = ne;
+  if (c) {
+    c->n_extracted = h->h_counts[0];
+    c->n_corner = h->h_counts[1];
+    c->n_surface = h->h_counts[2];
+  }
+  return SLIO_OK;
+}
+
+int slio_lio_run(slio_lio_handle h, slio_lio_counts* c) {
+  const int rc = slio_lio_run_async(h);
+  if (rc) return rc;
+  return slio_lio_get_counts(h, c);
+}
+
+int slio_lio_get_range_image(slio_lio_handle h, float* range_mat, int32_t* cell_point) {
+  LIO_CHECK_H(h);
+  if (!h->ran) {
+    set_error("slio_lio: no scan processed");
+    return SLIO_ESTATE;
+  }
+  if (range_mat)
+    LIO_HIP(hipMemcpyAsync(range_mat, h->range_mat, 4 * h->cells, hipMemcpyDeviceToHost, h->stream));
+  if (cell_point)  // kNone (0xffffffff) reads back as -1
+    LIO_HIP(hipMemcpyAsync(cell_point, h->owner, 4 * h->cells, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+int slio_lio_get_cloud_info(slio_lio_handle h, int32_t* start_ring, int32_t* end_ring,
+                            int32_t* col_ind, float* point_range, float* xyzi) {
+  slio_lio_counts c;
+  const int rc = slio_lio_get_counts(h, &c);
+  if (rc) return rc;
+  const int64_t n = c.n_extracted, R = h->g.n_scan;
+  if (start_ring) LIO_HIP(hipMemcpyAsync(start_ring, h->start_ring, 4 * R, hipMemcpyDeviceToHost, h->stream));
+  if (end_ring) LIO_HIP(hipMemcpyAsync(end_ring, h->end_ring, 4 * R, hipMemcpyDeviceToHost, h->stream));
+  if (n > 0) {
+    if (col_ind) LIO_HIP(hipMemcpyAsync(col_ind, h->col_ind, 4 * n, hipMemcpyDeviceToHost, h->stream));
+    if (point_range) LIO_HIP(hipMemcpyAsync(point_range, h->prange, 4 * n, hipMemcpyDeviceToHost, h->stream));
+    if (xyzi) LIO_HIP(hipMemcpyAsync(xyzi, h->xyzi, 16 * n, hipMemcpyDeviceToHost, h->stream));
+  }
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+int slio_lio_get_features(slio_lio_handle h, float* curvature, uint8_t* picked, int32_t* label) {
+  slio_lio_counts c;
+  const int rc = slio_lio_get_counts(h, &c);
+  if (rc) return rc;
+  const int64_t n = c.n_extracted;
+  if (n > 0) {
+    if (curvature) LIO_HIP(hipMemcpyAsync(curvature, h->curvature, 4 * n, hipMemcpyDeviceToHost, h->stream));
+    if (picked) LIO_HIP(hipMemcpyAsync(picked, h->picked0, n, hipMemcpyDeviceToHost, h->stream));
+    if (label) LIO_HIP(hipMemcpyAsync(label, h->label, 4 * n, hipMemcpyDeviceToHost, h->stream));
+  }
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+int slio_lio_get_clouds(slio_lio_handle h, float* corner_xyzi, float* surface_xyzi) {
+  slio_lio_counts c;
+  const int rc = slio_lio_get_counts(h, &c);
+  if (rc) return rc;
+  if (corner_xyzi && c.n_corner > 0)
+    LIO_HIP(hipMemcpyAsync(corner_xyzi, h->corner, 16 * c.n_corner, hipMemcpyDeviceToHost, h->stream));
+  if (surface_xyzi && c.n_surface > 0)
+    LIO_HIP(hipMemcpyAsync(surface_xyzi, h->surface, 16 * c.n_surface, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+}  // extern "C"
+
+#ifdef SLIO_LIO_STAMP
+extern "C" int slio_dbg_lio_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstamp), sizeof(g_lstamp)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -261,3 +261,46 @@ def make_problem(n_map: int, n_scan: int, seed: int = 20261015, pattern: str = "
         np.savez(fn, map=mp, body=fr.body, gt_rot=fr.gt_rot, gt_pos=fr.gt_pos,
                  init_rot=fr.init_rot, init_pos=fr.init_pos)
     return mp, fr
+
+
+# ---------------------------------------------------------------- C3: Ouster
+OUSTER_FOV_DEG = 16.6  # OS1-64: elevation -16.6 .. +16.6 deg
+
+
+def make_ouster_scan(seed: int = 20261015, n_scan: int = 64, horizon: int = 2048,
+                     yaw_rate: float = 0.5, dropout: float = 0.05, n_map_scene: int = 2_000_000,
+                     time_scan_cur: float = 1000.0) -> dict:
+    """One OS1-64-like sweep: n_scan x horizon returns in
+    ring-major order (the PointCloud2 layout of the Ouster driver), per-point
+    relative time from the column (t u32 ns -> t * 1e-9f, imageProjection.cpp
+    :244-258), azimuth jitter of +-0.6 column so that cells collide and go
+    empty, `dropout` zero returns, and a 200 Hz IMU stream with angular
+    velocity (0, 0, yaw_rate) covering the sweep.  The sensor turns during the
+    sweep, so each point is in the sensor frame of its own capture time."""
+    scene = make_scene(seed, n_map_scene)
+    rng = np.random.default_rng(seed + 3)
+    yaw0 = rng.uniform(-np.pi, np.pi)
+    org = np.array([rng.uniform(-3, 3), rng.uniform(-3, 3), 1.8])
+    res = 2 * np.pi / horizon
+    rows = np.repeat(np.arange(n_scan), horizon)
+    cols = np.tile(np.arange(horizon), n_scan)
+    el = np.deg2rad(-OUSTER_FOV_DEG + rows * (2 * OUSTER_FOV_DEG / (n_scan - 1)))
+    az = (cols - horizon // 2 + rng.uniform(-0.6, 0.6, rows.size)) * res
+    t_ns = np.round(cols * (1e8 / horizon)).astype(np.uint32)
+    t_rel = t_ns.astype(np.float32) * np.float32(1e-9)
+    dl = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], 1)
+    yaw = yaw0 + yaw_rate * t_rel.astype(np.float64)
+    cy, sy = np.cos(yaw), np.sin(yaw)
+    dw = np.stack([cy * dl[:, 0] - sy * dl[:, 1], sy * dl[:, 0] + cy * dl[:, 1], dl[:, 2]], 1)
+    rng_m = _cast(scene, org, dw, 120.0)
+    ok = np.isfinite(rng_m) & (rng.uniform(size=rows.size) >= dropout)
+    r = np.where(ok, rng_m + rng.normal(0.0, 0.01, rows.size), 0.0)
+    pts = (dl * r[:, None]).astype(np.float32)  # sensor frame at capture time
+    intensity = rng.uniform(0.0, 255.0, rows.size).astype(np.float32)
+    t_end = time_scan_cur + float(t_rel[-1])
+    stamps = np.arange(time_scan_cur - 0.0475, t_end + 0.05, 0.005)
+    gyro = np.tile([0.0, 0.0, yaw_rate], (stamps.size, 1)) + rng.normal(0, 1e-3, (stamps.size, 3))
+    return dict(x=np.ascontiguousarray(pts[:, 0]), y=np.ascontiguousarray(pts[:, 1]),
+                z=np.ascontiguousarray(pts[:, 2]), intensity=intensity,
+                ring=rows.astype(np.uint16), time=t_rel, imu_stamps=stamps, imu_gyro=gyro,
+                time_scan_cur=time_scan_cur, time_scan_end=t_end, n_scan=n_scan, horizon=horizon)

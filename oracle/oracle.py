@@ -23,8 +23,8 @@ _lib = None
 
 
 def build() -> str:
-    src = os.path.join(HERE, "slio_oracle.cpp")
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "Makefile")]
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
     return LIB
 
@@ -144,3 +144,82 @@ def ikf_update(tree: Tree, body, state26, P, R=0.001, maximum_iter=4, extrinsic=
                                sel.ctypes.data_as(_U8P), st.ctypes.data_as(_I64P))
     assert rc == 0, rc
     return s, Pm, st, idx, sqd, sel
+
+
+# ---------------------------------------------------------------- LIO-SAM front-end
+def _bind_frontend(lib):
+    if getattr(lib, "_fe_bound", False):
+        return
+    _U16P = C.POINTER(C.c_uint16)
+    lib.orc_lio_project.restype = C.c_int64
+    lib.orc_lio_project.argtypes = [C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                    _FP, _FP, _FP, _FP, _U16P, _FP, C.c_int64,
+                                    _DP, _DP, _DP, _DP, C.c_int, C.c_double, C.c_int,
+                                    _FP, _IP, _IP, _IP, _IP, _FP, _FP]
+    lib.orc_lio_features.restype = C.c_int
+    lib.orc_lio_features.argtypes = [C.c_int, C.c_float, C.c_float, C.c_float, _IP, _IP, _IP,
+                                     _FP, _FP, C.c_int64, _FP, _U8P, _IP, _FP, _I64P, _FP, _I64P]
+    lib._fe_bound = True
+
+
+def lio_project(scan: dict, n_scan: int, horizon: int, deskew_table=None, downsample_rate: int = 1,
+                min_range: float = 1.0, max_range: float = 1000.0) -> dict:
+    """imageProjection.cpp:610-678 on the CPU.  deskew_table = (imuTime,
+    rotX, rotY, rotZ, available) from frontend.imu_deskew_table or None."""
+    lib = load()
+    _bind_frontend(lib)
+    x, y, z, it = (_f(scan[k]) for k in ("x", "y", "z", "intensity"))
+    ring = np.ascontiguousarray(scan["ring"], dtype=np.uint16)
+    tm = _f(scan["time"])
+    n = x.shape[0]
+    if deskew_table is not None and deskew_table[4]:
+        tb = [np.ascontiguousarray(v, dtype=np.float64) for v in deskew_table[:4]]
+        on = 1
+    else:
+        tb = [np.zeros(1) for _ in range(4)]
+        on = 0
+    cells = n_scan * horizon
+    rm = np.empty(cells, np.float32)
+    own = np.empty(cells, np.int32)
+    st = np.empty(n_scan, np.int32)
+    en = np.empty(n_scan, np.int32)
+    ci = np.empty(cells, np.int32)
+    pr = np.empty(cells, np.float32)
+    xyzi = np.empty((cells, 4), np.float32)
+    ne = lib.orc_lio_project(n_scan, horizon, downsample_rate, min_range, max_range,
+                             *(a.ctypes.data_as(_FP) for a in (x, y, z, it)),
+                             ring.ctypes.data_as(C.POINTER(C.c_uint16)), tm.ctypes.data_as(_FP), n,
+                             *(a.ctypes.data_as(_DP) for a in tb), len(tb[0]),
+                             float(scan.get("time_scan_cur", 0.0)), on,
+                             rm.ctypes.data_as(_FP), own.ctypes.data_as(_IP),
+                             st.ctypes.data_as(_IP), en.ctypes.data_as(_IP), ci.ctypes.data_as(_IP),
+                             pr.ctypes.data_as(_FP), xyzi.ctypes.data_as(_FP))
+    return dict(range_mat=rm.reshape(n_scan, horizon), cell_point=own.reshape(n_scan, horizon),
+                startRingIndex=st, endRingIndex=en, pointColInd=ci[:ne].copy(),
+                pointRange=pr[:ne].copy(), cloud_deskewed=xyzi[:ne].copy())
+
+
+def lio_features(info: dict, n_scan: int, edge_threshold: float = 1.0, surf_threshold: float = 0.1,
+                 leaf: float = 0.4) -> dict:
+    """featureExtraction.cpp:108-296 on the CPU."""
+    lib = load()
+    _bind_frontend(lib)
+    n = info["pointRange"].shape[0]
+    st = np.ascontiguousarray(info["startRingIndex"], np.int32)
+    en = np.ascontiguousarray(info["endRingIndex"], np.int32)
+    ci = np.ascontiguousarray(info["pointColInd"], np.int32)
+    pr = _f(info["pointRange"])
+    xyzi = _f(info["cloud_deskewed"])
+    cv = np.empty(n, np.float32)
+    pk = np.empty(n, np.uint8)
+    lb = np.empty(n, np.int32)
+    co = np.empty((max(n, 1), 4), np.float32)
+    su = np.empty((max(n, 1), 4), np.float32)
+    nc, ns = C.c_int64(), C.c_int64()
+    lib.orc_lio_features(n_scan, edge_threshold, surf_threshold, leaf, st.ctypes.data_as(_IP),
+                         en.ctypes.data_as(_IP), ci.ctypes.data_as(_IP), pr.ctypes.data_as(_FP),
+                         xyzi.ctypes.data_as(_FP), n, cv.ctypes.data_as(_FP),
+                         pk.ctypes.data_as(_U8P), lb.ctypes.data_as(_IP), co.ctypes.data_as(_FP),
+                         C.byref(nc), su.ctypes.data_as(_FP), C.byref(ns))
+    return dict(cloudCurvature=cv, cloudNeighborPicked=pk, cloudLabel=lb,
+                cloud_corner=co[:nc.value].copy(), cloud_surface=su[:ns.value].copy())

@@ -70,6 +70,17 @@ def test_bad_arguments_fail_loudly(lib):
     assert lib.slio_create(C.byref(h), C.byref(p)) == -1
     assert b"far_query_margin" in lib.slio_last_error()
     assert lib.slio_iterate_async(None, None, 1, 0, None) == -1
+    # front-end C-ABI (include/slio_frontend.h): argument checks before any device call
+    lp = L.SlioLioParams()
+    assert lib.slio_lio_params_default(C.byref(lp)) == 0
+    assert (lp.n_scan, lp.horizon_scan, lp.downsample_rate) == (16, 1800, 1)
+    assert abs(lp.surf_leaf_size - 0.4) < 1e-7 and lp.edge_threshold == 1.0
+    assert lib.slio_lio_create(None, None) == -1
+    lp.n_scan = 0
+    assert lib.slio_lio_create(C.byref(h), C.byref(lp)) == -1
+    assert b"n_scan" in lib.slio_last_error()
+    assert lib.slio_lio_run_async(None) == -1
+    assert lib.slio_lio_destroy(None) == 0
 
 
 def test_reduce_super_matches_python_tree(lib):
