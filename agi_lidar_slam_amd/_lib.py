@@ -24,6 +24,7 @@ SLIO_KERNEL_SEARCH = 0
 SLIO_KERNEL_REUSE = 1
 SLIO_KERNEL_SUPER = 2
 SLIO_PROFILE_KEEP = 16
+SLIO_LIO_PROFILE_KEEP = 16
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ECAPACITY", -5: "ESTATE"}
 
@@ -156,6 +157,8 @@ SIGNATURES = {
     "slio_lio_get_cloud_info": (C.c_int, [_P, _IP, _IP, _IP, _FP, _FP]),
     "slio_lio_get_features": (C.c_int, [_P, _FP, _U8P, _IP]),
     "slio_lio_get_clouds": (C.c_int, [_P, _FP, _FP]),
+    "slio_lio_profile": (C.c_int, [_P, C.c_int]),
+    "slio_lio_profile_read": (C.c_int, [_P, _DP, _I64P]),
 }
 
 _lib = None

@@ -27,6 +27,7 @@
 // oracle/frontend_oracle.cpp: float trig as correctly
 // rounded values (double evaluation), sort ties by point index, smoothness
 // entries the reference never initialises are never picked.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,6 +35,8 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "slio_common.hpp"
 #include "slio_frontend.h"
@@ -1011,11 +1014,34 @@ struct slio_lio {
   FeatCfg fc{};
   size_t feat_smem = 0;
   bool ran = false;
+  // k_lio_features timing
+  bool prof = false;
+  double prof_ms = 0.0;
+  int64_t prof_n = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
 };
 
 namespace {
 
+void lio_prof_drain(slio_lio* h) {
+  for (auto& p : h->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.second) == hipSuccess &&
+        hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+      h->prof_ms += ms;
+      h->prof_n += 1;
+    }
+    h->pool.push_back(p);
+  }
+  h->pending.clear();
+}
+
 void lio_free(slio_lio* h) {
+  lio_prof_drain(h);
+  for (auto& p : h->pool) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
   void* dev[] = {h->x, h->y, h->z, h->in, h->time, h->ring, h->it, h->rx, h->ry, h->rz,
                  h->owner, h->range_mat, h->full, h->row_count, h->block_first,
                  h->start_ring, h->end_ring,
@@ -1232,11 +1258,45 @@ int slio_lio_run_async(slio_lio_handle h) {
   k_lio_smooth<<<(unsigned)((g.cells + 255) / 256), 256, 0, h->stream>>>(
       h->prange, h->col_ind, h->n_ext, h->curvature, h->picked0, h->label);
   const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count};
-  k_lio_features<<<R, kFeatThreads, h->feat_smem, h->stream>>>(ci, h->curvature, h->picked0,
-                                                                 h->fc, fo);
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (h->prof) {
+    if (h->pending.size() > 256) lio_prof_drain(h);
+    if (!h->pool.empty()) {
+      ev = h->pool.back();
+      h->pool.pop_back();
+    } else {
+      LIO_HIP(hipEventCreate(&ev.first));
+      LIO_HIP(hipEventCreate(&ev.second));
+    }
+    h->pending.push_back(ev);
+  }
+  hipExtLaunchKernelGGL(k_lio_features, dim3(R), dim3(kFeatThreads), (uint32_t)h->feat_smem,
+                        h->stream, ev.first, ev.second, 0, ci, (const float*)h->curvature,
+                        (const uint8_t*)h->picked0, h->fc, fo);
   k_lio_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
   LIO_HIP(hipGetLastError());
   h->ran = true;
+  return SLIO_OK;
+}
+
+int slio_lio_profile(slio_lio_handle h, int enable) {
+  LIO_CHECK_H(h);
+  const bool keep = (enable & SLIO_LIO_PROFILE_KEEP) != 0;
+  h->prof = (enable & ~SLIO_LIO_PROFILE_KEEP) != 0;
+  if (!keep) {  // pausing / resuming never waits; a reset drains first
+    lio_prof_drain(h);
+    h->prof_ms = 0.0;
+    h->prof_n = 0;
+  }
+  return SLIO_OK;
+}
+
+int slio_lio_profile_read(slio_lio_handle h, double* ms, int64_t* launches) {
+  LIO_CHECK_H(h);
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  lio_prof_drain(h);
+  if (ms) *ms = h->prof_ms;
+  if (launches) *launches = h->prof_n;
   return SLIO_OK;
 }
 

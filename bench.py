@@ -47,6 +47,127 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def bench_c3(args, rank, world, dev, dist):
+    """C3: LIO-SAM imageProjection + featureExtraction on a
+    64 x 2048 Ouster scan (131 072 points).  One step = one scan through the
+    whole device front-end with the scan resident in HBM.  N > 1: replicas
+    (every rank its own scan stream, no collective): value = scans of all
+    ranks / max-over-ranks time."""
+    import ctypes as C
+    from agi_lidar_slam_amd import _lib as L, build, synth
+    from agi_lidar_slam_amd.frontend import LioSamFrontEnd, LioSamParams, imu_deskew_table
+
+    if rank == 0:
+        build.build()
+    if world > 1:
+        dist.barrier()
+    L.load()
+    sc = synth.make_ouster_scan(seed=20261015 + rank)
+    tb = imu_deskew_table(sc["imu_stamps"], sc["imu_gyro"], sc["time_scan_cur"], sc["time_scan_end"])
+    fe = LioSamFrontEnd(LioSamParams(N_SCAN=64, Horizon_SCAN=2048), device=dev)
+    fe.set_deskew(*tb[:4], sc["time_scan_cur"], tb[4])
+    fe.upload(sc["x"], sc["y"], sc["z"], sc["intensity"], sc["ring"], sc["time"])
+    lib, h = fe.lib, fe.h
+    for _ in range(args.warmup):
+        fe.run()
+    counts = L.SlioLioCounts()
+    lib.slio_lio_profile(h, 0)
+    every = max(1, args.timing_every)
+    if world > 1:
+        dist.barrier()
+    L.check(lib.slio_lio_get_counts(h, C.byref(counts)), "counts")
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        timed = not args.no_kernel_timing and k % every == 0
+        if timed:
+            lib.slio_lio_profile(h, 1 | L.SLIO_LIO_PROFILE_KEEP)
+        rc = lib.slio_lio_run_async(h)
+        if rc:
+            L.check(rc, "slio_lio_run_async")
+        if timed:
+            lib.slio_lio_profile(h, L.SLIO_LIO_PROFILE_KEEP)
+    L.check(lib.slio_lio_get_counts(h, C.byref(counts)), "counts")  # waits for the stream
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ms, nl = C.c_double(), C.c_int64()
+    lib.slio_lio_profile_read(h, C.byref(ms), C.byref(nl))
+    if world > 1:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    value = args.steps * world / el
+    avg_s = (ms.value / max(nl.value, 1)) * 1e-3
+    n_ext, nc, ns = counts.n_extracted, counts.n_corner, counts.n_surface
+    # k_lio_features compulsory bytes: per extracted point curvature 4 + column 4
+    # + flag 1 + label 4 + the point 16 (surface / corner gathers), and the
+    # corner / surface outputs 16 B each
+    alg_bytes = 29 * n_ext + 16 * (nc + ns)
+    achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        n = max(1, args.cpu_scans_c3)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            info = O.lio_project(sc, 64, 2048, tb)
+            O.lio_features(info, 64)
+        cel = time.perf_counter() - t0
+        cpu = {
+            "value": n / cel,
+            "unit": "scans/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": (f"{n} scans through the single-threaded C++ restatement of projectPointCloud + "
+                       f"cloudExtraction + calculateSmoothness + markOccludedPoints + extractFeatures "
+                       f"(+ per-ring VoxelGrid), same 64x2048 Ouster scan; host {cpu_model()}, "
+                       f"nproc {os.cpu_count()}"),
+        }
+    out = {
+        "metric": "LIO-SAM imageProjection + featureExtraction scans/sec, 64-ring Ouster 131k-pt scan",
+        "value": value,
+        "unit": "scans/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (points, ranges, curvature) + f64 (deskew interpolation, trig)",
+        "data": "synthetic (seeded urban scene, OS1-64-like 64 x 2048 sweep with IMU deskew)",
+        "config": {
+            "workload": ("C3: LIO-SAM ImageProjection::projectPointCloud/cloudExtraction + "
+                         "FeatureExtraction::calculateSmoothness/markOccludedPoints/extractFeatures, "
+                         "64 x 2048 Ouster scan, deskew on"),
+            "points_in": int(sc["x"].size),
+            "points_extracted": int(n_ext),
+            "corners": int(nc),
+            "surface": int(ns),
+            "parallelism": (f"replicas x{world}: one scan stream per GPU, no collective"
+                            if world > 1 else "single GPU"),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_lio_features",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": None,
+            "alg_bytes_per_launch": alg_bytes,
+            "avg_launch_us": avg_s * 1e6,
+            "launches": int(nl.value),
+            "timing": f"HIP events in the dispatch packet, 1 in {every} timed steps",
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    fe.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,6 +188,10 @@ def main():
     ap.add_argument("--host-loop", action="store_true",
                     help="run the 24x24 step on the host after every pass (slio_ikf_update)")
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+                    help="c2: IKF iterations/s, 100k Avia scan vs 10M map (BASELINE.json metric); "
+                         "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan")
+    ap.add_argument("--cpu-scans-c3", type=int, default=300)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "search_traffic.json"))
     args = ap.parse_args()
 
@@ -79,8 +204,13 @@ def main():
 
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl" if args.workload == "c2" else "gloo")
     dev = local_rank if world > 1 else 0
+    if args.workload == "c3":
+        bench_c3(args, rank, world, dev, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from agi_lidar_slam_amd import _lib as L, build, synth
 

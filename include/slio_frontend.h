@@ -75,6 +75,15 @@ int slio_lio_run_async(slio_lio_handle h);
 int slio_lio_run(slio_lio_handle h, slio_lio_counts* counts);
 int slio_lio_get_counts(slio_lio_handle h, slio_lio_counts* counts);
 
+/* Kernel timing: enable != 0 times every k_lio_features launch (the
+ * dominant kernel; start/stop hipEvents carried in the dispatch packet) and
+ * accumulates device milliseconds; 0 disables.  SLIO_LIO_PROFILE_KEEP keeps
+ * the totals (pause / resume).  Read: accumulated ms and launch count
+ * (synchronises the stream). */
+#define SLIO_LIO_PROFILE_KEEP 16
+int slio_lio_profile(slio_lio_handle h, int enable);
+int slio_lio_profile_read(slio_lio_handle h, double* ms, int64_t* launches);
+
 /* rangeMat (n_scan * horizon_scan, FLT_MAX = empty, :146) and, per cell, the
  * index of the input point that filled it (-1 = empty). Either may be NULL. */
 int slio_lio_get_range_image(slio_lio_handle h, float* range_mat, int32_t* cell_point);

@@ -15,6 +15,9 @@ for step in "$@"; do
     bench)
       timeout -k 10 600 python bench.py --steps 100 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 4; }
       cat gpurun_out/${tag}_bench.json ;;
+    benchc3)
+      timeout -k 10 600 python bench.py --workload c3 --steps 500 --warmup 10 > gpurun_out/${tag}_benchc3.json 2> gpurun_out/${tag}_benchc3.err || { echo "benchc3 failed"; tail -20 gpurun_out/${tag}_benchc3.err; exit 4; }
+      cat gpurun_out/${tag}_benchc3.json ;;
     benchh)
       timeout -k 10 600 python bench.py --steps 100 --warmup 5 --host-loop --no-cpu-baseline > gpurun_out/${tag}_benchh.json 2> gpurun_out/${tag}_benchh.err || { echo "benchh failed"; tail -20 gpurun_out/${tag}_benchh.err; exit 4; }
       cat gpurun_out/${tag}_benchh.json ;;
