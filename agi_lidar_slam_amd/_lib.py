@@ -99,6 +99,49 @@ class SlioLioCounts(C.Structure):
     _fields_ = [("n_extracted", C.c_int64), ("n_corner", C.c_int64), ("n_surface", C.c_int64)]
 
 
+class SlioLegoParams(C.Structure):
+    """slio_lego_params (include/slio_frontend.h)."""
+    _fields_ = [
+        ("device", C.c_int32),
+        ("n_scan", C.c_int32),
+        ("horizon_scan", C.c_int32),
+        ("ground_scan_ind", C.c_int32),
+        ("segment_valid_point_num", C.c_int32),
+        ("segment_valid_line_num", C.c_int32),
+        ("ang_res_x", C.c_float),
+        ("ang_res_y", C.c_float),
+        ("ang_bottom", C.c_float),
+        ("sensor_mount_angle", C.c_float),
+        ("segment_theta", C.c_float),
+        ("edge_threshold", C.c_float),
+        ("surf_threshold", C.c_float),
+        ("leaf_size", C.c_float),
+        ("scan_period", C.c_float),
+        ("max_points", C.c_int32),
+        ("reserved", C.c_int32 * 4),
+    ]
+
+
+class SlioLegoImu(C.Structure):
+    _fields_ = [("time", C.POINTER(C.c_double))] + [(n, C.POINTER(C.c_float)) for n in (
+        "roll", "pitch", "yaw", "velo_x", "velo_y", "velo_z", "shift_x", "shift_y", "shift_z",
+        "ang_x", "ang_y", "ang_z")] + [
+        ("pointer_last", C.c_int32), ("pointer_last_iteration", C.c_int32), ("que_len", C.c_int32),
+        ("time_scan_cur", C.c_double), ("ang_last", C.c_float * 3)]
+
+
+class SlioLegoImuOut(C.Structure):
+    _fields_ = [("rpy_start", C.c_float * 3), ("rpy_cur", C.c_float * 3),
+                ("velo_from_start", C.c_float * 3), ("angular_from_start", C.c_float * 3),
+                ("ang_last", C.c_float * 3), ("pointer_last_iteration", C.c_int32)]
+
+
+class SlioLegoCounts(C.Structure):
+    _fields_ = [("n_segmented", C.c_int64), ("n_outlier", C.c_int64), ("n_sharp", C.c_int64),
+                ("n_less_sharp", C.c_int64), ("n_flat", C.c_int64), ("n_less_flat", C.c_int64),
+                ("orientation", C.c_float * 3)]
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
 
 _P = C.c_void_p
@@ -159,6 +202,22 @@ SIGNATURES = {
     "slio_lio_get_clouds": (C.c_int, [_P, _FP, _FP]),
     "slio_lio_profile": (C.c_int, [_P, C.c_int]),
     "slio_lio_profile_read": (C.c_int, [_P, _DP, _I64P]),
+    # include/slio_frontend.h (LeGO-LOAM front-end)
+    "slio_lego_params_default": (C.c_int, [C.POINTER(SlioLegoParams)]),
+    "slio_lego_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioLegoParams)]),
+    "slio_lego_destroy": (C.c_int, [_P]),
+    "slio_lego_set_stream": (C.c_int, [_P, _P]),
+    "slio_lego_set_imu": (C.c_int, [_P, C.POINTER(SlioLegoImu)]),
+    "slio_lego_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
+    "slio_lego_run_async": (C.c_int, [_P]),
+    "slio_lego_run": (C.c_int, [_P, C.POINTER(SlioLegoCounts)]),
+    "slio_lego_get_counts": (C.c_int, [_P, C.POINTER(SlioLegoCounts)]),
+    "slio_lego_get_image": (C.c_int, [_P, _FP, _IP, C.POINTER(C.c_int8), _IP]),
+    "slio_lego_get_seg_info": (C.c_int, [_P, _IP, _IP, _U8P, _IP, _FP, _FP, _FP]),
+    "slio_lego_get_features": (C.c_int, [_P, _FP, _FP, _U8P, _IP, C.POINTER(SlioLegoImuOut)]),
+    "slio_lego_get_clouds": (C.c_int, [_P, _FP, _FP, _FP, _FP]),
+    "slio_lego_profile": (C.c_int, [_P, C.c_int]),
+    "slio_lego_profile_read": (C.c_int, [_P, _DP, _I64P]),
 }
 
 _lib = None

@@ -55,6 +55,8 @@ namespace lio {
 
 constexpr int kMaxImu = 2000;          // queueLength (imageProjection.cpp:35)
 constexpr int kCornerPerRing = 6 * 20;  // 6 sectors x 20 corners (featureExtraction.cpp:209)
+constexpr int kFlatPerRing = 6 * 4;     // LeGO-LOAM: 6 sectors x 4 flats (featureAssociation.cpp:952)
+enum FeatMode { kModeLio = 0, kModeLego = 1 };
 constexpr uint32_t kNone = 0xffffffffu;
 
 struct Geo {
@@ -551,10 +553,16 @@ __global__ __launch_bounds__(256) void k_lio_smooth(const float* __restrict__ r,
 
 struct FeatOut {
   int32_t* label;          // n_ext
-  float4* corner_stage;    // n_scan * kCornerPerRing
+  float4* corner_stage;    // n_scan * kCornerPerRing (pick order)
   int32_t* corner_count;   // n_scan
   float4* surf_stage;      // n_ext (ring r at its first extracted index)
   int32_t* surf_count;     // n_scan
+  // LeGO-LOAM only
+  int8_t* corner_sharp;    // n_scan * kCornerPerRing: 1 = cornerPointsSharp (label 2)
+  int32_t* sharp_count;    // n_scan
+  float4* flat_stage;      // n_scan * kFlatPerRing (pick order)
+  int32_t* flat_count;     // n_scan
+  const uint8_t* ground;   // segmentedCloudGroundFlag (n_ext)
 };
 
 struct FeatCfg {
@@ -594,7 +602,12 @@ __device__ unsigned long long g_lstamp[256 * 8];  // [ring][slot]
 #endif
 
 // one ring per workgroup
-__global__ __launch_bounds__(kFeatThreads) void k_lio_features(
+// MODE kModeLio: LIO-SAM extractFeatures (featureExtraction.cpp:183-296);
+// kModeLego: LeGO-LOAM extractFeatures (featureAssociation.cpp:883-1007):
+// edges only off the ground (labels 2 for the first 2 = sharp, 1 up to 20),
+// flats only on the ground, at most 4 per sector (the 4th does not suppress).
+template <int MODE>
+__global__ __launch_bounds__(kFeatThreads) void k_fe_features(
     const CloudInfo ci, const float* __restrict__ curvature, const uint8_t* __restrict__ picked0,
     FeatCfg cfg, FeatOut out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -611,8 +624,11 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
   volatile uint8_t* flag = reinterpret_cast<volatile uint8_t*>(slist + cfg.ring_cap);
   volatile int8_t* lab = reinterpret_cast<volatile int8_t*>(flag + cfg.ring_cap);
   uint8_t* reach = reinterpret_cast<uint8_t*>(const_cast<int8_t*>(lab) + cfg.ring_cap);
+  uint8_t* gfl = reach + cfg.ring_cap;  // LeGO: segmentedCloudGroundFlag
   __shared__ int s_nsurf, s_ncorner;
   __shared__ int corner_pos[kCornerPerRing];
+  __shared__ int flat_pos[kFlatPerRing];
+  __shared__ int s_nflat;
   __shared__ int scratch[kFeatThreads / 64 + 1];
   __shared__ float s_min[3], s_max[3];
   __shared__ int s_overflow, s_minb[3], s_mul[3];
@@ -624,12 +640,13 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
   const int base = max(start - 5, 0);
   const int span_end = min(end + 5, n - 1);  // last index touched
   LSTAMP(0);
-  int ncorner = 0;  // wavefront 0 counter (uniform)
+  int ncorner = 0, nflat = 0, nsharp = 0;  // wavefront 0 counters (uniform)
   for (int q = base + t; q <= span_end; q += kFeatThreads) {
     curv[q - base] = curvature[q];
     col[q - base] = ci.col_ind[q];
     flag[q - base] = picked0[q];
     lab[q - base] = 0;
+    if (MODE == kModeLego) gfl[q - base] = out.ground[q];
   }
   __syncthreads();
 
@@ -714,7 +731,7 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
       bool stop = false;
       for (int top = ep; top >= sp && !stop; top -= 64) {
         const int k = top - lane;
-        int ind = 0, lo = 0, hi = -1;
+        int ind = 0, lo = 0, hi = -1, myrank = 0;
         bool el = false, tail = false, mine = false;
         if (k >= sp) {
           ind = ind_at(k);
@@ -723,7 +740,7 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
           lo = ind - (rc & 15);
           hi = ind + (rc >> 4);
           const float cv = curv[bb];
-          el = !flag[bb] && cv > cfg.edge_thr;
+          el = !flag[bb] && cv > cfg.edge_thr && (MODE == kModeLio || !gfl[bb]);
           tail = k < ep && !(cv > cfg.edge_thr);
         }
         const bool last_chunk = __ballot(tail) != 0;
@@ -738,25 +755,32 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
           const int hil = __builtin_amdgcn_readlane(hi, l);
           if (lane == l) {
             mine = true;
+            myrank = picks;
             corner_pos[ncorner + picks - 1] = ind;
+            if (MODE == kModeLego) out.corner_sharp[(int64_t)r * kCornerPerRing + ncorner + picks - 1] = picks <= 2;
           }
           el = el && lane > l && !(ind >= lol && ind <= hil);
           msk = __ballot(el);
         }
         if (mine) {
-          lab[ind - base] = 1;
+          lab[ind - base] = (MODE == kModeLego && myrank <= 2) ? 2 : 1;
           for (int q = lo; q <= hi; ++q) flag[q - base] = 1;
         }
         if (last_chunk) break;
       }
       ncorner += min(picks, 20);
+      nsharp += min(picks, 2);
       // flats: k = sp .. ep (:239-263).  Ascending curvature: the scan stops
       // after the first sorted value >= surfThreshold; k = ep is examined last.
+      // LeGO-LOAM: ground points only, at most 4 (the 4th is labelled but does
+      // not suppress, featureAssociation.cpp:947-953).
       bool done_sorted = false;
-      for (int bot = sp; bot < ep && !done_sorted; bot += 64) {
+      int fpicks = 0;
+      bool fstop = false;
+      for (int bot = sp; bot < ep && !done_sorted && !fstop; bot += 64) {
         const int k = bot + lane;
         int ind = 0, lo = 0, hi = -1;
-        bool el = false, tail = false, mine = false;
+        bool el = false, tail = false, mine = false, supp = false;
         if (k < ep) {
           ind = ind_at(k);
           const int bb = ind - base;
@@ -764,36 +788,53 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
           lo = ind - (rc & 15);
           hi = ind + (rc >> 4);
           const float cv = curv[bb];
-          el = !flag[bb] && cv < cfg.surf_thr;
+          el = !flag[bb] && cv < cfg.surf_thr && (MODE == kModeLio || gfl[bb]);
           tail = !(cv < cfg.surf_thr);
         }
         done_sorted = __ballot(tail) != 0;
         uint64_t msk = __ballot(el);
         while (msk) {
           const int l = __ffsll((long long)msk) - 1;
+          ++fpicks;
+          if (lane == l) {
+            mine = true;
+            if (MODE == kModeLego) flat_pos[nflat + fpicks - 1] = ind;
+          }
+          if (MODE == kModeLego && fpicks >= 4) {
+            fstop = true;
+            break;
+          }
+          supp |= lane == l;
           const int lol = __builtin_amdgcn_readlane(lo, l);
           const int hil = __builtin_amdgcn_readlane(hi, l);
-          mine |= lane == l;
           el = el && lane > l && !(ind >= lol && ind <= hil);
           msk = __ballot(el);
         }
-        if (mine) {
-          lab[ind - base] = -1;
+        if (mine) lab[ind - base] = -1;
+        if (supp)
           for (int q = lo; q <= hi; ++q) flag[q - base] = 1;
-        }
       }
-      {  // k = ep (outside the sorted range)
+      if (!fstop) {  // k = ep (outside the sorted range)
         const int bb = ep - base;
-        if (!flag[bb] && curv[bb] < cfg.surf_thr) {
+        if (!flag[bb] && curv[bb] < cfg.surf_thr && (MODE == kModeLio || gfl[bb])) {
+          ++fpicks;
           const int rc = reach[bb];
           const int lol = ep - (rc & 15), hil = ep + (rc >> 4);
-          if (lane == 0) lab[bb] = -1;
-          if (lane <= hil - lol) flag[lol + lane - base] = 1;
+          if (lane == 0) {
+            lab[bb] = -1;
+            if (MODE == kModeLego) flat_pos[nflat + fpicks - 1] = ep;
+          }
+          if (!(MODE == kModeLego && fpicks >= 4) && lane <= hil - lol) flag[lol + lane - base] = 1;
         }
       }
+      if (MODE == kModeLego) nflat += min(fpicks, 4);
     }
     LSTAMP_ACC(7);
-    if (t == 0) s_ncorner = ncorner;
+    if (t == 0) {
+      s_ncorner = ncorner;
+      s_nflat = nflat;
+      if (MODE == kModeLego) out.sharp_count[r] = nsharp;
+    }
   }
   __syncthreads();
   // surfaceCloudScan (:265-269): sector positions k in [sp, ep] with label
@@ -827,6 +868,14 @@ __global__ __launch_bounds__(kFeatThreads) void k_lio_features(
   for (int q = base + t; q <= span_end; q += kFeatThreads)
     if (q >= start && q <= end) out.label[q] = lab[q - base];
   if (t == 0) out.corner_count[r] = nc;
+  if (MODE == kModeLego) {
+    const int nf = s_nflat;
+    for (int q = t; q < nf; q += kFeatThreads) {
+      const int p = flat_pos[q];
+      out.flat_stage[(int64_t)r * kFlatPerRing + q] = ci.xyzi[(p >= start && p <= end) ? p : start];
+    }
+    if (t == 0) out.flat_count[r] = nf;
+  }
 
   // ---- pcl::VoxelGrid(leaf) on surfaceCloudScan
   const int m = s_nsurf;
@@ -1160,7 +1209,7 @@ int slio_lio_create(slio_lio_handle* out, const slio_lio_params* p) {
   h->fc.ring_cap = H + 16;
   const int kcap = std::max(6 * h->fc.sort_cap, h->fc.vox_cap);
   h->feat_smem = 8 * (size_t)(kcap + 6 * h->fc.sort_cap) + 16 * (size_t)h->fc.vox_cap +
-                 (4 + 4 + 4 + 1 + 1 + 1) * (size_t)h->fc.ring_cap + 16;
+                 (4 + 4 + 4 + 1 + 1 + 1 + 1) * (size_t)h->fc.ring_cap + 16;
   if (6 * h->fc.sort_cap > 4 * kFeatThreads) {
     set_error("slio_lio_create: horizon_scan too large for the sector sort");
     lio_free(h);
@@ -1174,8 +1223,8 @@ int slio_lio_create(slio_lio_handle* out, const slio_lio_params* p) {
     return SLIO_EINVAL;
   }
   if (h->feat_smem > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)k_lio_features, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)h->feat_smem);
+    (void)hipFuncSetAttribute((const void*)k_fe_features<kModeLio>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->feat_smem);
   *out = h;
   return SLIO_OK;
 }
@@ -1257,7 +1306,8 @@ int slio_lio_run_async(slio_lio_handle h) {
   k_lio_extract<<<R, kRowThreads, 0, h->stream>>>(g, h->range_mat, h->full, h->row_count, ci);
   k_lio_smooth<<<(unsigned)((g.cells + 255) / 256), 256, 0, h->stream>>>(
       h->prange, h->col_ind, h->n_ext, h->curvature, h->picked0, h->label);
-  const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count};
+  const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
+                   nullptr, nullptr, nullptr, nullptr, nullptr};
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (h->prof) {
     if (h->pending.size() > 256) lio_prof_drain(h);
@@ -1270,7 +1320,7 @@ int slio_lio_run_async(slio_lio_handle h) {
     }
     h->pending.push_back(ev);
   }
-  hipExtLaunchKernelGGL(k_lio_features, dim3(R), dim3(kFeatThreads), (uint32_t)h->feat_smem,
+  hipExtLaunchKernelGGL(k_fe_features<kModeLio>, dim3(R), dim3(kFeatThreads), (uint32_t)h->feat_smem,
                         h->stream, ev.first, ev.second, 0, ci, (const float*)h->curvature,
                         (const uint8_t*)h->picked0, h->fc, fo);
   k_lio_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
@@ -1389,3 +1439,1116 @@ extern "C" int slio_dbg_lio_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstamp), sizeof(g_lstamp)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// ======================================================================
+// LeGO-LOAM.  One scan = 14 launches:
+//   memsets (cell owners, ground, component stats)
+//   k_lego_claim     per point   projectPointCloud: row from the vertical
+//                                angle, the LAST point wins (atomicMax, :177-213)
+//   k_lego_fill      per cell    rangeMat / fullCloud (intensity row + col/1e4)
+//   k_lego_ground    per column  groundRemoval, sequential over the ground rows
+//                                as the reference loop (:216-262), labelMat -1
+//   k_lego_union     per cell    labelComponents as connected components: the
+//                                BFS edge test (:355-372) is symmetric, so BFS
+//                                visits exactly a component; lock-free
+//                                union-find linking to the smaller index, so a
+//                                root is the component's first row-major cell
+//   k_lego_compress  per cell    roots, component size, rows of its pushed cells
+//   k_lego_rowcount  per ring    feasible roots / segmented / outlier counts
+//   k_lego_extract   per ring    labelCount order of feasible roots, cloud_info,
+//                                segmented + outlier clouds (:268-330)
+//   k_lego_label     per cell    labelMat (label, 999999 or -1)
+//   k_lego_half      per point   adjustDistortion's halfPassed switch point
+//   k_lego_deskew    per point   adjustDistortion (:617-805)
+//   k_lio_smooth     per point   calculateSmoothness + markOccludedPoints
+//   k_fe_features<kModeLego>     extractFeatures (:883-1007) + VoxelGrid 0.2
+//   k_lego_concat    per ring    sharp / less sharp / flat / less flat clouds
+// ======================================================================
+namespace slio {
+namespace lego {
+using namespace slio::lio;
+
+struct LGeo {
+  int N, H, gsi, vpn, vln;
+  float res_x, res_y, bottom, mount, theta;
+  float sX, cX, sY, cY;  // sin / cos of segmentAlphaX / segmentAlphaY
+  int64_t cells;
+};
+
+__device__ __forceinline__ bool lego_row(const LGeo& g, float x, float y, float z, int& row) {
+  // verticalAngle; rowIdn is a size_t: the quotient truncates toward zero,
+  // (-1, 0) -> 0, <= -1 or NaN wraps out of range (imageProjection.cpp:180-182)
+  const float va = (float)((double)(fatan2(z, sqrtf(x * x + y * y)) * 180.0f) / M_PI);
+  const float q = (va + g.bottom) / g.res_y;
+  if (!(q > -1.0f) || !(q < (float)g.N)) return false;
+  row = (int)q;
+  return row < g.N;
+}
+
+__device__ __forceinline__ bool lego_col(const LGeo& g, float x, float y, int& col) {
+  const float ha = (float)((double)(fatan2(x, y) * 180.0f) / M_PI);
+  int64_t c = (int64_t)(-round(((double)ha - 90.0) / (double)g.res_x) + (double)(g.H / 2));
+  if (c >= g.H) c -= g.H;
+  if (c < 0 || c >= g.H) return false;
+  col = (int)c;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_lego_claim(const float* __restrict__ x,
+                                                    const float* __restrict__ y,
+                                                    const float* __restrict__ z, int64_t n, LGeo g,
+                                                    int32_t* owner) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int row, col;
+  if (!lego_row(g, x[i], y[i], z[i], row) || !lego_col(g, x[i], y[i], col)) return;
+  atomicMax(&owner[col + (int64_t)row * g.H], (int32_t)i);
+}
+
+__global__ __launch_bounds__(256) void k_lego_fill(const float* __restrict__ x,
+                                                   const float* __restrict__ y,
+                                                   const float* __restrict__ z, LGeo g,
+                                                   const int32_t* owner, float* range_mat,
+                                                   float4* full) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.cells) return;
+  const int o = owner[c];
+  if (o < 0) {
+    range_mat[c] = FLT_MAX;
+    full[c] = make_float4(0.f, 0.f, 0.f, -1.0f);  // nanPoint's intensity (:65-68)
+    return;
+  }
+  const float px = x[o], py = y[o], pz = z[o];
+  const int row = (int)(c / g.H), col = (int)(c - (int64_t)row * g.H);
+  range_mat[c] = sqrtf(px * px + py * py + pz * pz);
+  full[c] = make_float4(px, py, pz, (float)((double)(float)row + (double)(float)col / 10000.0));
+}
+
+__global__ __launch_bounds__(256) void k_lego_ground(LGeo g, const int32_t* owner, const float4* full,
+                                                     int8_t* ground, int32_t* parent) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= g.H) return;
+  for (int i = 0; i < g.gsi; ++i) {
+    const int64_t lo = j + (int64_t)i * g.H, up = lo + g.H;
+    if (owner[lo] < 0 || owner[up] < 0) {
+      ground[lo] = -1;
+      continue;
+    }
+    const float4 a = full[lo], b = full[up];
+    const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
+    const float angle = (float)((double)(fatan2(dz, sqrtf(dx * dx + dy * dy)) * 180.0f) / M_PI);
+    if (fabsf(angle - g.mount) <= 10) {
+      ground[lo] = 1;
+      ground[up] = 1;
+    }
+  }
+  // labelMat = -1 for ground and empty cells (:247-254); the rest start as
+  // their own union-find roots
+  for (int i = 0; i < g.N; ++i) {
+    const int64_t c = j + (int64_t)i * g.H;
+    parent[c] = (ground[c] == 1 || owner[c] < 0) ? -1 : (int32_t)c;
+  }
+}
+
+__device__ __forceinline__ int32_t ld_parent(const int32_t* p, int64_t i) {
+  return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// parent pointers only ever move to smaller indices, so every chain ends
+__device__ __forceinline__ int32_t uf_find(const int32_t* parent, int32_t x) {
+  while (true) {
+    const int32_t p = ld_parent(parent, x);
+    if (p == x) return x;
+    x = p;
+  }
+}
+
+__device__ void uf_unite(int32_t* parent, int32_t a, int32_t b) {
+  while (true) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a > b) {
+      const int32_t t = a;
+      a = b;
+      b = t;
+    }
+    const int32_t old = atomicCAS(&parent[b], b, a);  // link the larger root below the smaller
+    if (old == b) return;
+    b = old;
+  }
+}
+
+__device__ __forceinline__ bool lego_edge(const LGeo& g, float ra, float rb, bool horiz) {
+  const float d1 = fmaxf(ra, rb), d2 = fminf(ra, rb);
+  const float s = horiz ? g.sX : g.sY, c = horiz ? g.cX : g.cY;
+  return fatan2(d2 * s, (d1 - d2 * c)) > g.theta;  // :358-362
+}
+
+__global__ __launch_bounds__(256) void k_lego_union(LGeo g, const float* __restrict__ range_mat,
+                                                    int32_t* parent) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.cells || ld_parent(parent, c) < 0) return;
+  const int row = (int)(c / g.H), col = (int)(c - (int64_t)row * g.H);
+  const float rc = range_mat[c];
+  // right neighbour (column wrap) and the one below; the reverse directions
+  // are the same undirected edges seen from the other cell
+  const int64_t cr = (col + 1 < g.H ? col + 1 : 0) + (int64_t)row * g.H;
+  if (cr != c && ld_parent(parent, cr) >= 0 && lego_edge(g, rc, range_mat[cr], true))
+    uf_unite(parent, (int32_t)c, (int32_t)cr);
+  if (row + 1 < g.N) {
+    const int64_t cd = c + g.H;
+    if (ld_parent(parent, cd) >= 0 && lego_edge(g, rc, range_mat[cd], false))
+      uf_unite(parent, (int32_t)c, (int32_t)cd);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lego_compress(LGeo g, int32_t* parent, int32_t* csize,
+                                                       unsigned long long* rows) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.cells || ld_parent(parent, c) < 0) return;
+  const int32_t r = uf_find(parent, (int32_t)c);
+  // path compression: any ancestor is a valid value for concurrent readers
+  __hip_atomic_store(parent + c, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicAdd(&csize[r], 1);
+  // lineCountFlag is set for every pushed cell, not for the seed (:373)
+  if (r != c) {
+    const int row = (int)(c / g.H);
+    atomicOr(&rows[2 * (int64_t)r + (row >> 6)], 1ull << (row & 63));
+  }
+}
+
+__device__ __forceinline__ bool lego_feasible(const LGeo& g, const int32_t* csize,
+                                              const unsigned long long* rows, int32_t r) {
+  const int sz = csize[r];
+  if (sz >= 30) return true;
+  if (sz < g.vpn) return false;
+  const int lc = __popcll(rows[2 * (int64_t)r]) + __popcll(rows[2 * (int64_t)r + 1]);
+  return lc >= g.vln;
+}
+
+// per cell of ring r: 0 feasible root, 1 segmented point, 2 outlier point
+__device__ __forceinline__ void lego_cell_class(const LGeo& g, int r, int j, const int8_t* ground,
+                                                const int32_t* parent, const int32_t* csize,
+                                                const unsigned long long* rows, bool& root,
+                                                bool& seg, bool& outl) {
+  const int64_t c = j + (int64_t)r * g.H;
+  const int32_t p = parent[c];
+  const bool gnd = ground[c] == 1;
+  root = seg = outl = false;
+  bool positive = false, rejected = false;
+  if (p >= 0) {
+    const int32_t rt = uf_find(parent, p);
+    const bool feas = lego_feasible(g, csize, rows, rt);
+    root = feas && rt == c;
+    positive = feas;
+    rejected = !feas;
+  }
+  if (!(positive || rejected || gnd)) return;  // label -1 and not ground
+  if (rejected) {  // 999999 (:286-293)
+    outl = r > g.gsi && j % 5 == 0;
+    return;
+  }
+  if (gnd && j % 5 != 0 && j > 5 && j < g.H - 5) return;  // ground decimation (:295-297)
+  seg = true;
+}
+
+constexpr int kLegoRowThreads = 1024;
+
+__global__ __launch_bounds__(kLegoRowThreads) void k_lego_rowcount(LGeo g, const int8_t* ground,
+                                                                   const int32_t* parent,
+                                                                   const int32_t* csize,
+                                                                   const unsigned long long* rows,
+                                                                   int32_t* cnt /* [N][3] */) {
+  __shared__ int scratch[kLegoRowThreads / 64 + 1];
+  const int r = blockIdx.x, t = threadIdx.x;
+  int a = 0, b = 0, d = 0;
+  for (int j = t; j < g.H; j += kLegoRowThreads) {
+    bool root, seg, outl;
+    lego_cell_class(g, r, j, ground, parent, csize, rows, root, seg, outl);
+    a += root;
+    b += seg;
+    d += outl;
+  }
+  int e;
+  a = block_exclusive_scan<kLegoRowThreads>(a, scratch, e);
+  b = block_exclusive_scan<kLegoRowThreads>(b, scratch, e);
+  d = block_exclusive_scan<kLegoRowThreads>(d, scratch, e);
+  if (t == 0) {
+    cnt[3 * r] = a;
+    cnt[3 * r + 1] = b;
+    cnt[3 * r + 2] = d;
+  }
+}
+
+struct LegoSeg {
+  int32_t *start_ring, *end_ring, *col_ind;
+  uint8_t* ground_flag;
+  float* range;
+  float4* xyzi;
+  float4* outlier;
+  int32_t* n;  // n_segmented, n_outlier
+};
+
+__global__ __launch_bounds__(kLegoRowThreads) void k_lego_extract(
+    LGeo g, const int8_t* ground, const int32_t* parent, const int32_t* csize,
+    const unsigned long long* rows, const int32_t* cnt, const float* range_mat, const float4* full,
+    int32_t* rootlab, LegoSeg sg) {
+  __shared__ int scratch[kLegoRowThreads / 64 + 1];
+  const int r = blockIdx.x, t = threadIdx.x;
+  int pa = 0, pb = 0, pd = 0;
+  for (int q = t; q < r; q += kLegoRowThreads) {
+    pa += cnt[3 * q];
+    pb += cnt[3 * q + 1];
+    pd += cnt[3 * q + 2];
+  }
+  int e;
+  const int oa = block_exclusive_scan<kLegoRowThreads>(pa, scratch, e);
+  const int ob = block_exclusive_scan<kLegoRowThreads>(pb, scratch, e);
+  const int od = block_exclusive_scan<kLegoRowThreads>(pd, scratch, e);
+  if (t == 0) {
+    sg.start_ring[r] = ob - 1 + 5;
+    sg.end_ring[r] = ob + cnt[3 * r + 1] - 1 - 5;
+    if (r == g.N - 1) {
+      sg.n[0] = ob + cnt[3 * r + 1];
+      sg.n[1] = od + cnt[3 * r + 2];
+    }
+  }
+  // thread t owns the contiguous columns [t * per, (t + 1) * per)
+  const int per = (g.H + kLegoRowThreads - 1) / kLegoRowThreads;
+  const int j0 = t * per, j1 = min(j0 + per, g.H);
+  int a = 0, b = 0, d = 0;
+  for (int j = j0; j < j1; ++j) {
+    bool root, seg, outl;
+    lego_cell_class(g, r, j, ground, parent, csize, rows, root, seg, outl);
+    a += root;
+    b += seg;
+    d += outl;
+  }
+  int ea, eb, ed;
+  block_exclusive_scan<kLegoRowThreads>(a, scratch, ea);
+  block_exclusive_scan<kLegoRowThreads>(b, scratch, eb);
+  block_exclusive_scan<kLegoRowThreads>(d, scratch, ed);
+  int ka = oa + ea, kb = ob + eb, kd = od + ed;
+  for (int j = j0; j < j1; ++j) {
+    bool root, seg, outl;
+    lego_cell_class(g, r, j, ground, parent, csize, rows, root, seg, outl);
+    const int64_t c = j + (int64_t)r * g.H;
+    if (root) rootlab[c] = 1 + ka++;  // labelCount order (:390)
+    if (seg) {
+      sg.ground_flag[kb] = ground[c] == 1;
+      sg.col_ind[kb] = j;
+      sg.range[kb] = range_mat[c];
+      sg.xyzi[kb] = full[c];
+      ++kb;
+    }
+    if (outl) sg.outlier[kd++] = full[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lego_label(LGeo g, const int32_t* parent, const int32_t* csize,
+                                                    const unsigned long long* rows,
+                                                    const int32_t* rootlab, int32_t* label) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.cells) return;
+  const int32_t p = parent[c];
+  if (p < 0) {
+    label[c] = -1;
+    return;
+  }
+  const int32_t rt = uf_find(parent, p);
+  label[c] = lego_feasible(g, csize, rows, rt) ? rootlab[rt] : 999999;
+}
+
+struct LegoImuDev {
+  const double* time;
+  const float *roll, *pitch, *yaw, *vx, *vy, *vz, *ax, *ay, *az;
+  int last, last_it, Q;
+  double t0;
+  float ang_last[3];
+  int on;
+};
+
+struct LegoImuOutDev {
+  float rpy_start[3], rpy_cur[3], velo_from_start[3], angular_from_start[3], ang_last[3];
+};
+
+// adjustDistortion's per-point orientation before the halfPassed switch
+__device__ __forceinline__ float ori_a(float so, float px, float pz, bool& passes) {
+  float ori = -fatan2(px, pz);
+  if (ori < so - M_PI / 2)
+    ori = (float)((double)ori + 2 * M_PI);
+  else if (ori > so + M_PI * 3 / 2)
+    ori = (float)((double)ori - 2 * M_PI);
+  passes = ori - so > M_PI;
+  return ori;
+}
+
+__global__ __launch_bounds__(256) void k_lego_half(const float4* seg, const int32_t* nseg, float so,
+                                                   uint32_t* slot, LegoImuOutDev* io, float al0,
+                                                   float al1, float al2) {
+  __shared__ uint32_t wmin[4];
+  const int n = *nseg;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) {  // the state adjustDistortion leaves when it writes nothing
+    *io = LegoImuOutDev{};
+    io->ang_last[0] = al0;
+    io->ang_last[1] = al1;
+    io->ang_last[2] = al2;
+  }
+  bool f = false;
+  if (i < n) {
+    const float4 p = seg[i];
+    ori_a(so, p.y, p.x, f);  // point.x = y, point.z = x
+  }
+  uint32_t v = f ? (uint32_t)i : kNone;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) slot[blockIdx.x] = min(min(wmin[0], wmin[1]), min(wmin[2], wmin[3]));
+}
+
+struct ImuCur {
+  float r, p, y, vx, vy, vz;
+  bool after;
+  int f, b;
+  float rf, rb;
+};
+
+// :652-719 interpolation of the IMU ring at timeScanCur + pointTime
+__device__ ImuCur imu_at(const LegoImuDev& m, float pointTime) {
+  ImuCur c;
+  const double tq = m.t0 + pointTime;
+  int f = m.last_it;
+  while (f != m.last) {
+    if (tq < m.time[f]) break;
+    f = (f + 1) % m.Q;
+  }
+  c.f = f;
+  c.b = (f + m.Q - 1) % m.Q;
+  c.after = tq > m.time[f];
+  c.rf = c.rb = 0.f;
+  if (c.after) {
+    c.r = m.roll[f];
+    c.p = m.pitch[f];
+    c.y = m.yaw[f];
+    c.vx = m.vx[f];
+    c.vy = m.vy[f];
+    c.vz = m.vz[f];
+  } else {
+    const int b = c.b;
+    c.rf = (float)((tq - m.time[b]) / (m.time[f] - m.time[b]));
+    c.rb = (float)((m.time[f] - tq) / (m.time[f] - m.time[b]));
+    c.r = m.roll[f] * c.rf + m.roll[b] * c.rb;
+    c.p = m.pitch[f] * c.rf + m.pitch[b] * c.rb;
+    if (m.yaw[f] - m.yaw[b] > M_PI)
+      c.y = (float)(m.yaw[f] * c.rf + ((double)m.yaw[b] + 2 * M_PI) * c.rb);
+    else if (m.yaw[f] - m.yaw[b] < -M_PI)
+      c.y = (float)(m.yaw[f] * c.rf + ((double)m.yaw[b] - 2 * M_PI) * c.rb);
+    else
+      c.y = m.yaw[f] * c.rf + m.yaw[b] * c.rb;
+    c.vx = m.vx[f] * c.rf + m.vx[b] * c.rb;
+    c.vy = m.vy[f] * c.rf + m.vy[b] * c.rb;
+    c.vz = m.vz[f] * c.rf + m.vz[b] * c.rb;
+  }
+  return c;
+}
+
+constexpr int kImuQueLds = 512;
+
+__global__ __launch_bounds__(256) void k_lego_deskew(const float4* seg, const int32_t* nseg,
+                                                     const uint32_t* slot, int nslot, float so,
+                                                     float eo, float od, float scan_period,
+                                                     LegoImuDev m, float4* out,
+                                                     LegoImuOutDev* io) {
+  __shared__ uint32_t wmin[4];
+  __shared__ double s_time[kImuQueLds];
+  __shared__ float s_arr[9][kImuQueLds];
+  __shared__ float st[12];  // rs ps ys vxs vys vzs cR cP cY sR sP sY
+  const int n = *nseg;
+  const int t = threadIdx.x;
+  const int i = blockIdx.x * 256 + t;
+  // the halfPassed switch point: the first point whose pre-switch orientation passes
+  uint32_t v = kNone;
+  for (int q = t; q < nslot; q += 256) v = min(v, slot[q]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  if ((t & 63) == 0) wmin[t >> 6] = v;
+  const bool imu = m.on && m.last >= 0;
+  if (imu && m.Q <= kImuQueLds) {
+    for (int q = t; q < m.Q; q += 256) {
+      s_time[q] = m.time[q];
+      s_arr[0][q] = m.roll[q];
+      s_arr[1][q] = m.pitch[q];
+      s_arr[2][q] = m.yaw[q];
+      s_arr[3][q] = m.vx[q];
+      s_arr[4][q] = m.vy[q];
+      s_arr[5][q] = m.vz[q];
+      s_arr[6][q] = m.ax[q];
+      s_arr[7][q] = m.ay[q];
+      s_arr[8][q] = m.az[q];
+    }
+  }
+  __syncthreads();
+  if (imu && m.Q <= kImuQueLds) {
+    m.time = s_time;
+    m.roll = s_arr[0];
+    m.pitch = s_arr[1];
+    m.yaw = s_arr[2];
+    m.vx = s_arr[3];
+    m.vy = s_arr[4];
+    m.vz = s_arr[5];
+    m.ax = s_arr[6];
+    m.ay = s_arr[7];
+    m.az = s_arr[8];
+  }
+  const uint32_t half = min(min(wmin[0], wmin[1]), min(wmin[2], wmin[3]));
+  // start state from point 0 (i == 0 branch, :721-781)
+  if (imu && t == 0 && n > 0) {
+    const float4 p0 = seg[0];
+    bool f0;
+    const float o0 = ori_a(so, p0.y, p0.x, f0);
+    const float rel0 = (o0 - so) / od;
+    const ImuCur c0 = imu_at(m, rel0 * scan_period);
+    st[0] = c0.r;
+    st[1] = c0.p;
+    st[2] = c0.y;
+    st[3] = c0.vx;
+    st[4] = c0.vy;
+    st[5] = c0.vz;
+    st[6] = fcos(c0.r);
+    st[7] = fcos(c0.p);
+    st[8] = fcos(c0.y);
+    st[9] = fsin(c0.r);
+    st[10] = fsin(c0.p);
+    st[11] = fsin(c0.y);
+    if (blockIdx.x == 0) {
+      float a[3];
+      if (c0.after) {
+        a[0] = m.ax[c0.f];
+        a[1] = m.ay[c0.f];
+        a[2] = m.az[c0.f];
+      } else {
+        a[0] = m.ax[c0.f] * c0.rf + m.ax[c0.b] * c0.rb;
+        a[1] = m.ay[c0.f] * c0.rf + m.ay[c0.b] * c0.rb;
+        a[2] = m.az[c0.f] * c0.rf + m.az[c0.b] * c0.rb;
+      }
+      for (int k = 0; k < 3; ++k) {
+        io->angular_from_start[k] = a[k] - m.ang_last[k];
+        io->ang_last[k] = a[k];
+      }
+      io->rpy_start[0] = c0.r;
+      io->rpy_start[1] = c0.p;
+      io->rpy_start[2] = c0.y;
+    }
+  }
+  __syncthreads();
+  if (i >= n) return;
+  const float4 s4 = seg[i];
+  float px = s4.y, py = s4.z, pz = s4.x;
+  float ori;
+  if ((uint32_t)i <= half) {
+    bool f;
+    ori = ori_a(so, px, pz, f);
+  } else {
+    ori = -fatan2(px, pz);
+    ori = (float)((double)ori + 2 * M_PI);
+    if (ori < eo - M_PI * 3 / 2)
+      ori = (float)((double)ori + 2 * M_PI);
+    else if (ori > eo + M_PI / 2)
+      ori = (float)((double)ori - 2 * M_PI);
+  }
+  const float relTime = (ori - so) / od;
+  const float inten = int(s4.w) + scan_period * relTime;
+  if (imu) {
+    const ImuCur c = imu_at(m, relTime * scan_period);
+    if (i == n - 1) {
+      io->rpy_cur[0] = c.r;
+      io->rpy_cur[1] = c.p;
+      io->rpy_cur[2] = c.y;
+    }
+    if (i > 0) {
+      const float cRs = st[6], cPs = st[7], cYs = st[8], sRs = st[9], sPs = st[10], sYs = st[11];
+      if (i == n - 1) {  // VeloToStartIMU (:392-427) of the last point
+        const float vx = c.vx - st[3], vy = c.vy - st[4], vz = c.vz - st[5];
+        const float x1 = cYs * vx - sYs * vz, y1 = vy, z1 = sYs * vx + cYs * vz;
+        const float x2 = x1, y2 = cPs * y1 + sPs * z1, z2 = -sPs * y1 + cPs * z1;
+        io->velo_from_start[0] = cRs * x2 + sRs * y2;
+        io->velo_from_start[1] = -sRs * x2 + cRs * y2;
+        io->velo_from_start[2] = z2;
+      }
+      // TransformToStartIMU (:429-458); imuShiftFromStartCur is 0
+      const float x1 = fcos(c.r) * px - fsin(c.r) * py;
+      const float y1 = fsin(c.r) * px + fcos(c.r) * py;
+      const float z1 = pz;
+      const float x2 = x1;
+      const float y2 = fcos(c.p) * y1 - fsin(c.p) * z1;
+      const float z2 = fsin(c.p) * y1 + fcos(c.p) * z1;
+      const float x3 = fcos(c.y) * x2 + fsin(c.y) * z2;
+      const float y3 = y2;
+      const float z3 = -fsin(c.y) * x2 + fcos(c.y) * z2;
+      const float x4 = cYs * x3 - sYs * z3;
+      const float y4 = y3;
+      const float z4 = sYs * x3 + cYs * z3;
+      const float x5 = x4;
+      const float y5 = cPs * y4 + sPs * z4;
+      const float z5 = -sPs * y4 + cPs * z4;
+      px = cRs * x5 + sRs * y5 + 0.0f;
+      py = -sRs * x5 + cRs * y5 + 0.0f;
+      pz = z5 + 0.0f;
+    }
+  }
+  out[i] = make_float4(px, py, pz, inten);
+}
+
+__global__ __launch_bounds__(256) void k_lego_concat(int n_scan, const int32_t* start_ring, FeatOut f,
+                                                     float4* sharp, float4* less_sharp, float4* flat,
+                                                     float4* less_flat, int64_t* counts) {
+  __shared__ int s_o[4];
+  const int r = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+    for (int q = 0; q < r; ++q) {
+      o0 += f.sharp_count[q];
+      o1 += f.corner_count[q];
+      o2 += f.flat_count[q];
+      o3 += f.surf_count[q];
+    }
+    s_o[0] = o0;
+    s_o[1] = o1;
+    s_o[2] = o2;
+    s_o[3] = o3;
+    if (r == n_scan - 1) {
+      counts[0] = o0 + f.sharp_count[r];
+      counts[1] = o1 + f.corner_count[r];
+      counts[2] = o2 + f.flat_count[r];
+      counts[3] = o3 + f.surf_count[r];
+    }
+    // cornerPointsSharp: the label-2 picks in pick order (<= 12 per ring)
+    int k = 0;
+    for (int q = 0; q < f.corner_count[r]; ++q)
+      if (f.corner_sharp[(int64_t)r * kCornerPerRing + q])
+        sharp[o0 + k++] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < f.corner_count[r]; q += 256)
+    less_sharp[s_o[1] + q] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
+  for (int q = threadIdx.x; q < f.flat_count[r]; q += 256)
+    flat[s_o[2] + q] = f.flat_stage[(int64_t)r * kFlatPerRing + q];
+  const float4* src = f.surf_stage + (start_ring[r] - 4);
+  for (int q = threadIdx.x; q < f.surf_count[r]; q += 256) less_flat[s_o[3] + q] = src[q];
+}
+
+}  // namespace lego
+}  // namespace slio
+
+using namespace slio::lego;
+
+struct slio_lego {
+  slio_lego_params prm{};
+  LGeo g{};
+  hipStream_t own = nullptr, stream = nullptr;
+  int64_t cap = 0, cells = 0;
+  float *x = nullptr, *y = nullptr, *z = nullptr;
+  int64_t n = 0;
+  float orient[3] = {0.f, 0.f, 0.f};
+  // IMU ring (device) + state
+  double* itime = nullptr;
+  float* iarr = nullptr;  // 12 arrays of que_len
+  int que = 0;
+  LegoImuDev imu{};
+  int imu_last_host = 0;
+  // image / segmentation
+  int32_t* owner = nullptr;
+  float* range_mat = nullptr;
+  float4* full = nullptr;
+  int8_t* ground = nullptr;
+  int32_t* parent = nullptr;
+  int32_t* csize = nullptr;
+  unsigned long long* rows = nullptr;
+  int32_t* cnt = nullptr;
+  int32_t* rootlab = nullptr;
+  int32_t* label = nullptr;
+  int32_t *start_ring = nullptr, *end_ring = nullptr, *col_ind = nullptr, *nseg = nullptr;
+  uint8_t* gflag = nullptr;
+  float* srange = nullptr;
+  float4 *sxyzi = nullptr, *outlier = nullptr;
+  // features
+  uint32_t* slot = nullptr;
+  float4* desk = nullptr;
+  LegoImuOutDev* io = nullptr;
+  float* curvature = nullptr;
+  uint8_t* picked0 = nullptr;
+  int32_t* flabel = nullptr;
+  float4* corner_stage = nullptr;
+  int8_t* corner_sharp = nullptr;
+  int32_t *corner_count = nullptr, *sharp_count = nullptr, *flat_count = nullptr, *surf_count = nullptr;
+  float4 *flat_stage = nullptr, *surf_stage = nullptr;
+  float4 *c_sharp = nullptr, *c_less_sharp = nullptr, *c_flat = nullptr, *c_less_flat = nullptr;
+  int64_t* counts = nullptr;
+  FeatCfg fc{};
+  size_t feat_smem = 0;
+  bool ran = false;
+  bool prof = false;
+  double prof_ms = 0.0;
+  int64_t prof_n = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
+};
+
+namespace {
+
+void lego_prof_drain(slio_lego* h) {
+  for (auto& p : h->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.second) == hipSuccess &&
+        hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+      h->prof_ms += ms;
+      h->prof_n += 1;
+    }
+    h->pool.push_back(p);
+  }
+  h->pending.clear();
+}
+
+void lego_free(slio_lego* h) {
+  lego_prof_drain(h);
+  for (auto& p : h->pool) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  void* dev[] = {h->x, h->y, h->z, h->itime, h->iarr, h->owner, h->range_mat, h->full, h->ground,
+                 h->parent, h->csize, h->rows, h->cnt, h->rootlab, h->label, h->start_ring,
+                 h->end_ring, h->col_ind, h->nseg, h->gflag, h->srange, h->sxyzi, h->outlier,
+                 h->slot, h->desk, h->io, h->curvature, h->picked0, h->flabel, h->corner_stage,
+                 h->corner_sharp, h->corner_count, h->sharp_count, h->flat_count, h->surf_count,
+                 h->flat_stage, h->surf_stage, h->c_sharp, h->c_less_sharp, h->c_flat,
+                 h->c_less_flat, h->counts};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  if (h->own) (void)hipStreamDestroy(h->own);
+}
+
+#define LEGO_CHECK_H(h)                    \
+  do {                                     \
+    if (!(h)) {                            \
+      set_error("null slio_lego handle");  \
+      return SLIO_EINVAL;                  \
+    }                                      \
+    LIO_HIP(hipSetDevice((h)->prm.device)); \
+  } while (0)
+
+inline float hfatan2(float y, float x) { return (float)std::atan2((double)y, (double)x); }
+
+}  // namespace
+
+extern "C" {
+
+int slio_lego_params_default(slio_lego_params* p) {
+  if (!p) return SLIO_EINVAL;
+  std::memset(p, 0, sizeof(*p));
+  p->n_scan = 16;
+  p->horizon_scan = 1800;
+  p->ground_scan_ind = 7;
+  p->segment_valid_point_num = 5;
+  p->segment_valid_line_num = 3;
+  p->ang_res_x = 0.2f;
+  p->ang_res_y = 2.0f;
+  p->ang_bottom = 15.0f + 0.1f;
+  p->sensor_mount_angle = 0.0f;
+  p->segment_theta = 1.0472f;
+  p->edge_threshold = 0.1f;
+  p->surf_threshold = 0.1f;
+  p->leaf_size = 0.2f;
+  p->scan_period = 0.1f;
+  return SLIO_OK;
+}
+
+int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
+  if (!out || !p) {
+    set_error("slio_lego_create: null argument");
+    return SLIO_EINVAL;
+  }
+  *out = nullptr;
+  if (p->n_scan <= 1 || p->n_scan > 128 || p->horizon_scan <= 0 || p->horizon_scan > 8192 ||
+      p->ground_scan_ind < 0 || p->ground_scan_ind >= p->n_scan || !(p->leaf_size > 0.0f) ||
+      !(p->ang_res_x > 0.0f) || !(p->ang_res_y > 0.0f) || p->max_points < 0) {
+    set_error("slio_lego_create: bad n_scan (2..128) / horizon_scan / ground_scan_ind / resolution / leaf");
+    return SLIO_EINVAL;
+  }
+  int ndev = 0;
+  LIO_HIP(hipGetDeviceCount(&ndev));
+  if (p->device < 0 || p->device >= ndev) {
+    set_error("slio_lego_create: no such HIP device");
+    return SLIO_EDEVICE;
+  }
+  LIO_HIP(hipSetDevice(p->device));
+  auto* h = new slio_lego();
+  h->prm = *p;
+  h->cells = (int64_t)p->n_scan * p->horizon_scan;
+  h->cap = p->max_points > 0 ? p->max_points : 4 * h->cells;
+  const float ax = (float)((double)p->ang_res_x / 180.0 * M_PI);
+  const float ay = (float)((double)p->ang_res_y / 180.0 * M_PI);
+  h->g = LGeo{p->n_scan, p->horizon_scan, p->ground_scan_ind, p->segment_valid_point_num,
+              p->segment_valid_line_num, p->ang_res_x, p->ang_res_y, p->ang_bottom,
+              p->sensor_mount_angle, p->segment_theta,
+              (float)std::sin((double)ax), (float)std::cos((double)ax),
+              (float)std::sin((double)ay), (float)std::cos((double)ay), h->cells};
+  const int64_t C = h->cells, N = h->cap, R = p->n_scan;
+  hipError_t e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
+  h->stream = h->own;
+#define A(ptr, bytes) \
+  if (!e) e = hipMalloc(reinterpret_cast<void**>(&(ptr)), (bytes))
+  A(h->x, 4 * N);
+  A(h->y, 4 * N);
+  A(h->z, 4 * N);
+  A(h->owner, 4 * C);
+  A(h->range_mat, 4 * C);
+  A(h->full, 16 * C);
+  A(h->ground, C);
+  A(h->parent, 4 * C);
+  A(h->csize, 4 * C);
+  A(h->rows, 16 * C);
+  A(h->cnt, 12 * R);
+  A(h->rootlab, 4 * C);
+  A(h->label, 4 * C);
+  A(h->start_ring, 4 * R);
+  A(h->end_ring, 4 * R);
+  A(h->col_ind, 4 * C);
+  A(h->nseg, 8);
+  A(h->gflag, C);
+  A(h->srange, 4 * C);
+  A(h->sxyzi, 16 * C);
+  A(h->outlier, 16 * C);
+  A(h->slot, 4 * ((C + 255) / 256 + 1));
+  A(h->desk, 16 * C);
+  A(h->io, sizeof(LegoImuOutDev));
+  A(h->curvature, 4 * C);
+  A(h->picked0, C);
+  A(h->flabel, 4 * C);
+  A(h->corner_stage, 16 * R * kCornerPerRing);
+  A(h->corner_sharp, R * kCornerPerRing);
+  A(h->corner_count, 4 * R);
+  A(h->sharp_count, 4 * R);
+  A(h->flat_count, 4 * R);
+  A(h->surf_count, 4 * R);
+  A(h->flat_stage, 16 * R * kFlatPerRing);
+  A(h->surf_stage, 16 * C);
+  A(h->c_sharp, 16 * R * kCornerPerRing);
+  A(h->c_less_sharp, 16 * R * kCornerPerRing);
+  A(h->c_flat, 16 * R * kFlatPerRing);
+  A(h->c_less_flat, 16 * C);
+  A(h->counts, 32);
+#undef A
+  if (!e) e = hipMemset(h->io, 0, sizeof(LegoImuOutDev));
+  if (e) {
+    set_error(std::string("slio_lego_create: ") + hipGetErrorString(e));
+    lego_free(h);
+    delete h;
+    return SLIO_ENOMEM;
+  }
+  const int H = p->horizon_scan;
+  h->fc.edge_thr = p->edge_threshold;
+  h->fc.surf_thr = p->surf_threshold;
+  h->fc.leaf = p->leaf_size;
+  h->fc.sort_cap = 64;
+  while (h->fc.sort_cap < H / 6 + 2) h->fc.sort_cap <<= 1;
+  h->fc.vox_cap = 64;
+  while (h->fc.vox_cap < H) h->fc.vox_cap <<= 1;
+  h->fc.ring_cap = H + 16;
+  const int kcap = std::max(6 * h->fc.sort_cap, h->fc.vox_cap);
+  h->feat_smem = 8 * (size_t)(kcap + 6 * h->fc.sort_cap) + 16 * (size_t)h->fc.vox_cap +
+                 (4 + 4 + 4 + 1 + 1 + 1 + 1) * (size_t)h->fc.ring_cap + 16;
+  if (6 * h->fc.sort_cap > 4 * kFeatThreads || h->feat_smem > 160 * 1024 - 4096) {
+    set_error("slio_lego_create: horizon_scan too large for the per-ring LDS layout");
+    lego_free(h);
+    delete h;
+    return SLIO_EINVAL;
+  }
+  if (h->feat_smem > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)k_fe_features<kModeLego>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->feat_smem);
+  *out = h;
+  return SLIO_OK;
+}
+
+int slio_lego_destroy(slio_lego_handle h) {
+  if (!h) return SLIO_OK;
+  (void)hipSetDevice(h->prm.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  lego_free(h);
+  delete h;
+  return SLIO_OK;
+}
+
+int slio_lego_set_stream(slio_lego_handle h, void* stream) {
+  LEGO_CHECK_H(h);
+  h->stream = stream ? (hipStream_t)stream : h->own;
+  return SLIO_OK;
+}
+
+int slio_lego_set_imu(slio_lego_handle h, const slio_lego_imu* m) {
+  LEGO_CHECK_H(h);
+  h->imu.on = 0;
+  if (!m || m->pointer_last < 0) {
+    h->imu.last = -1;
+    h->imu_last_host = m ? m->pointer_last : 0;
+    for (int a = 0; a < 3; ++a) h->imu.ang_last[a] = m ? m->ang_last[a] : 0.0f;
+    return SLIO_OK;
+  }
+  if (m->que_len <= 0 || m->que_len > 65536 || m->pointer_last >= m->que_len ||
+      m->pointer_last_iteration < 0 || m->pointer_last_iteration >= m->que_len || !m->time) {
+    set_error("slio_lego_set_imu: bad que_len / pointers");
+    return SLIO_EINVAL;
+  }
+  const int Q = m->que_len;
+  if (Q > h->que) {
+    if (h->itime) (void)hipFree(h->itime);
+    if (h->iarr) (void)hipFree(h->iarr);
+    h->itime = nullptr;
+    h->iarr = nullptr;
+    LIO_HIP(hipMalloc(&h->itime, 8 * Q));
+    LIO_HIP(hipMalloc(&h->iarr, 4 * 12 * (size_t)Q));
+    h->que = Q;
+  }
+  const float* arr[12] = {m->roll, m->pitch, m->yaw, m->velo_x, m->velo_y, m->velo_z,
+                          m->shift_x, m->shift_y, m->shift_z, m->ang_x, m->ang_y, m->ang_z};
+  for (int k = 0; k < 12; ++k)
+    if (!arr[k]) {
+      set_error("slio_lego_set_imu: null IMU array");
+      return SLIO_EINVAL;
+    }
+  LIO_HIP(hipMemcpyAsync(h->itime, m->time, 8 * Q, hipMemcpyHostToDevice, h->stream));
+  for (int k = 0; k < 12; ++k)
+    LIO_HIP(hipMemcpyAsync(h->iarr + (size_t)k * Q, arr[k], 4 * Q, hipMemcpyHostToDevice, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  float* a = h->iarr;
+  h->imu = LegoImuDev{h->itime, a, a + Q, a + 2 * Q, a + 3 * Q, a + 4 * Q, a + 5 * Q,
+                      a + 9 * Q, a + 10 * Q, a + 11 * Q, m->pointer_last,
+                      m->pointer_last_iteration, Q, m->time_scan_cur,
+                      {m->ang_last[0], m->ang_last[1], m->ang_last[2]}, 1};
+  h->imu_last_host = m->pointer_last;
+  return SLIO_OK;
+}
+
+int slio_lego_upload(slio_lego_handle h, const float* x, const float* y, const float* z, int64_t n) {
+  LEGO_CHECK_H(h);
+  if (n < 0 || (n > 0 && (!x || !y || !z))) {
+    set_error("slio_lego_upload: bad arguments");
+    return SLIO_EINVAL;
+  }
+  if (n > h->cap || n > INT32_MAX) {
+    set_error("slio_lego_upload: scan exceeds max_points");
+    return SLIO_ECAPACITY;
+  }
+  h->n = n;
+  // findStartEndAngle (imageProjection.cpp:160-175)
+  if (n >= 2) {
+    const float so = -hfatan2(y[0], x[0]);
+    float eo = (float)(-(double)hfatan2(y[n - 1], x[n - 2]) + 2 * M_PI);
+    if (eo - so > 3 * M_PI)
+      eo = (float)((double)eo - 2 * M_PI);
+    else if (eo - so < M_PI)
+      eo = (float)((double)eo + 2 * M_PI);
+    h->orient[0] = so;
+    h->orient[1] = eo;
+    h->orient[2] = eo - so;
+  } else {
+    h->orient[0] = h->orient[1] = h->orient[2] = 0.0f;
+  }
+  if (n > 0) {
+    LIO_HIP(hipMemcpyAsync(h->x, x, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->y, y, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipMemcpyAsync(h->z, z, 4 * n, hipMemcpyHostToDevice, h->stream));
+    LIO_HIP(hipStreamSynchronize(h->stream));
+  }
+  h->ran = false;
+  return SLIO_OK;
+}
+
+int slio_lego_run_async(slio_lego_handle h) {
+  LEGO_CHECK_H(h);
+  const LGeo& g = h->g;
+  const int R = g.N;
+  const unsigned cb = (unsigned)((g.cells + 255) / 256);
+  LIO_HIP(hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream));
+  LIO_HIP(hipMemsetAsync(h->ground, 0, g.cells, h->stream));
+  LIO_HIP(hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream));
+  LIO_HIP(hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream));
+  if (h->n > 0)
+    k_lego_claim<<<(unsigned)((h->n + 255) / 256), 256, 0, h->stream>>>(h->x, h->y, h->z, h->n, g,
+                                                                          h->owner);
+  k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, h->owner, h->range_mat, h->full);
+  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, h->owner, h->full, h->ground, h->parent);
+  k_lego_union<<<cb, 256, 0, h->stream>>>(g, h->range_mat, h->parent);
+  k_lego_compress<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows);
+  k_lego_rowcount<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
+                                                        h->cnt);
+  const LegoSeg sg{h->start_ring, h->end_ring, h->col_ind, h->gflag, h->srange, h->sxyzi,
+                   h->outlier, h->nseg};
+  k_lego_extract<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
+                                                       h->cnt, h->range_mat, h->full, h->rootlab, sg);
+  k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label);
+  // adjustDistortion
+  const int nslot = (int)cb;
+  k_lego_half<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->orient[0], h->slot, h->io,
+                                          h->imu.ang_last[0], h->imu.ang_last[1], h->imu.ang_last[2]);
+  k_lego_deskew<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->slot, nslot, h->orient[0],
+                                            h->orient[1], h->orient[2], h->prm.scan_period, h->imu,
+                                            h->desk, h->io);
+  k_lio_smooth<<<cb, 256, 0, h->stream>>>(h->srange, h->col_ind, h->nseg, h->curvature, h->picked0,
+                                          h->flabel);
+  const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->srange, h->desk, h->nseg};
+  const FeatOut fo{h->flabel, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
+                   h->corner_sharp, h->sharp_count, h->flat_stage, h->flat_count, h->gflag};
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (h->prof) {
+    if (h->pending.size() > 256) lego_prof_drain(h);
+    if (!h->pool.empty()) {
+      ev = h->pool.back();
+      h->pool.pop_back();
+    } else {
+      LIO_HIP(hipEventCreate(&ev.first));
+      LIO_HIP(hipEventCreate(&ev.second));
+    }
+    h->pending.push_back(ev);
+  }
+  hipExtLaunchKernelGGL(k_fe_features<kModeLego>, dim3(R), dim3(kFeatThreads),
+                        (uint32_t)h->feat_smem, h->stream, ev.first, ev.second, 0, ci,
+                        (const float*)h->curvature, (const uint8_t*)h->picked0, h->fc, fo);
+  k_lego_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->c_sharp, h->c_less_sharp,
+                                          h->c_flat, h->c_less_flat, h->counts);
+  LIO_HIP(hipGetLastError());
+  h->ran = true;
+  return SLIO_OK;
+}
+
+int slio_lego_get_counts(slio_lego_handle h, slio_lego_counts* c) {
+  LEGO_CHECK_H(h);
+  if (!h->ran) {
+    set_error("slio_lego: no scan processed");
+    return SLIO_ESTATE;
+  }
+  int32_t ns[2];
+  int64_t k[4];
+  LIO_HIP(hipMemcpyAsync(ns, h->nseg, 8, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipMemcpyAsync(k, h->counts, 32, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  if (c) {
+    c->n_segmented = ns[0];
+    c->n_outlier = ns[1];
+    c->n_sharp = k[0];
+    c->n_less_sharp = k[1];
+    c->n_flat = k[2];
+    c->n_less_flat = k[3];
+    for (int a = 0; a < 3; ++a) c->orientation[a] = h->orient[a];
+  }
+  return SLIO_OK;
+}
+
+int slio_lego_run(slio_lego_handle h, slio_lego_counts* c) {
+  const int rc = slio_lego_run_async(h);
+  if (rc) return rc;
+  return slio_lego_get_counts(h, c);
+}
+
+int slio_lego_get_image(slio_lego_handle h, float* range_mat, int32_t* cell_point, int8_t* ground,
+                        int32_t* label) {
+  slio_lego_counts c;
+  const int rc = slio_lego_get_counts(h, &c);
+  if (rc) return rc;
+  const int64_t C = h->cells;
+  if (range_mat) LIO_HIP(hipMemcpyAsync(range_mat, h->range_mat, 4 * C, hipMemcpyDeviceToHost, h->stream));
+  if (cell_point) LIO_HIP(hipMemcpyAsync(cell_point, h->owner, 4 * C, hipMemcpyDeviceToHost, h->stream));
+  if (ground) LIO_HIP(hipMemcpyAsync(ground, h->ground, C, hipMemcpyDeviceToHost, h->stream));
+  if (label) LIO_HIP(hipMemcpyAsync(label, h->label, 4 * C, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+int slio_lego_get_seg_info(slio_lego_handle h, int32_t* start_ring, int32_t* end_ring,
+                           uint8_t* ground_flag, int32_t* col_ind, float* range, float* seg_xyzi,
+                           float* outlier_xyzi) {
+  slio_lego_counts c;
+  const int rc = slio_lego_get_counts(h, &c);
+  if (rc) return rc;
+  const int64_t R = h->g.N, n = c.n_segmented, no = c.n_outlier;
+  if (start_ring) LIO_HIP(hipMemcpyAsync(start_ring, h->start_ring, 4 * R, hipMemcpyDeviceToHost, h->stream));
+  if (end_ring) LIO_HIP(hipMemcpyAsync(end_ring, h->end_ring, 4 * R, hipMemcpyDeviceToHost, h->stream));
+  if (n > 0) {
+    if (ground_flag) LIO_HIP(hipMemcpyAsync(ground_flag, h->gflag, n, hipMemcpyDeviceToHost, h->stream));
+    if (col_ind) LIO_HIP(hipMemcpyAsync(col_ind, h->col_ind, 4 * n, hipMemcpyDeviceToHost, h->stream));
+    if (range) LIO_HIP(hipMemcpyAsync(range, h->srange, 4 * n, hipMemcpyDeviceToHost, h->stream));
+    if (seg_xyzi) LIO_HIP(hipMemcpyAsync(seg_xyzi, h->sxyzi, 16 * n, hipMemcpyDeviceToHost, h->stream));
+  }
+  if (outlier_xyzi && no > 0)
+    LIO_HIP(hipMemcpyAsync(outlier_xyzi, h->outlier, 16 * no, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+int slio_lego_get_features(slio_lego_handle h, float* deskewed, float* curvature, uint8_t* picked,
+                           int32_t* label, slio_lego_imu_out* imu_out) {
+  slio_lego_counts c;
+  const int rc = slio_lego_get_counts(h, &c);
+  if (rc) return rc;
+  const int64_t n = c.n_segmented;
+  if (n > 0) {
+    if (deskewed) LIO_HIP(hipMemcpyAsync(deskewed, h->desk, 16 * n, hipMemcpyDeviceToHost, h->stream));
+    if (curvature) LIO_HIP(hipMemcpyAsync(curvature, h->curvature, 4 * n, hipMemcpyDeviceToHost, h->stream));
+    if (picked) LIO_HIP(hipMemcpyAsync(picked, h->picked0, n, hipMemcpyDeviceToHost, h->stream));
+    if (label) LIO_HIP(hipMemcpyAsync(label, h->flabel, 4 * n, hipMemcpyDeviceToHost, h->stream));
+  }
+  LegoImuOutDev io;
+  LIO_HIP(hipMemcpyAsync(&io, h->io, sizeof(io), hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  if (imu_out) {
+    std::memcpy(imu_out->rpy_start, io.rpy_start, sizeof(io.rpy_start));
+    std::memcpy(imu_out->rpy_cur, io.rpy_cur, sizeof(io.rpy_cur));
+    std::memcpy(imu_out->velo_from_start, io.velo_from_start, sizeof(io.velo_from_start));
+    std::memcpy(imu_out->angular_from_start, io.angular_from_start, sizeof(io.angular_from_start));
+    std::memcpy(imu_out->ang_last, io.ang_last, sizeof(io.ang_last));
+    imu_out->pointer_last_iteration = h->imu_last_host;  // :804
+  }
+  return SLIO_OK;
+}
+
+int slio_lego_get_clouds(slio_lego_handle h, float* sharp, float* less_sharp, float* flat,
+                         float* less_flat) {
+  slio_lego_counts c;
+  const int rc = slio_lego_get_counts(h, &c);
+  if (rc) return rc;
+  if (sharp && c.n_sharp > 0)
+    LIO_HIP(hipMemcpyAsync(sharp, h->c_sharp, 16 * c.n_sharp, hipMemcpyDeviceToHost, h->stream));
+  if (less_sharp && c.n_less_sharp > 0)
+    LIO_HIP(hipMemcpyAsync(less_sharp, h->c_less_sharp, 16 * c.n_less_sharp, hipMemcpyDeviceToHost, h->stream));
+  if (flat && c.n_flat > 0)
+    LIO_HIP(hipMemcpyAsync(flat, h->c_flat, 16 * c.n_flat, hipMemcpyDeviceToHost, h->stream));
+  if (less_flat && c.n_less_flat > 0)
+    LIO_HIP(hipMemcpyAsync(less_flat, h->c_less_flat, 16 * c.n_less_flat, hipMemcpyDeviceToHost, h->stream));
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  return SLIO_OK;
+}
+
+int slio_lego_profile(slio_lego_handle h, int enable) {
+  LEGO_CHECK_H(h);
+  const bool keep = (enable & SLIO_LIO_PROFILE_KEEP) != 0;
+  h->prof = (enable & ~SLIO_LIO_PROFILE_KEEP) != 0;
+  if (!keep) {
+    lego_prof_drain(h);
+    h->prof_ms = 0.0;
+    h->prof_n = 0;
+  }
+  return SLIO_OK;
+}
+
+int slio_lego_profile_read(slio_lego_handle h, double* ms, int64_t* launches) {
+  LEGO_CHECK_H(h);
+  LIO_HIP(hipStreamSynchronize(h->stream));
+  lego_prof_drain(h);
+  if (ms) *ms = h->prof_ms;
+  if (launches) *launches = h->prof_n;
+  return SLIO_OK;
+}
+
+}  // extern "C"

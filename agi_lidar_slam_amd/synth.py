@@ -304,3 +304,38 @@ def make_ouster_scan(seed: int = 20261015, n_scan: int = 64, horizon: int = 2048
                 z=np.ascontiguousarray(pts[:, 2]), intensity=intensity,
                 ring=rows.astype(np.uint16), time=t_rel, imu_stamps=stamps, imu_gyro=gyro,
                 time_scan_cur=time_scan_cur, time_scan_end=t_end, n_scan=n_scan, horizon=horizon)
+
+
+# ---------------------------------------------------------------- LeGO-LOAM: VLP-16 + IMU
+def make_vlp16_sweep(seed: int = 20261015, horizon: int = 1800, yaw_rate: float = 0.3,
+                     dropout: float = 0.03, n_map_scene: int = 2_000_000,
+                     time_scan_cur: float = 500.0) -> dict:
+    """One VLP-16 sweep in firing order (16 lasers per azimuth step, the
+    velodyne_pointcloud layout LeGO-LOAM reads), no-return points dropped,
+    sensor turning at yaw_rate about z; plus a 200 Hz IMU stream (orientation,
+    linear acceleration, angular velocity) covering the sweep."""
+    scene = make_scene(seed, n_map_scene)
+    rng = np.random.default_rng(seed + 4)
+    yaw0 = rng.uniform(-np.pi, np.pi)
+    org = np.array([rng.uniform(-3, 3), rng.uniform(-3, 3), 1.7])
+    cols = np.repeat(np.arange(horizon), 16)
+    rings = np.tile(np.arange(16), horizon)
+    t = cols * (0.1 / horizon)
+    az = -(cols + rng.uniform(-0.3, 0.3, cols.size)) * (2 * np.pi / horizon) + np.pi  # clockwise
+    el = np.deg2rad(-15.0 + 2.0 * rings + rng.normal(0, 0.02, cols.size))
+    dl = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], 1)
+    yaw = yaw0 + yaw_rate * t
+    cy, sy = np.cos(yaw), np.sin(yaw)
+    dw = np.stack([cy * dl[:, 0] - sy * dl[:, 1], sy * dl[:, 0] + cy * dl[:, 1], dl[:, 2]], 1)
+    r = _cast(scene, org, dw, 100.0)
+    ok = np.isfinite(r) & (rng.uniform(size=cols.size) >= dropout)
+    r = r + rng.normal(0.0, 0.01, cols.size)
+    pts = (dl[ok] * r[ok, None]).astype(np.float32)
+    stamps = np.arange(time_scan_cur - 0.2, time_scan_cur + 0.2, 0.005)
+    ts = stamps - time_scan_cur
+    imu = dict(time=stamps, roll=np.full(stamps.size, 0.01), pitch=np.full(stamps.size, -0.02),
+               yaw=np.angle(np.exp(1j * (yaw0 + yaw_rate * ts))),
+               acc=np.tile([0.1, 0.05, 9.81], (stamps.size, 1)) + rng.normal(0, 0.01, (stamps.size, 3)),
+               gyro=np.tile([0.0, 0.0, yaw_rate], (stamps.size, 1)))
+    return dict(x=np.ascontiguousarray(pts[:, 0]), y=np.ascontiguousarray(pts[:, 1]),
+                z=np.ascontiguousarray(pts[:, 2]), time_scan_cur=time_scan_cur, imu=imu)

@@ -97,6 +97,100 @@ int slio_lio_get_features(slio_lio_handle h, float* curvature, uint8_t* picked, 
 /* cloud_corner [n_corner * 4], cloud_surface [n_surface * 4].  Either may be NULL. */
 int slio_lio_get_clouds(slio_lio_handle h, float* corner_xyzi, float* surface_xyzi);
 
+/* ======================================================================
+ * LeGO-LOAM
+ *   ImageProjection::cloudHandler  LeGO-LOAM/src/imageProjection.cpp:151-158
+ *     findStartEndAngle :160-175, projectPointCloud :177-213 (the LAST point
+ *     wins a cell), groundRemoval :216-262, cloudSegmentation :268-330 +
+ *     labelComponents :332-393 -> cloud_info.msg + segmented / outlier clouds
+ *   FeatureAssociation::runFeatureAssociation (front half)
+ *     featureAssociation.cpp: adjustDistortion :617-805, calculateSmoothness
+ *     :807-834, markOccludedPoints :838-876, extractFeatures :883-1007
+ * The IMU ring buffer (imuHandler / AccumulateIMUShiftAndRotation :430-588)
+ * is host state handed over with slio_lego_set_imu.
+ * ====================================================================== */
+typedef struct slio_lego* slio_lego_handle;
+
+typedef struct slio_lego_params {
+  int32_t device;
+  int32_t n_scan;                  /* N_SCAN (utility.h:20, 16)                */
+  int32_t horizon_scan;            /* Horizon_SCAN (1800)                      */
+  int32_t ground_scan_ind;         /* groundScanInd (7)                        */
+  int32_t segment_valid_point_num; /* segmentValidPointNum (5)                 */
+  int32_t segment_valid_line_num;  /* segmentValidLineNum (3)                  */
+  float ang_res_x;                 /* 0.2 deg                                  */
+  float ang_res_y;                 /* 2.0 deg                                  */
+  float ang_bottom;                /* 15.0 + 0.1 deg                           */
+  float sensor_mount_angle;        /* 0 deg                                    */
+  float segment_theta;             /* 1.0472 rad (60 deg)                      */
+  float edge_threshold;            /* 0.1                                      */
+  float surf_threshold;            /* 0.1                                      */
+  float leaf_size;                 /* less-flat VoxelGrid leaf (0.2, :222)     */
+  float scan_period;               /* 0.1 s                                    */
+  int32_t max_points;              /* input capacity (0 -> 4 * cells)          */
+  int32_t reserved[4];
+} slio_lego_params;
+
+/* FeatureAssociation IMU state read by adjustDistortion: the que_len-entry
+ * ring buffer (imuTime double, the rest float), imuPointerLast (-1: no IMU),
+ * imuPointerLastIteration, timeScanCur and imuAngularRotation{X,Y,Z}Last. */
+typedef struct slio_lego_imu {
+  const double* time;
+  const float *roll, *pitch, *yaw;
+  const float *velo_x, *velo_y, *velo_z;
+  const float *shift_x, *shift_y, *shift_z;
+  const float *ang_x, *ang_y, *ang_z; /* imuAngularRotation{X,Y,Z} */
+  int32_t pointer_last, pointer_last_iteration, que_len;
+  double time_scan_cur;
+  float ang_last[3];
+} slio_lego_imu;
+
+/* State adjustDistortion leaves for the back half (updateInitialGuess
+ * :1999-2029): imu{Roll,Pitch,Yaw}Start, imu{Roll,Pitch,Yaw}Cur of the last
+ * point, imuVeloFromStart{X,Y,Z}Cur of the last point, imuAngularFromStart,
+ * the new imuAngularRotation*Last and imuPointerLastIteration. */
+typedef struct slio_lego_imu_out {
+  float rpy_start[3], rpy_cur[3], velo_from_start[3], angular_from_start[3], ang_last[3];
+  int32_t pointer_last_iteration;
+} slio_lego_imu_out;
+
+typedef struct slio_lego_counts {
+  int64_t n_segmented, n_outlier, n_sharp, n_less_sharp, n_flat, n_less_flat;
+  float orientation[3]; /* startOrientation, endOrientation, orientationDiff */
+} slio_lego_counts;
+
+int slio_lego_params_default(slio_lego_params* p);
+int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p);
+int slio_lego_destroy(slio_lego_handle h);
+int slio_lego_set_stream(slio_lego_handle h, void* stream);
+/* IMU state for the next run; NULL or pointer_last < 0 -> no IMU correction. */
+int slio_lego_set_imu(slio_lego_handle h, const slio_lego_imu* imu);
+/* laserCloudIn x, y, z (PointXYZI order of the driver); findStartEndAngle runs here. */
+int slio_lego_upload(slio_lego_handle h, const float* x, const float* y, const float* z, int64_t n);
+int slio_lego_run_async(slio_lego_handle h);
+int slio_lego_run(slio_lego_handle h, slio_lego_counts* counts);
+int slio_lego_get_counts(slio_lego_handle h, slio_lego_counts* counts);
+/* rangeMat, the input index that filled each cell (-1 empty), groundMat, labelMat. */
+int slio_lego_get_image(slio_lego_handle h, float* range_mat, int32_t* cell_point, int8_t* ground,
+                        int32_t* label);
+/* cloud_info (startRingIndex, endRingIndex, segmentedCloudGroundFlag,
+ * segmentedCloudColInd, segmentedCloudRange), segmented cloud xyzi (as
+ * imageProjection publishes it) and outlier cloud xyzi.  Any may be NULL. */
+int slio_lego_get_seg_info(slio_lego_handle h, int32_t* start_ring, int32_t* end_ring,
+                           uint8_t* ground_flag, int32_t* col_ind, float* range, float* seg_xyzi,
+                           float* outlier_xyzi);
+/* After adjustDistortion: the segmented cloud in the LOAM frame (x, y, z,
+ * ring + scanPeriod * relTime), cloudCurvature, cloudNeighborPicked after
+ * markOccludedPoints, cloudLabel (2 sharp, 1 less sharp, -1 flat, 0), IMU state. */
+int slio_lego_get_features(slio_lego_handle h, float* deskewed, float* curvature, uint8_t* picked,
+                           int32_t* label, slio_lego_imu_out* imu_out);
+/* cornerPointsSharp, cornerPointsLessSharp, surfPointsFlat, surfPointsLessFlat. */
+int slio_lego_get_clouds(slio_lego_handle h, float* sharp, float* less_sharp, float* flat,
+                         float* less_flat);
+/* Timing of the feature kernel, as slio_lio_profile. */
+int slio_lego_profile(slio_lego_handle h, int enable);
+int slio_lego_profile_read(slio_lego_handle h, double* ms, int64_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

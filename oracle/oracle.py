@@ -223,3 +223,149 @@ def lio_features(info: dict, n_scan: int, edge_threshold: float = 1.0, surf_thre
                          C.byref(nc), su.ctypes.data_as(_FP), C.byref(ns))
     return dict(cloudCurvature=cv, cloudNeighborPicked=pk, cloudLabel=lb,
                 cloud_corner=co[:nc.value].copy(), cloud_surface=su[:ns.value].copy())
+
+
+# ---------------------------------------------------------------- LeGO-LOAM front-end
+class OrcLegoParams(C.Structure):
+    _fields_ = [("n_scan", C.c_int32), ("horizon", C.c_int32), ("ground_scan_ind", C.c_int32),
+                ("seg_valid_point", C.c_int32), ("seg_valid_line", C.c_int32),
+                ("ang_res_x", C.c_float), ("ang_res_y", C.c_float), ("ang_bottom", C.c_float),
+                ("sensor_mount_angle", C.c_float), ("segment_theta", C.c_float),
+                ("edge_thr", C.c_float), ("surf_thr", C.c_float), ("leaf", C.c_float),
+                ("scan_period", C.c_float)]
+
+
+class OrcLegoImu(C.Structure):
+    _fields_ = [("time", _DP)] + [(n, _FP) for n in (
+        "roll", "pitch", "yaw", "velo_x", "velo_y", "velo_z", "shift_x", "shift_y", "shift_z",
+        "ang_x", "ang_y", "ang_z")] + [
+        ("pointer_last", C.c_int32), ("pointer_last_iteration", C.c_int32), ("que_len", C.c_int32),
+        ("time_scan_cur", C.c_double), ("ang_last", C.c_float * 3)]
+
+
+class OrcLegoImuOut(C.Structure):
+    _fields_ = [("rpy_start", C.c_float * 3), ("rpy_cur", C.c_float * 3),
+                ("velo_from_start", C.c_float * 3), ("angular_from_start", C.c_float * 3),
+                ("ang_last", C.c_float * 3), ("pointer_last_iteration", C.c_int32)]
+
+
+def lego_params(p) -> OrcLegoParams:
+    return OrcLegoParams(p.N_SCAN, p.Horizon_SCAN, p.groundScanInd, p.segmentValidPointNum,
+                         p.segmentValidLineNum, p.ang_res_x, p.ang_res_y, p.ang_bottom,
+                         p.sensorMountAngle, p.segmentTheta, p.edgeThreshold, p.surfThreshold,
+                         p.leafSize, p.scanPeriod)
+
+
+def _bind_lego(lib):
+    if getattr(lib, "_lego_bound", False):
+        return
+    _I8P = C.POINTER(C.c_int8)
+    lib.orc_lego_project.restype = C.c_int64
+    lib.orc_lego_project.argtypes = [C.POINTER(OrcLegoParams), _FP, _FP, _FP, C.c_int64, _FP, _FP,
+                                     _IP, _I8P, _IP, _IP, _IP, _U8P, _IP, _FP, _FP, _FP, _I64P]
+    lib.orc_lego_features.restype = C.c_int
+    lib.orc_lego_features.argtypes = [C.POINTER(OrcLegoParams), _FP, _IP, _IP, _U8P, _IP, _FP, _FP,
+                                      C.c_int64, C.POINTER(OrcLegoImu), C.POINTER(OrcLegoImuOut),
+                                      _FP, _FP, _U8P, _IP, _FP, _I64P, _FP, _I64P, _FP, _I64P,
+                                      _FP, _I64P]
+    lib._lego_bound = True
+
+
+def lego_project(x, y, z, params) -> dict:
+    """LeGO-LOAM imageProjection.cpp:160-393 on the CPU."""
+    lib = load()
+    _bind_lego(lib)
+    P = lego_params(params)
+    x, y, z = _f(x), _f(y), _f(z)
+    n = x.shape[0]
+    N, H = params.N_SCAN, params.Horizon_SCAN
+    cells = N * H
+    orient = np.zeros(3, np.float32)
+    rm = np.empty(cells, np.float32)
+    own = np.empty(cells, np.int32)
+    gr = np.empty(cells, np.int8)
+    lb = np.empty(cells, np.int32)
+    st, en = np.empty(N, np.int32), np.empty(N, np.int32)
+    gf = np.empty(cells, np.uint8)
+    ci = np.empty(cells, np.int32)
+    sr = np.empty(cells, np.float32)
+    sx = np.empty((cells, 4), np.float32)
+    ox = np.empty((cells, 4), np.float32)
+    no = C.c_int64()
+    ns = lib.orc_lego_project(C.byref(P), x.ctypes.data_as(_FP), y.ctypes.data_as(_FP),
+                              z.ctypes.data_as(_FP), n, orient.ctypes.data_as(_FP),
+                              rm.ctypes.data_as(_FP), own.ctypes.data_as(_IP),
+                              gr.ctypes.data_as(C.POINTER(C.c_int8)), lb.ctypes.data_as(_IP),
+                              st.ctypes.data_as(_IP), en.ctypes.data_as(_IP),
+                              gf.ctypes.data_as(_U8P), ci.ctypes.data_as(_IP),
+                              sr.ctypes.data_as(_FP), sx.ctypes.data_as(_FP),
+                              ox.ctypes.data_as(_FP), C.byref(no))
+    return dict(orientation=orient, range_mat=rm.reshape(N, H), cell_point=own.reshape(N, H),
+                ground=gr.reshape(N, H), label=lb.reshape(N, H), startRingIndex=st,
+                endRingIndex=en, segmentedCloudGroundFlag=gf[:ns].copy(),
+                segmentedCloudColInd=ci[:ns].copy(), segmentedCloudRange=sr[:ns].copy(),
+                segmented_cloud=sx[:ns].copy(), outlier_cloud=ox[:no.value].copy())
+
+
+def _imu_struct(imu, time_scan_cur):
+    keep = []
+
+    def fp(a):
+        a = np.ascontiguousarray(a, np.float32)
+        keep.append(a)
+        return a.ctypes.data_as(_FP)
+    t = np.ascontiguousarray(imu.time, np.float64)
+    keep.append(t)
+    s = OrcLegoImu(t.ctypes.data_as(_DP), *(fp(getattr(imu, n)) for n in (
+        "roll", "pitch", "yaw", "velo_x", "velo_y", "velo_z", "shift_x", "shift_y", "shift_z",
+        "ang_x", "ang_y", "ang_z")), imu.pointer_last, imu.pointer_last_iteration, imu.Q,
+        float(time_scan_cur), (C.c_float * 3)(*imu.ang_last))
+    return s, keep
+
+
+def lego_features(seg: dict, params, imu=None, time_scan_cur: float = 0.0) -> dict:
+    """featureAssociation.cpp:617-1007 on the CPU.  `imu` is an
+    agi_lidar_slam_amd.lego.LegoImu (None: no IMU, imuPointerLast = -1)."""
+    lib = load()
+    _bind_lego(lib)
+    P = lego_params(params)
+    n = seg["segmentedCloudRange"].shape[0]
+    st = np.ascontiguousarray(seg["startRingIndex"], np.int32)
+    en = np.ascontiguousarray(seg["endRingIndex"], np.int32)
+    gf = np.ascontiguousarray(seg["segmentedCloudGroundFlag"], np.uint8)
+    ci = np.ascontiguousarray(seg["segmentedCloudColInd"], np.int32)
+    sr = _f(seg["segmentedCloudRange"])
+    sx = _f(seg["segmented_cloud"])
+    orient = _f(seg["orientation"])
+    m = max(n, 1)
+    dk = np.empty((m, 4), np.float32)
+    cv, pk, lb = np.empty(m, np.float32), np.empty(m, np.uint8), np.empty(m, np.int32)
+    outs = [np.empty((m, 4), np.float32) for _ in range(4)]
+    cnt = [C.c_int64() for _ in range(4)]
+    io = OrcLegoImuOut()
+    ip = None
+    keep = None
+    if imu is not None:
+        s, keep = _imu_struct(imu, time_scan_cur)
+        ip = C.byref(s)
+    lib.orc_lego_features(C.byref(P), orient.ctypes.data_as(_FP), st.ctypes.data_as(_IP),
+                          en.ctypes.data_as(_IP), gf.ctypes.data_as(_U8P), ci.ctypes.data_as(_IP),
+                          sr.ctypes.data_as(_FP), sx.ctypes.data_as(_FP), n, ip, C.byref(io),
+                          dk.ctypes.data_as(_FP), cv.ctypes.data_as(_FP), pk.ctypes.data_as(_U8P),
+                          lb.ctypes.data_as(_IP),
+                          outs[0].ctypes.data_as(_FP), C.byref(cnt[0]),
+                          outs[1].ctypes.data_as(_FP), C.byref(cnt[1]),
+                          outs[2].ctypes.data_as(_FP), C.byref(cnt[2]),
+                          outs[3].ctypes.data_as(_FP), C.byref(cnt[3]))
+    del keep
+    return dict(deskewed=dk[:n].copy(), cloudCurvature=cv[:n].copy(),
+                cloudNeighborPicked=pk[:n].copy(), cloudLabel=lb[:n].copy(),
+                cornerPointsSharp=outs[0][:cnt[0].value].copy(),
+                cornerPointsLessSharp=outs[1][:cnt[1].value].copy(),
+                surfPointsFlat=outs[2][:cnt[2].value].copy(),
+                surfPointsLessFlat=outs[3][:cnt[3].value].copy(),
+                imu_out=dict(rpy_start=np.array(io.rpy_start), rpy_cur=np.array(io.rpy_cur),
+                             velo_from_start=np.array(io.velo_from_start),
+                             angular_from_start=np.array(io.angular_from_start),
+                             ang_last=np.array(io.ang_last),
+                             pointer_last_iteration=io.pointer_last_iteration))

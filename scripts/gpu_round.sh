@@ -9,6 +9,10 @@ for step in "$@"; do
       timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${tag}_tests.log 2>&1
       rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/${tag}_tests.log
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+    fetests)
+      timeout -k 10 600 python -m pytest tests/test_gpu_frontend.py tests/test_gpu_lego.py -m gpu -q -rs > gpurun_out/${tag}_fetests.log 2>&1
+      rc=$?; echo "fetests rc=$rc"; tail -40 gpurun_out/${tag}_fetests.log
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     sweep)
       timeout -k 10 600 python scripts/sweep_search.py > gpurun_out/${tag}_sweep.log 2>&1 || { echo "sweep failed"; tail -20 gpurun_out/${tag}_sweep.log; exit 3; }
       cat gpurun_out/${tag}_sweep.log | grep -v amdgpu.ids ;;

@@ -81,6 +81,18 @@ def test_bad_arguments_fail_loudly(lib):
     assert b"n_scan" in lib.slio_last_error()
     assert lib.slio_lio_run_async(None) == -1
     assert lib.slio_lio_destroy(None) == 0
+    gp = L.SlioLegoParams()
+    assert lib.slio_lego_params_default(C.byref(gp)) == 0
+    assert (gp.n_scan, gp.horizon_scan, gp.ground_scan_ind) == (16, 1800, 7)
+    assert (gp.segment_valid_point_num, gp.segment_valid_line_num) == (5, 3)
+    assert abs(gp.ang_bottom - 15.1) < 1e-6 and abs(gp.segment_theta - 1.0472) < 1e-7
+    assert lib.slio_lego_create(None, None) == -1
+    gp.ground_scan_ind = 16
+    assert lib.slio_lego_create(C.byref(h), C.byref(gp)) == -1
+    assert b"ground_scan_ind" in lib.slio_last_error()
+    assert lib.slio_lego_run_async(None) == -1
+    assert lib.slio_lego_set_imu(None, None) == -1
+    assert lib.slio_lego_destroy(None) == 0
 
 
 def test_reduce_super_matches_python_tree(lib):
