@@ -6,13 +6,16 @@ export TMPDIR=/tmp
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${tag}_tests.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
       rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/${tag}_tests.log
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     fetests)
       timeout -k 10 600 python -m pytest tests/test_gpu_frontend.py tests/test_gpu_lego.py -m gpu -q -rs > gpurun_out/${tag}_fetests.log 2>&1
       rc=$?; echo "fetests rc=$rc"; tail -40 gpurun_out/${tag}_fetests.log
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/${tag}_smoke.log; exit 6; }
+      tail -3 gpurun_out/${tag}_smoke.log ;;
     sweep)
       timeout -k 10 600 python scripts/sweep_search.py > gpurun_out/${tag}_sweep.log 2>&1 || { echo "sweep failed"; tail -20 gpurun_out/${tag}_sweep.log; exit 3; }
       cat gpurun_out/${tag}_sweep.log | grep -v amdgpu.ids ;;
