@@ -64,11 +64,19 @@ struct IkfCtl {
   slio_state x;      // x_ (current iterate)
   slio_state xprop;  // x_propagated
   double P[576];     // P_ (row-major)
-  double KH[576];    // K * H of the last valid pass
+  double P11i[144];  // (P[:12, :12])^-1 of P_, fixed during an update (host)
+  double G[288];     // P[:, :12] P11i                                   (host)
+  double dxn[24];    // x [-] x_propagated of the current iterate: 0 on the first
+                     // pass (host), then written by the pass kernel (device)
   int32_t converge, t, done, search_now;
   int32_t passes, searches, valid_passes, mode;
   int64_t last_m;
   int32_t singular, pad;
+  double LM[300];    // Cholesky factor of S = P11i + H^T H / R, H^T H / R and
+                     // 1 / diag of the factor, of the last valid pass (device only)
 };
+
+// P11^-1 and G = P[:, :12] P11^-1 of an update's prior P (slio_ikf.cpp)
+bool info_constants(const double* P, double P11i[144], double G[288]);
 
 }  // namespace slio

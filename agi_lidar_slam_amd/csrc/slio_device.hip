@@ -626,7 +626,7 @@ __device__ __forceinline__ bool far_outside(const GridGeom& g, float far_sq, flo
 }
 
 struct PassCfg {
-  const IkfCtl* ctl;  // device-resident update: pose + pass selection from HBM (else null)
+  IkfCtl* ctl;        // device-resident update: pose + pass selection from HBM (else null)
   int want_search;    // with ctl: run only if ctl->search_now == want_search
   float plane_thr;
   float max_sqd;
@@ -649,19 +649,45 @@ __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
 constexpr int kSolveThreads = 256;
 constexpr int kSuperSeg = 8;
 
+// global-address-space views for the in-launch hand-off (sc1 accesses)
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) uint32_t guint;
+
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t arrive(uint32_t* p) {
+  return __hip_atomic_fetch_add((guint*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void reset_counter(uint32_t* p) {
+  __hip_atomic_store((guint*)p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // LDS of the filter step.
 struct SolveLds {
-  double tot[SLIO_NPROD];
-  double M[144];
-  double K12[288];
-  double a[12][25];
-  double dxn[24], dx[24], Kh[24], f[12];
-  double KH[576];
-  double P[576];
   double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums of this pass
-  slio_state x, xprop;                  // staged IkfCtl fields (one parallel sweep
-  int32_t fl[8];                        // in, one out: no serial HBM round trips)
-  int piv, s_final;
+  double S[144];     // P11^-1 + M  (SPD), M = H^T H / R
+  double M[144];
+  double P11i[144];  // (P[:12, :12])^-1
+  double G[288];     // P[:, :12] P11^-1
+  double P[576];
+  double Lf[144];    // Cholesky factor of S (rows, lower)
+  double invd[12];   // 1 / its diagonal
+  double Z[144];     // S^-1 M           (P update)
+  double K[288];     // G S^-1 M = K H [:, :12]   (P update)
+  double hth[SLIO_NPROD - SLIO_NHTH];  // H^T h (12) and m
+  double dxn[24], dx[24];
+  slio_state x, xprop;  // staged control-block fields
+  int32_t fl[8];
+  int ok, s_final;
 };
 static_assert(offsetof(IkfCtl, xprop) == sizeof(slio_state), "IkfCtl: x, xprop adjacent");
 static_assert(offsetof(SolveLds, xprop) - offsetof(SolveLds, x) == sizeof(slio_state),
@@ -672,264 +698,375 @@ constexpr int kStateD = sizeof(slio_state) / sizeof(double);
 // flag slots of IkfCtl::converge..mode
 enum { F_CONV, F_T, F_DONE, F_SEARCH, F_PASSES, F_SEARCHES, F_VALID, F_MODE };
 
-// Gauss-Jordan with partial pivoting on the 12 x 24 augmented [B | I], by
-// the first wavefront: lane j < 24 holds column j in registers and the
-// pivot row / factors are broadcast with readlane -- no workgroup barriers.
-// Operation order is exactly the host invert<12>'s (first maximum |a[r][c]|
-// as pivot, row c scaled by 1/pivot, every other row r with f = a[r][c] != 0
-// updated a[r][j] -= f * a[c][j]), so the inverse is bitwise the host's.
-// Returns (to all lanes of wave 0) false on an exactly singular pivot.
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
   return __hiloint2double(hi, lo);
 }
 
-__device__ bool gj12_wave(SolveLds& L) {
+// upper-triangle product index of (i, j), i <= j (product_table order)
+__device__ __forceinline__ int tri_index(int i, int j) { return i * 12 - (i * (i - 1)) / 2 + (j - i); }
+
+// double offset inside slio_state of error-state component k in [0, 24) for
+// the vector blocks (pos 0-2, T_LI 9-11, vel, bg, ba, grav); rotations 3-8
+// go through so3 exp / log.
+__device__ __forceinline__ int state_off(int k) { return k < 3 ? k : k + 2; }
+
+// Cholesky S = L L^T of the 12 x 12 SPD S by wave 0, row layout (lane i < 12
+// keeps row i in registers; column j is broadcast with readlane), then
+// S y = b by forward and backward substitution.  S = P11^-1 + M has every
+// eigenvalue >= that of P11^-1 > 0, so no pivoting is needed.  Leaves L in
+// L.Lf (rows) and returns y (uniform); false on a non-positive pivot.
+__device__ __forceinline__ bool chol_solve_wave(SolveLds& L, const double (&b)[12], double (&y)[12]) {
   const int lane = threadIdx.x;  // wave 0 only
-  const bool col = lane < 24;
-  double v[12];
+  const bool row = lane < 12;
+  double a[12];
 #pragma unroll
-  for (int r = 0; r < 12; ++r) v[r] = col ? L.a[r][lane] : 0.0;
+  for (int k = 0; k < 12; ++k) a[k] = row ? L.S[lane * 12 + k] : 0.0;
+  double invd = 0.0;
 #pragma unroll
-  for (int c = 0; c < 12; ++c) {
-    // pivot search in lane c's column (rows c..11, first maximum)
-    double best = fabs(v[c]);
-    int p = c;
+  for (int j = 0; j < 12; ++j) {
+    const double d = readlane_d(a[j], j);
+    if (!(d > 0.0)) return false;
+    // 1 / sqrt(d): hardware estimate + two Newton steps (< 1 ulp), far
+    // shorter than IEEE sqrt followed by IEEE division
+    double inv = __builtin_amdgcn_rsq(d);
 #pragma unroll
-    for (int r = c + 1; r < 12; ++r) {
-      const double a = fabs(v[r]);
-      if (a > best) {
-        best = a;
-        p = r;
-      }
+    for (int it = 0; it < 2; ++it) {
+      const double r = fma(-(d * inv), inv, 1.0);
+      inv = fma(0.5 * inv, r, inv);
     }
-    p = __builtin_amdgcn_readlane(p, c);
-    best = readlane_d(best, c);
-    if (best == 0.0) return false;
-    // swap rows c and p
-    double vp = v[c];
+    const double ljj = d * inv;
+    a[j] = (lane == j) ? ljj : a[j] * inv;  // lanes i > j: L[i][j]
+    invd = (lane == j) ? inv : invd;
 #pragma unroll
-    for (int r = c + 1; r < 12; ++r) vp = (r == p) ? v[r] : vp;
-#pragma unroll
-    for (int r = c + 1; r < 12; ++r) v[r] = (r == p) ? v[c] : v[r];
-    v[c] = vp;
-    // scale row c by 1 / pivot
-    const double inv = 1.0 / readlane_d(v[c], c);
-    v[c] *= inv;
-    // eliminate column c from every other row
-#pragma unroll
-    for (int r = 0; r < 12; ++r) {
-      if (r == c) continue;
-      const double f = readlane_d(v[r], c);
-      if (f != 0.0) v[r] -= f * v[c];
+    for (int k = j + 1; k < 12; ++k) {
+      const double lkj = readlane_d(a[j], k);  // L[k][j]
+      a[k] = fma(-a[j], lkj, a[k]);
     }
   }
+  if (row) {
 #pragma unroll
-  for (int r = 0; r < 12; ++r)
-    if (col) L.a[r][lane] = v[r];
+    for (int k = 0; k < 12; ++k) L.Lf[lane * 12 + k] = (k <= lane) ? a[k] : 0.0;
+    L.invd[lane] = invd;
+  }
+  wave_fence();
+  // forward: L z = b (lane i keeps the running residual of row i)
+  double r = 0.0;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) r = (lane == k) ? b[k] : r;
+  double z = 0.0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const double zj = readlane_d(r * invd, j);
+    z = (lane == j) ? zj : z;
+    r = fma(-a[j], zj, r);
+  }
+  // backward: L^T y = z (lane i holds column i of L = row i of L^T)
+  double lt[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) lt[k] = row ? L.Lf[k * 12 + lane] : 0.0;
+  double s = z;
+#pragma unroll
+  for (int j = 11; j >= 0; --j) {
+    const double yj = readlane_d(s * invd, j);
+    y[j] = yj;
+    s = fma(-lt[j], yj, s);
+  }
   return true;
 }
 
-// x1 [-] x2 (esekfom.hpp:236-258) by two lanes: part 0 = the vector blocks
-// and the rotation, part 1 = the R_LI rotation.
-__device__ void state_boxminus_part(const slio_state& x1, const slio_state& x2, double d[24],
-                                    int part) {
-  if (part == 0) {
-    for (int i = 0; i < 3; ++i) {
-      d[i] = x1.pos[i] - x2.pos[i];
-      d[9 + i] = x1.tli[i] - x2.tli[i];
-      d[12 + i] = x1.vel[i] - x2.vel[i];
-      d[15 + i] = x1.bg[i] - x2.bg[i];
-      d[18 + i] = x1.ba[i] - x2.ba[i];
-      d[21 + i] = x1.grav[i] - x2.grav[i];
-    }
-    so3_boxminus(Quat{x1.rot[0], x1.rot[1], x1.rot[2], x1.rot[3]},
-                 Quat{x2.rot[0], x2.rot[1], x2.rot[2], x2.rot[3]}, d + 3);
-  } else {
-    so3_boxminus(Quat{x1.rli[0], x1.rli[1], x1.rli[2], x1.rli[3]},
-                 Quat{x2.rli[0], x2.rli[1], x2.rli[2], x2.rli[3]}, d + 6);
-  }
-}
-
-// x [+] f (esekfom.hpp:59-73) by two lanes: part 0 = vectors + rotation,
-// part 1 = R_LI.
-__device__ void state_boxplus_part(slio_state& x, const double f[24], int part) {
-  if (part == 0) {
-    for (int i = 0; i < 3; ++i) {
-      x.pos[i] = x.pos[i] + f[i];
-      x.tli[i] = x.tli[i] + f[9 + i];
-      x.vel[i] = x.vel[i] + f[12 + i];
-      x.bg[i] = x.bg[i] + f[15 + i];
-      x.ba[i] = x.ba[i] + f[18 + i];
-      x.grav[i] = x.grav[i] + f[21 + i];
-    }
-    const Quat r = qnormalized(qmul(Quat{x.rot[0], x.rot[1], x.rot[2], x.rot[3]}, so3_exp(f + 3)));
-    x.rot[0] = r.w; x.rot[1] = r.x; x.rot[2] = r.y; x.rot[3] = r.z;
-  } else {
-    const Quat l = qnormalized(qmul(Quat{x.rli[0], x.rli[1], x.rli[2], x.rli[3]}, so3_exp(f + 6)));
-    x.rli[0] = l.w; x.rli[1] = l.x; x.rli[2] = l.y; x.rli[3] = l.z;
-  }
-}
-
-// One filter step of update_iterated_dyn_share_modified on device by one
-// workgroup of NT threads, with the operation order of the host filter_step
-// (slio_ikf.cpp):
-//   M = H^T H / R, X = (I + M P[:12, :12])^-1  (12x12 Gauss-Jordan)
-//   K12 = P[:, :12] X  = K_front[:, :12] of esekfom.hpp:311 (push-through
-//   identity: (P^-1 + E^T M E)^-1 E^T = P E^T (I + M E P E^T)^-1)
-//   K h = K12 H^T h / R, K H = K12 M, dx = K h + (K H - I) dx_new,
-// then x [+] dx, the convergence logic of esekfom.hpp:323-344 and, on the
-// final pass, P = (I - K H) P.
-// L.sup holds the pass's super-chunk sums on entry (all threads of the
-// workgroup call this; ctl->done is uniform).
+// One filter step of update_iterated_dyn_share_modified (esekfom.hpp:303-344)
+// on device by one workgroup of NT threads, in information form:
+//   K_front[:, :12] = (P^-1 + E^T M E)^-1 E^T = G S^-1,  G = P[:, :12] P11^-1,
+//   S = P11^-1 + M,  M = H^T H / R   (push-through identity; P11 = P[:12, :12])
+//   dx = K h + (K H - I) dx_new = G S^-1 v - dx_new,  v = H^T h / R + M dx_new[:12]
+// so a pass is one 12 x 12 Cholesky solve; the final pass forms
+// K H [:, :12] = G S^-1 M and P = (I - K H) P (esekfom.hpp:341-343).  P11^-1
+// and G are fixed during an update (P changes only at its end) and come from
+// the host.  Algebraically the host filter_step (slio_ikf.cpp); rounding
+// differs.
+// L.sup holds the pass's super-chunk sums on entry, except the rows in
+// load_mask, which are loaded here from sup_src (sc1 loads) in the same round
+// trip as the control block.  src is where the control block is read from:
+// the caller's mapped host block on the first pass of an update, else ctl.
+// hblk (the mapped host block) receives x, P and the flags when the update
+// ends.  All threads of the workgroup call this.
 template <int NT>
-__device__ void ikf_solve_block(IkfCtl* ctl, double R, int i, int maxit, SolveLds& L) {
-  static_assert(NT >= 128, "solve: one thread per sum");
+__device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, double R, int i,
+                                int maxit, SolveLds& L, const double* sup_src,
+                                uint32_t load_mask) {
+  static_assert(NT >= 256, "solve: at least four wavefronts");
   const int t = threadIdx.x;
-  if (t < SLIO_NPROD) {
-    double v = L.sup[0][t];
-    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][t];
-    L.tot[t] = v;
-  }
+  const bool first = src != ctl;
   {
-    const double* src = reinterpret_cast<const double*>(&ctl->x);
-    double* dst = reinterpret_cast<double*>(&L.x);
-    for (int e = t; e < 2 * kStateD; e += NT) dst[e] = src[e];
+    // one round trip: every load of the super rows and of the control block
+    // (x, x_prop, P, G, P11^-1: a contiguous run of doubles) is issued before
+    // any LDS store; global-address-space pointers keep them off the flat path
+    constexpr int kCtlD = (int)(offsetof(IkfCtl, converge) / sizeof(double));
+    constexpr int kRows = SLIO_NSUPER * SLIO_NPROD;
+    constexpr int kC = (kCtlD + NT - 1) / NT, kR = (kRows + NT - 1) / NT;
+    static_assert(offsetof(SolveLds, xprop) == offsetof(SolveLds, x) + sizeof(slio_state), "");
+    const gdouble* gc = (const gdouble*)(const double*)src;
+    double cv[kC], rv[kR];
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const int e = t + u * NT;
+      const bool on = e < kRows && sup_src && ((load_mask >> (e / SLIO_NPROD)) & 1u);
+      rv[u] = on ? ld_sc1(sup_src + e) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int e = t + u * NT;
+      cv[u] = e < kCtlD ? gc[e] : 0.0;
+    }
+    typedef __attribute__((address_space(1))) int32_t gint;
+    const int32_t fl = t < 8 ? ((const gint*)(const int32_t*)&src->converge)[t] : 0;
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const int e = t + u * NT;
+      if (e < kRows && sup_src && ((load_mask >> (e / SLIO_NPROD)) & 1u))
+        L.sup[e / SLIO_NPROD][e % SLIO_NPROD] = rv[u];
+    }
+    // control block doubles -> LDS fields (x, xprop | P | P11i | G)
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int e = t + u * NT;
+      if (e < kCtlD) {
+        constexpr int oP = (int)(offsetof(IkfCtl, P) / sizeof(double));
+        constexpr int oI = (int)(offsetof(IkfCtl, P11i) / sizeof(double));
+        constexpr int oG = (int)(offsetof(IkfCtl, G) / sizeof(double));
+        constexpr int oD = (int)(offsetof(IkfCtl, dxn) / sizeof(double));
+        if (e < oP)
+          reinterpret_cast<double*>(&L.x)[e] = cv[u];
+        else if (e < oI)
+          L.P[e - oP] = cv[u];
+        else if (e < oG)
+          L.P11i[e - oI] = cv[u];
+        else if (e < oD)
+          L.G[e - oG] = cv[u];
+        else
+          L.dxn[e - oD] = cv[u];
+        if (first) reinterpret_cast<double*>(ctl)[e] = cv[u];  // keep the block in HBM
+      }
+    }
+    if (t < 8) L.fl[t] = fl;
+    if (first && t == 0) ctl->singular = 0;
   }
-  for (int e = t; e < 576; e += NT) L.P[e] = ctl->P[e];
-  if (t < 8) L.fl[t] = (&ctl->converge)[t];
   __syncthreads();
   SSTAMP(4);
-  const int64_t m = (int64_t)llround(L.tot[90]);
+  // S, M; H^T h and m (dx_new came with the control block: the pass kernel
+  // formed it while the search ran, ikf_dx_new)
+  for (int e = t; e < 144; e += NT) {
+    const int r = e / 12, c = e - r * 12;
+    const int k = r <= c ? tri_index(r, c) : tri_index(c, r);
+    double v = L.sup[0][k];
+#pragma unroll
+    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][k];
+    const double m = v / R;
+    L.M[e] = m;
+    L.S[e] = L.P11i[e] + m;
+  }
+  if (t >= 144 && t < 144 + SLIO_NPROD - SLIO_NHTH) {
+    const int k = SLIO_NHTH + t - 144;
+    double v = L.sup[0][k];
+#pragma unroll
+    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][k];
+    L.hth[t - 144] = v;
+  }
+  __syncthreads();
+  SSTAMP(5);
+  const int64_t m = (int64_t)llround(L.hth[12]);
   const bool valid = m >= 1;
-  if (valid) {
-    // the two parts on lanes of different wavefronts, so they run concurrently
-    if (t == NT - 1 || t == NT - 65) state_boxminus_part(L.x, L.xprop, L.dxn, t == NT - 1);
-    if (t < SLIO_NHTH) {
-      int ii = 0, kk = t;
-      while (kk >= 12 - ii) {
-        kk -= 12 - ii;
-        ++ii;
-      }
-      const int jj = ii + kk;
-      const double v = L.tot[t] / R;
-      L.M[ii * 12 + jj] = v;
-      L.M[jj * 12 + ii] = v;
-    }
-    __syncthreads();
-    for (int e = t; e < 288; e += NT) {
-      const int r = e / 24, j = e - r * 24;
-      if (j < 12) {
+  if (t < 64) {
+    // wave 0: the whole pass-to-pass chain, no workgroup barrier
+    bool big = false;
+    bool ok = true;
+    if (valid) {
+      double b[12];
+#pragma unroll
+      for (int r = 0; r < 12; ++r) b[r] = 0.0;
+      if (t < 12) {
         double s2 = 0.0;
-        for (int k = 0; k < 12; ++k) s2 += L.M[r * 12 + k] * L.P[k * 24 + j];
-        L.a[r][j] = (r == j ? 1.0 : 0.0) + s2;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) s2 = fma(L.M[t * 12 + k], L.dxn[k], s2);
+        b[0] = L.hth[t] / R + s2;  // v[t], moved to slot t below
+      }
+      {
+        // v as a uniform vector: v[r] from lane r
+        const double vl = b[0];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) b[r] = readlane_d(vl, r);
+      }
+      double y[12];
+      SSTAMP(9);
+      ok = chol_solve_wave(L, b, y);
+      SSTAMP(10);
+      if (ok) {
+        // dx = G y - dx_new, |dx| > epsi (esekfom.hpp:17, 325-331)
+        bool bb = false;
+        if (t < 24) {
+          double s2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 12; ++k) s2 = fma(L.G[t * 12 + k], y[k], s2);
+          const double d = s2 - L.dxn[t];
+          L.dx[t] = d;
+          bb = fabs(d) > 0.001;
+        }
+        big = __ballot(bb) != 0;
+        wave_fence();
+        SSTAMP(11);
+        // x [+] dx (esekfom.hpp:59-73): vector blocks on lanes 0..23, the two
+        // rotations on lanes 32/33
+        if (t < 24) {
+          if (t < 3 || t >= 9) {
+            double* xs = reinterpret_cast<double*>(&L.x);
+            xs[state_off(t)] = xs[state_off(t)] + L.dx[t];
+          }
+        } else if (t == 32 || t == 33) {
+          const int u = t - 32;
+          double* q = u ? L.x.rli : L.x.rot;
+          const Quat rq =
+              qnormalized(qmul(Quat{q[0], q[1], q[2], q[3]}, so3_exp(L.dx + 3 + 3 * u)));
+          q[0] = rq.w;
+          q[1] = rq.x;
+          q[2] = rq.y;
+          q[3] = rq.z;
+        }
+      }
+    }
+    if (t == 0) {
+      L.ok = ok ? 1 : 0;
+      int32_t* f = L.fl;
+      int fin = 0;
+      if (ok) {
+        f[F_PASSES] += 1;
+        f[F_SEARCHES] += f[F_SEARCH];
+        if (valid) {
+          f[F_VALID] += 1;
+          if (f[F_MODE] == SLIO_MODE_FIXED) {
+            fin = i == maxit - 1;
+            f[F_SEARCH] = 1;
+          } else {
+            const int conv = big ? 0 : 1;
+            f[F_CONV] = conv;
+            if (conv) f[F_T] += 1;
+            if (!f[F_T] && i == maxit - 2) f[F_CONV] = 1;
+            fin = (f[F_T] > 1 || i == maxit - 1);
+            f[F_SEARCH] = f[F_CONV];
+          }
+        } else if (i == maxit - 1) {
+          // reference: the loop ends without the P update; fixed mode applies
+          // the last valid pass's K H if there was one
+          fin = (f[F_MODE] == SLIO_MODE_FIXED && f[F_VALID] > 0);
+        }
+        if (fin || i == maxit - 1) f[F_DONE] = 1;
       } else {
-        L.a[r][j] = (j - 12 == r) ? 1.0 : 0.0;
+        f[F_DONE] = 1;  // non-positive pivot: the update stops (singular)
       }
+      L.s_final = fin;
+    }
+  }
+  __syncthreads();
+  SSTAMP(6);
+  if (!L.ok) {
+    if (t == 0) {
+      ctl->singular = 1;
+      ctl->done = 1;
+      hblk->singular = 1;
+      hblk->done = 1;
+      __threadfence_system();
+    }
+    return;
+  }
+  if (valid)  // keep L and M of this pass for a final pass without effective points
+    for (int e = t; e < 300; e += NT)
+      ctl->LM[e] = e < 144 ? L.Lf[e] : (e < 288 ? L.M[e - 144] : L.invd[e - 288]);
+  const bool fin = L.s_final != 0;
+  constexpr int kPer = (576 + NT - 1) / NT;
+  double pn[kPer];
+  if (fin) {
+    // P = (I - K H) P with K H [:, :12] = G S^-1 M (esekfom.hpp:341-343)
+    if (!valid) {
+      for (int e = t; e < 288; e += NT) {
+        const double v = ctl->LM[e];
+        if (e < 144)
+          L.Lf[e] = v;
+        else
+          L.M[e - 144] = v;
+      }
+      if (t < 12) L.invd[t] = ctl->LM[288 + t];
+      __syncthreads();
+    }
+    if (t < 12) {
+      // column t of Z = S^-1 M = L^-T L^-1 M
+      double zc[12];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        double s2 = L.M[j * 12 + t];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s2 = fma(-L.Lf[j * 12 + k], zc[k], s2);
+        zc[j] = s2 * L.invd[j];
+      }
+#pragma unroll
+      for (int j = 11; j >= 0; --j) {
+        double s2 = zc[j];
+#pragma unroll
+        for (int k = j + 1; k < 12; ++k) s2 = fma(-L.Lf[k * 12 + j], zc[k], s2);
+        zc[j] = s2 * L.invd[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 12; ++j) L.Z[j * 12 + t] = zc[j];
     }
     __syncthreads();
-    SSTAMP(5);
-    if (t < 64) {
-      const bool ok = gj12_wave(L);
-      if (t == 0) L.piv = ok ? 1 : 0;
-    }
-    __syncthreads();
-    SSTAMP(6);
-    if (!L.piv) {
-      if (t == 0) {
-        ctl->singular = 1;
-        ctl->done = 1;
-      }
-      return;
-    }
     for (int e = t; e < 288; e += NT) {
       const int r = e / 12, cc = e - r * 12;
       double s2 = 0.0;
-      for (int k = 0; k < 12; ++k) s2 += L.P[r * 24 + k] * L.a[k][12 + cc];
-      L.K12[e] = s2;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) s2 = fma(L.G[r * 12 + k], L.Z[k * 12 + cc], s2);
+      L.K[e] = s2;
     }
     __syncthreads();
-    SSTAMP(7);
-    if (t < 24) {
-      double s2 = 0.0;
-      for (int j = 0; j < 12; ++j) s2 += L.K12[t * 12 + j] * L.tot[SLIO_NHTH + j];
-      L.Kh[t] = s2 / R;
-    }
-    for (int e = t; e < 576; e += NT) {
-      const int r = e / 24, cc = e - r * 24;
-      double v = 0.0;
-      if (cc < 12)
-        for (int j = 0; j < 12; ++j) v += L.K12[r * 12 + j] * L.M[j * 12 + cc];
-      L.KH[e] = v;
-      ctl->KH[e] = v;
-    }
-    __syncthreads();
-    if (t < 24) {
-      double s2 = 0.0;
-      for (int j = 0; j < 24; ++j) s2 += (L.KH[t * 24 + j] - (t == j ? 1.0 : 0.0)) * L.dxn[j];
-      L.dx[t] = L.Kh[t] + s2;
-    }
-    __syncthreads();
-    SSTAMP(8);
-  }
-  // any |dx| > epsi (esekfom.hpp:17, 325-331), wave 0 ballot
-  bool big = false;
-  if (t < 64) {
-    const bool b = valid && t < 24 && fabs(L.dx[t]) > 0.001;
-    big = __ballot(b) != 0;
-  }
-  if (t == 0) {
-    int32_t* f = L.fl;
-    f[F_PASSES] += 1;
-    f[F_SEARCHES] += f[F_SEARCH];
-    int fin = 0;
-    if (valid) {
-      f[F_VALID] += 1;
-      if (f[F_MODE] == SLIO_MODE_FIXED) {
-        fin = i == maxit - 1;
-        f[F_SEARCH] = 1;
-      } else {
-        const int conv = big ? 0 : 1;
-        f[F_CONV] = conv;
-        if (conv) f[F_T] += 1;
-        if (!f[F_T] && i == maxit - 2) f[F_CONV] = 1;
-        fin = (f[F_T] > 1 || i == maxit - 1);
-        f[F_SEARCH] = f[F_CONV];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = t + u * NT;
+      if (e < 576) {
+        const int r = e / 24, cc = e - r * 24;
+        double s2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) s2 = fma(L.K[r * 12 + k], L.P[k * 24 + cc], s2);
+        pn[u] = L.P[e] - s2;
+        ctl->P[e] = pn[u];
       }
-    } else if (i == maxit - 1) {
-      // reference: the loop ends without the P update; fixed mode applies
-      // the last valid pass's K H if there was one
-      fin = (f[F_MODE] == SLIO_MODE_FIXED && f[F_VALID] > 0);
     }
-    if (fin || i == maxit - 1) f[F_DONE] = 1;
-    L.s_final = fin;
-    ctl->last_m = m;
   }
-  __syncthreads();
-  SSTAMP(9);
-  const bool fin = L.s_final != 0;
-  if (fin && !valid)
-    for (int e = t; e < 576; e += NT) L.KH[e] = ctl->KH[e];  // last valid pass's K H
-  __syncthreads();
-  // x [+] dx on one lane, overlapped with P = (I - K H) P (esekfom.hpp:341-343)
-  if (valid && (t == NT - 1 || t == NT - 65)) state_boxplus_part(L.x, L.dx, t == NT - 1);
-  if (fin)
-    for (int e = t; e < 576; e += NT) {
-      const int r = e / 24, cc = e - r * 24;
-      double s2 = 0.0;
-      for (int q = 0; q < 24; ++q) s2 += ((r == q ? 1.0 : 0.0) - L.KH[r * 24 + q]) * L.P[q * 24 + cc];
-      ctl->P[e] = s2;
-    }
-  __syncthreads();
-  SSTAMP(10);
+  SSTAMP(7);
   {
-    const double* src = reinterpret_cast<const double*>(&L.x);
-    double* dst = reinterpret_cast<double*>(&ctl->x);
-    for (int e = t; e < kStateD; e += NT) dst[e] = src[e];
+    const double* xs = reinterpret_cast<const double*>(&L.x);
+    double* xd = reinterpret_cast<double*>(&ctl->x);
+    for (int e = t; e < kStateD; e += NT) xd[e] = xs[e];
   }
   if (t < 8) (&ctl->converge)[t] = L.fl[t];
-  SSTAMP(11);
+  if (t == 0) ctl->last_m = m;
+  if (L.fl[F_DONE]) {
+    // the update ends: x, P and the flags to the caller's mapped host block
+    // (visible to the host once the kernel has completed)
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = t + u * NT;
+      if (e < 576) hblk->P[e] = fin ? pn[u] : L.P[e];
+    }
+    const double* xs = reinterpret_cast<const double*>(&L.x);
+    double* xd = reinterpret_cast<double*>(&hblk->x);
+    for (int e = t; e < kStateD; e += NT) xd[e] = xs[e];
+    if (t < 8) (&hblk->converge)[t] = L.fl[t];
+    if (t == 0) {
+      hblk->last_m = m;
+      hblk->singular = 0;
+    }
+    __threadfence_system();
+  }
+  SSTAMP(8);
 }
 
 // fixed-order product phase: rows[SLIO_CHUNK][kRow] in LDS -> chunk partial.
@@ -968,6 +1105,33 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
 template <int LPQ>
 constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
 
+// dx_new = x [-] x_propagated (esekfom.hpp:236-258) of the iterate a
+// device-resident pass runs at, for that pass's filter step: formed by block
+// 0 of the pass kernel (lanes 0..23 the vector blocks, lanes 32 / 64 the
+// two rotations, on different wavefronts) while the pass itself runs, off
+// the filter step's critical path.  Needs >= 128 threads.
+__device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
+  if (blockIdx.x != 0) return;
+  const int t = threadIdx.x;
+  if (t < 24) {
+    const int k = t;
+    if (k < 3 || k >= 9) {
+      const double* xs = reinterpret_cast<const double*>(&ctl->x);
+      const double* ps = reinterpret_cast<const double*>(&ctl->xprop);
+      ctl->dxn[k] = xs[state_off(k)] - ps[state_off(k)];
+    }
+  } else if (t == 32 || t == 64) {
+    const int u = t == 32;
+    const double* q1 = u ? ctl->x.rli : ctl->x.rot;
+    const double* q2 = u ? ctl->xprop.rli : ctl->xprop.rot;
+    double d[3];
+    so3_boxminus(Quat{q1[0], q1[1], q1[2], q1[3]}, Quat{q2[0], q2[1], q2[2], q2[3]}, d);
+    ctl->dxn[3 + 3 * u] = d[0];
+    ctl->dxn[4 + 3 * u] = d[1];
+    ctl->dxn[5 + 3 * u] = d[2];
+  }
+}
+
 // One h_share_model search pass over one 128-point chunk.
 // Phase 1 (kNN): LPQ lanes per scan point find the exact 5-NN; results go to
 // LDS.  Phase 2 (fit): one lane per point reloads the 5 neighbours (L2-hot),
@@ -983,6 +1147,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     return;
   const PoseDev pose = DEVPOSE ? pose_from_state(cfg.ctl->x) : pose_arg;
   constexpr int NT = search_block<LPQ>();
+  if (DEVPOSE) ikf_dx_new(cfg.ctl);
   constexpr int QPP = NT / LPQ;               // queries per kNN pass
   constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
   static_assert(SLIO_CHUNK % QPP == 0, "chunk must be a multiple of queries/pass");
@@ -1208,6 +1373,7 @@ __global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan,
                   cfg.ctl->search_now != cfg.want_search))
     return;
   const PoseDev pose = DEVPOSE ? pose_from_state(cfg.ctl->x) : pose_arg;
+  if (DEVPOSE) ikf_dx_new(cfg.ctl);
   __shared__ double rows[SLIO_CHUNK][kRow];
   __shared__ double part[1][SLIO_NPROD];
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
@@ -1244,69 +1410,108 @@ __global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan,
   chunk_products<SLIO_CHUNK>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
 }
 
-// super-chunk sums in a fixed order: segment g of the 8 sums chunks
-// c0+g, c0+g+8, ... sequentially, then the 8 segment sums are added in order.
-// Rows of super-chunks this rank does not own are written as zeros.
-// ctl != null (single-rank device-resident update): the last of the 8 blocks
-// to finish (threadfence reduction: agent-scope release + counter, acquire
-// in the last block) runs the filter step on the 8 rows, so a pass plus its
-// filter step is two launches.
-__global__ __launch_bounds__(SLIO_NPROD * kSuperSeg) void k_super_sums(
-    const double* __restrict__ chunk_part, int64_t C, int s_begin, int s_end,
-    double* super_out, IkfCtl* ctl, uint32_t* count, double R, int iter, int maxit) {
-  constexpr int NT = SLIO_NPROD * kSuperSeg;
-  __shared__ double part[kSuperSeg][SLIO_NPROD];
+// Super-chunk sums in a fixed order: segment g of the 8 sums chunks c0+g,
+// c0+g+8, ... sequentially, then the 8 segment sums are added in order.  Rows
+// of super-chunks this rank does not own are written as zeros, so a SUM
+// all-reduce over ranks is an exact gather.
+// ctl != null (single-rank device-resident update): the super rows are
+// published write-through (sc1) and drained, one lane per block arrives on
+// cnt, and the block whose arrival completes the count -- told by the value
+// its add returned -- reads the other seven rows with sc1 loads and runs the
+// filter step (MI355X_MICROARCH.md, inter-workgroup visibility: first row of
+// the sc1 hand-off table).  A pass plus its filter step is two launches.
+__global__ __launch_bounds__(kSolveThreads) void k_super_sums(
+    const double* __restrict__ chunk_part, int64_t C, int s_begin, int s_end, double* super_out,
+    IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, uint32_t* cnt, double R, int iter, int maxit) {
+  constexpr int NT = kSolveThreads;
+  constexpr int KP = (kSuperSeg * SLIO_NPROD + NT - 1) / NT;  // (segment, product) pairs per thread
+  __shared__ double part[kSuperSeg * SLIO_NPROD];
   __shared__ SolveLds L;
   __shared__ int last;
   const int s = blockIdx.x;
   const int t = threadIdx.x;
-  const int seg = t / SLIO_NPROD, kk = t % SLIO_NPROD;
   if (ctl) SSTAMP(0);
-  double acc = 0.0;
-  if (s >= s_begin && s < s_end) {
+  {
+    // pair p = g * NPROD + kk: segment g, product kk; chunk c0 + g + 8 j of
+    // pair p sits at chunk_part[(c0 + 8 j) * NPROD + p]
+    double acc[KP];
+    int64_t lim[KP];
     const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
+    const bool mine = s >= s_begin && s < s_end;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const int p = t + k * NT;
+      const int g = p / SLIO_NPROD;
+      lim[k] = (mine && p < kSuperSeg * SLIO_NPROD) ? (c1 - c0 - g + kSuperSeg - 1) / kSuperSeg : 0;
+      acc[k] = 0.0;
+    }
+    const int64_t nj = lim[0];  // segment 0 is the longest
+    const double* base = chunk_part + c0 * SLIO_NPROD + t;
+    // the first kJ chunks of every segment in one round trip: all KP * kJ
+    // loads are issued before the first add (a pair past its last chunk
+    // adds 0); C2's 100k-point scan has <= 13 chunks per segment
+    constexpr int kJ = 16;
+    {
+      double v[KP][kJ];
+#pragma unroll
+      for (int j = 0; j < kJ; ++j)
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+          v[k][j] = j < lim[k] ? base[j * (kSuperSeg * SLIO_NPROD) + k * NT] : 0.0;
+#pragma unroll
+      for (int j = 0; j < kJ; ++j)
+#pragma unroll
+        for (int k = 0; k < KP; ++k) acc[k] = acc[k] + v[k][j];
+    }
+    // longer scans: the rest, branch-free (a pair past its last chunk
+    // re-reads a valid address and adds 0)
 #pragma unroll 4
-    for (int64_t c = c0 + seg; c < c1; c += kSuperSeg) acc = acc + chunk_part[c * SLIO_NPROD + kk];
+    for (int64_t j = kJ; j < nj; ++j) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const int64_t jj = j < lim[k] ? j : (lim[k] > 0 ? lim[k] - 1 : 0);
+        const double v = lim[k] > 0 ? base[jj * (kSuperSeg * SLIO_NPROD) + k * NT] : 0.0;
+        acc[k] = acc[k] + (j < lim[k] ? v : 0.0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (t + k * NT < kSuperSeg * SLIO_NPROD) part[t + k * NT] = acc[k];
   }
-  part[seg][kk] = acc;
   __syncthreads();
   if (t < SLIO_NPROD) {
-    double v = part[0][t];
+    double v = part[t];
 #pragma unroll
-    for (int q = 1; q < kSuperSeg; ++q) v = v + part[q][t];
-    super_out[s * SLIO_NPROD + t] = v;
+    for (int q = 1; q < kSuperSeg; ++q) v = v + part[q * SLIO_NPROD + t];
     L.sup[s][t] = v;
+    if (ctl)
+      st_sc1(super_out + s * SLIO_NPROD + t, v);
+    else
+      super_out[s * SLIO_NPROD + t] = v;
   }
   if (!ctl) return;
-  SSTAMP(1);
-  __threadfence();
+  drain_stores();
   __syncthreads();
-  if (t == 0) last = atomicAdd(count, 1u) == (uint32_t)(SLIO_NSUPER - 1);
+  SSTAMP(1);
+  if (t == 0) last = arrive(cnt) == (uint32_t)(SLIO_NSUPER - 1);
   __syncthreads();
   if (!last) return;
   SSTAMP(2);
-  __threadfence();
-  if (t == 0) *count = 0;
-  for (int e = t; e < SLIO_NSUPER * SLIO_NPROD; e += NT) {
-    const int q = e / SLIO_NPROD;
-    if (q != s) L.sup[q][e - q * SLIO_NPROD] = super_out[e];
-  }
-  __syncthreads();
+  if (t == 0) reset_counter(cnt);
+  if (src == ctl && ctl->done) return;  // the first pass of an update always runs
   SSTAMP(3);
-  if (ctl->done) return;
-  ikf_solve_block<NT>(ctl, R, iter, maxit, L);
+  ikf_solve_block<NT>(ctl, src, hblk, R, iter, maxit, L, super_out,
+                      ((1u << SLIO_NSUPER) - 1u) & ~(1u << s));
 }
 
 // ---------------------------------------------------------------- device IKF
 // Filter step after the multi-rank all-reduce: super sums from HBM.
-__global__ __launch_bounds__(kSolveThreads) void k_ikf_solve(IkfCtl* ctl, const double* sup,
+__global__ __launch_bounds__(kSolveThreads) void k_ikf_solve(IkfCtl* ctl, const IkfCtl* src,
+                                                             IkfCtl* hblk, const double* sup,
                                                              double R, int i, int maxit) {
   __shared__ SolveLds L;
-  if (ctl->done) return;
-  for (int e = threadIdx.x; e < SLIO_NSUPER * SLIO_NPROD; e += kSolveThreads)
-    L.sup[e / SLIO_NPROD][e % SLIO_NPROD] = sup[e];
-  __syncthreads();
-  ikf_solve_block<kSolveThreads>(ctl, R, i, maxit, L);
+  if (src == ctl && ctl->done) return;
+  ikf_solve_block<kSolveThreads>(ctl, src, hblk, R, i, maxit, L, sup, (1u << SLIO_NSUPER) - 1u);
 }
 
 // ---------------------------------------------------------------- context
@@ -1328,9 +1533,10 @@ struct Ctx {
   double* chunk_part = nullptr;
   double* d_super = nullptr;
   double* d_super_own = nullptr;
-  uint32_t* count = nullptr;  // k_super_sums last-block counter (zero between launches)
+  uint32_t* count = nullptr;  // k_super_sums arrival counter (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
-  IkfCtl* h_ctl = nullptr;  // pinned staging copy
+  IkfCtl* h_ctl = nullptr;  // mapped, coherent host block: update input and output
+  IkfCtl* d_hctl = nullptr; // its device view
   hipEvent_t done_ev = nullptr;  // end of a device-resident update (polled)
   double* h_super = nullptr;  // pinned
   bool searched = false;
@@ -1450,14 +1656,19 @@ static hipError_t wait_stream(Ctx& c) {
 
 // Fused filter step of a single-rank device-resident update.
 struct SolveArgs {
-  int on;        // run the filter step in the pass epilogue
+  int on;        // run the filter step in the super-sum kernel (single rank)
   int pass_idx;  // ctl->passes this pass belongs to
   int iter, maxit;
   double R;
+  const IkfCtl* src;  // control block source: the mapped host block on pass 0, else ctl
+  IkfCtl* hblk;       // mapped host block (device view): update output
 };
 
+static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa);
+
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
-                        int extrinsic_est, const SolveArgs* sa = nullptr) {
+                        int extrinsic_est, const SolveArgs* sa = nullptr,
+                        bool with_super = true) {
   if (!c.map) {
     set_error("slio pass: no map uploaded");
     return SLIO_ESTATE;
@@ -1473,8 +1684,11 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   const int64_t C = num_chunks(c.n);
   int64_t c0, c1;
   rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
+  // pose: by value (host-driven passes and the first pass of a device-resident
+  // update) or from the control block in HBM (later device-resident passes)
+  const bool devpose = ctl && !Parg;
   PassCfg cfg;
-  cfg.ctl = ctl;
+  cfg.ctl = devpose ? ctl : nullptr;
   cfg.want_search = 1;
   cfg.plane_thr = c.prm.plane_threshold;
   cfg.max_sqd = c.prm.max_match_sqd;
@@ -1516,7 +1730,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
                         ev.first, ev.second, 0, mv, s, P, cfg, o)
 #define SLIO_LAUNCH2(L, SPH) \
   do {                        \
-    if (ctl)                  \
+    if (devpose)              \
       SLIO_LAUNCH(L, SPH, true); \
     else                      \
       SLIO_LAUNCH(L, SPH, false); \
@@ -1539,26 +1753,36 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     PassCfg rcfg = cfg;
     rcfg.want_search = 0;
     const dim3 nb((unsigned)nblk), bs(SLIO_CHUNK);
-    if (ctl)
+    if (devpose)
       hipExtLaunchKernelGGL(k_reuse_pass<true>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
                             rcfg, o);
     else
       hipExtLaunchKernelGGL(k_reuse_pass<false>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
                             rcfg, o);
   }
-  {
-    const auto ev = timing(SLIO_KERNEL_SUPER);
-    // single-rank device-resident update: + filter step in the last block
-    const bool fuse = sa && sa->on;
-    hipExtLaunchKernelGGL(k_super_sums, dim3(SLIO_NSUPER), dim3(SLIO_NPROD * kSuperSeg), 0,
-                          c.stream, ev.first, ev.second, 0, (const double*)c.chunk_part, C,
-                          c.prm.rank * per, (c.prm.rank + 1) * per, c.d_super,
-                          fuse ? ctl : (IkfCtl*)nullptr, c.count, fuse ? sa->R : 0.0,
-                          fuse ? sa->iter : 0, fuse ? sa->maxit : 0);
-  }
+  if (with_super) enqueue_super(c, ctl, sa);
   SLIO_HIP(hipGetLastError());
   if (which != 0) c.searched = true;
   return SLIO_OK;
+}
+
+// Super-chunk sums of the pass just enqueued (+ the filter step of a
+// single-rank device-resident update).
+static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa) {
+  const int64_t C = num_chunks(c.n);
+  const int per = SLIO_NSUPER / c.prm.nranks;
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (c.prof && (c.prof_mask & (1 << SLIO_KERNEL_SUPER))) {
+    ev = prof_pair(c);
+    c.pending[SLIO_KERNEL_SUPER].push_back(ev);
+  }
+  const bool fuse = sa && sa->on;
+  hipExtLaunchKernelGGL(k_super_sums, dim3(SLIO_NSUPER), dim3(kSolveThreads), 0, c.stream,
+                        ev.first, ev.second, 0, (const double*)c.chunk_part, C,
+                        c.prm.rank * per, (c.prm.rank + 1) * per, c.d_super,
+                        fuse ? ctl : (IkfCtl*)nullptr, fuse ? sa->src : (const IkfCtl*)nullptr,
+                        fuse ? sa->hblk : (IkfCtl*)nullptr, c.count, fuse ? sa->R : 0.0,
+                        fuse ? sa->iter : 0, fuse ? sa->maxit : 0);
 }
 
 }  // namespace slio
@@ -1651,8 +1875,8 @@ int slio_create(slio_handle* out, const slio_params* p) {
   h->c.stream = h->c.own_stream;
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
-      hipMalloc(&h->c.count, sizeof(uint32_t) * 4) != hipSuccess ||
-      hipMemset(h->c.count, 0, sizeof(uint32_t) * 4) != hipSuccess) {
+      hipMalloc(&h->c.count, sizeof(uint32_t) * 16) != hipSuccess ||
+      hipMemset(h->c.count, 0, sizeof(uint32_t) * 16) != hipSuccess) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
     return SLIO_ENOMEM;
@@ -1924,7 +2148,8 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   Ctx& c = h->c;
   if (!c.ctl) {
     SLIO_HIP(hipMalloc(&c.ctl, sizeof(IkfCtl)));
-    SLIO_HIP(hipHostMalloc(&c.h_ctl, sizeof(IkfCtl)));
+    SLIO_HIP(hipHostMalloc(&c.h_ctl, sizeof(IkfCtl), hipHostMallocMapped | hipHostMallocCoherent));
+    SLIO_HIP(hipHostGetDevicePointer((void**)&c.d_hctl, c.h_ctl, 0));
   }
   IkfCtl& hc = *c.h_ctl;
   hc.x = *x;
@@ -1938,26 +2163,57 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   hc.mode = mode;
   hc.last_m = 0;
   hc.singular = 0;
-  SLIO_HIP(hipMemcpyAsync(c.ctl, c.h_ctl, sizeof(IkfCtl), hipMemcpyHostToDevice, c.stream));
+  for (int k = 0; k < 24; ++k) hc.dxn[k] = 0.0;  // x == x_propagated on pass 0
+  // The control block comes in and goes out through the mapped host block:
+  // pass 0 takes its pose by value and its filter step reads the block over
+  // the bus (then keeps it in HBM); the step that ends the update writes x,
+  // P and the flags back.  No copy-engine work on the path.
   const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
+  const PoseDev pose0 = [&] {
+    slio_pose p;
+    std::memcpy(p.rot, x->rot, sizeof(p.rot));
+    std::memcpy(p.pos, x->pos, sizeof(p.pos));
+    std::memcpy(p.rli, x->rli, sizeof(p.rli));
+    std::memcpy(p.tli, x->tli, sizeof(p.tli));
+    return make_pose(&p);
+  }();
   for (int i = first; i < maximum_iter; ++i) {
-    // single rank: the filter step runs in the pass kernel's last block;
+    // single rank: the filter step runs in the super-sum kernel's last block;
     // multi-rank: pass -> all-reduce of the super sums -> k_ikf_solve
-    const SolveArgs sa{reduce ? 0 : 1, i - first, i, maximum_iter, R};
-    int rc = enqueue_pass(c, nullptr, c.ctl, mode == SLIO_MODE_FIXED ? 1 : 2, extrinsic_est, &sa);
+    const bool p0 = i == first;
+    const IkfCtl* src = p0 ? (const IkfCtl*)c.d_hctl : c.ctl;
+    const SolveArgs sa{reduce ? 0 : 1, i - first, i, maximum_iter, R, src, c.d_hctl};
+    // pass 0 always searches (converge starts true, esekfom.hpp:282)
+    const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
+    int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, extrinsic_est, &sa, !p0 || reduce);
     if (rc) return rc;
+    if (p0) {
+      // information-form constants of the update (P is fixed until its end),
+      // formed on the host while pass 0's search runs; pass 0's filter step
+      // reads them from the mapped block
+      if (!info_constants(P, hc.P11i, hc.G)) {
+        (void)hipStreamSynchronize(c.stream);
+        set_error("slio_ikf_update_device: singular covariance block P[:12, :12]");
+        return SLIO_EINVAL;
+      }
+      if (!reduce) enqueue_super(c, c.ctl, &sa);
+    }
     if (reduce) {
       rc = reduce(reduce_ctx, c.d_super, (int64_t)SLIO_NSUPER * SLIO_NPROD, (void*)c.stream);
       if (rc) {
         set_error("slio_ikf_update_device: reduce callback failed");
         return SLIO_EDEVICE;
       }
-      k_ikf_solve<<<1, kSolveThreads, 0, c.stream>>>(c.ctl, c.d_super, R, i, maximum_iter);
+      k_ikf_solve<<<1, kSolveThreads, 0, c.stream>>>(c.ctl, src, c.d_hctl, c.d_super, R, i,
+                                                     maximum_iter);
     }
   }
   SLIO_HIP(hipGetLastError());
-  SLIO_HIP(hipMemcpyAsync(c.h_ctl, c.ctl, sizeof(IkfCtl), hipMemcpyDeviceToHost, c.stream));
   SLIO_HIP(wait_stream(c));
+  if (!c.h_ctl->done) {
+    set_error("slio_ikf_update_device: the update did not complete");
+    return SLIO_EDEVICE;
+  }
   if (c.h_ctl->singular) {
     set_error("slio_ikf_update_device: singular covariance");
     return SLIO_EINVAL;

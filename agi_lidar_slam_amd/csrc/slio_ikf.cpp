@@ -6,8 +6,8 @@
 // gain K of the reference is never formed:
 //   K * h       = K_front[:, :12] * (H^T h) / R
 //   (K * H)[:, :12] = K_front[:, :12] * (H^T H) / R
-// and K_front[:, :12] comes from a 12x12 inverse (see filter_step): all
-// algebraically identical to esekfom.hpp:306-319.  The control flow
+// and K_front[:, :12] = G S^-1 comes from a 12x12 Cholesky (see filter_step):
+// all algebraically identical to esekfom.hpp:306-319.  The control flow
 // (passes i = -1 .. maximum_iter-1, re-search only after a converged pass or
 // forced at i == maximum_iter-2, skip on effct_feat_num < 1, final
 // P = (I - KH) P) follows esekfom.hpp:292-345 line for line.
@@ -74,64 +74,124 @@ slio_pose pose_of(const slio_state& x) {
 }
 
 // One filter update from the pass sums (esekfom.hpp:303-321), updating x and
-// returning K H and dx.  K_front[:, :12] = (H^T H / R + P^-1)^-1 [:, :12] is
-// evaluated with the push-through identity
-//   (P^-1 + E^T M E)^-1 E^T = P E^T (I + M E P E^T)^-1,  M = H^T H / R,
-// i.e. K12 = P[:, :12] (I + M P11)^-1: one 12x12 inverse, no P^-1 (the
-// reference inverts two 24x24 matrices per pass, esekfom.hpp:311).  The
-// device kernel k_ikf_solve uses exactly this operation order.
-bool filter_step(const slio_state& x_prop, const double* P, double R, const double HTH[78],
-                 const double HTh[12], slio_state& x, double KH[576], double dx[24]) {
+// returning K H [:, :12] (K H [:, 12:] = 0) and dx.  With M = H^T H / R and
+// the push-through identity (P^-1 + E^T M E)^-1 E^T = G S^-1,
+// S = P11^-1 + M (SPD), G = P[:, :12] P11^-1:
+//   K h + (K H - I) dx_new = G S^-1 v - dx_new,  v = H^T h / R + M dx_new[:12]
+//   K H [:, :12] = G S^-1 M
+// one 12 x 12 Cholesky per pass instead of the reference's two 24 x 24
+// inverses (esekfom.hpp:311).  The device filter step (ikf_solve_block,
+// slio_device.hip) performs the same operations in the same order.
+bool filter_step(const slio_state& x_prop, const double* P11i, const double* G, double R,
+                 const double HTH[78], const double HTh[12], slio_state& x, double K12[288],
+                 double dx[24]) {
   double dx_new[24];
   boxminus(x, x_prop, dx_new);
-  double M[144];
-  int k = 0;
-  for (int i = 0; i < 12; ++i)
-    for (int j = i; j < 12; ++j) {
-      const double v = HTH[k] / R;
-      M[i * 12 + j] = v;
-      M[j * 12 + i] = v;
-      ++k;
-    }
-  double B[144], X[144];
+  double M[144], S[144];
   for (int r = 0; r < 12; ++r)
-    for (int j = 0; j < 12; ++j) {
-      double s = 0.0;
-      for (int q = 0; q < 12; ++q) s += M[r * 12 + q] * P[q * 24 + j];
-      B[r * 12 + j] = (r == j ? 1.0 : 0.0) + s;
-    }
-  if (!invert<12>(B, X)) return false;
-  double K12[288];
-  for (int r = 0; r < 24; ++r)
     for (int c = 0; c < 12; ++c) {
-      double s = 0.0;
-      for (int q = 0; q < 12; ++q) s += P[r * 24 + q] * X[q * 12 + c];
-      K12[r * 12 + c] = s;
+      const int i = r <= c ? r : c, j = r <= c ? c : r;
+      const double m = HTH[i * 12 - (i * (i - 1)) / 2 + (j - i)] / R;
+      M[r * 12 + c] = m;
+      S[r * 12 + c] = P11i[r * 12 + c] + m;
     }
-  double Kh[24];
-  for (int r = 0; r < 24; ++r) {
-    double s = 0.0;
-    for (int j = 0; j < 12; ++j) s += K12[r * 12 + j] * HTh[j];
-    Kh[r] = s / R;
-    for (int c = 0; c < 24; ++c) {
-      double v = 0.0;
-      if (c < 12)
-        for (int j = 0; j < 12; ++j) v += K12[r * 12 + j] * M[j * 12 + c];
-      KH[r * 24 + c] = v;
+  double v[12];
+  for (int r = 0; r < 12; ++r) {
+    double s2 = 0.0;
+    for (int k = 0; k < 12; ++k) s2 = std::fma(M[r * 12 + k], dx_new[k], s2);
+    v[r] = HTh[r] / R + s2;
+  }
+  // S = L L^T (right-looking, column j scaled by 1 / L[j][j])
+  double L[144], invd[12];
+  std::memcpy(L, S, sizeof(L));
+  for (int j = 0; j < 12; ++j) {
+    const double d = L[j * 12 + j];
+    if (!(d > 0.0)) return false;
+    const double ljj = std::sqrt(d);
+    const double inv = 1.0 / ljj;
+    invd[j] = inv;
+    L[j * 12 + j] = ljj;
+    for (int i = j + 1; i < 12; ++i) L[i * 12 + j] = L[i * 12 + j] * inv;
+    for (int k = j + 1; k < 12; ++k)
+      for (int i = k; i < 12; ++i) L[i * 12 + k] = std::fma(-L[i * 12 + j], L[k * 12 + j], L[i * 12 + k]);
+  }
+  // S y = v
+  double r[12], y[12];
+  std::memcpy(r, v, sizeof(r));
+  for (int j = 0; j < 12; ++j) {
+    const double zj = r[j] * invd[j];
+    r[j] = zj;
+    for (int i = j + 1; i < 12; ++i) r[i] = std::fma(-L[i * 12 + j], zj, r[i]);
+  }
+  for (int j = 11; j >= 0; --j) {
+    const double yj = r[j] * invd[j];
+    y[j] = yj;
+    for (int i = 0; i < j; ++i) r[i] = std::fma(-L[j * 12 + i], yj, r[i]);
+  }
+  for (int q = 0; q < 24; ++q) {
+    double s2 = 0.0;
+    for (int k = 0; k < 12; ++k) s2 = std::fma(G[q * 12 + k], y[k], s2);
+    dx[q] = s2 - dx_new[q];
+  }
+  // K H [:, :12] = G Z, Z = S^-1 M (column by column)
+  double Z[144];
+  for (int c = 0; c < 12; ++c) {
+    double zc[12];
+    for (int j = 0; j < 12; ++j) {
+      double s2 = M[j * 12 + c];
+      for (int k = 0; k < j; ++k) s2 = std::fma(-L[j * 12 + k], zc[k], s2);
+      zc[j] = s2 * invd[j];
     }
+    for (int j = 11; j >= 0; --j) {
+      double s2 = zc[j];
+      for (int k = j + 1; k < 12; ++k) s2 = std::fma(-L[k * 12 + j], zc[k], s2);
+      zc[j] = s2 * invd[j];
+    }
+    for (int j = 0; j < 12; ++j) Z[j * 12 + c] = zc[j];
   }
-  for (int i = 0; i < 24; ++i) {
-    double s = 0.0;
-    for (int j = 0; j < 24; ++j) s += (KH[i * 24 + j] - (i == j ? 1.0 : 0.0)) * dx_new[j];
-    dx[i] = Kh[i] + s;
-  }
+  for (int q = 0; q < 24; ++q)
+    for (int c = 0; c < 12; ++c) {
+      double s2 = 0.0;
+      for (int k = 0; k < 12; ++k) s2 = std::fma(G[q * 12 + k], Z[k * 12 + c], s2);
+      K12[q * 12 + c] = s2;
+    }
   slio_state xn;
   boxplus(x, dx, xn);
   x = xn;
   return true;
 }
 
+// P = (I - K H) P = P - K H [:, :12] P[:12, :]  (esekfom.hpp:341-343)
+void covariance_update(double* P, const double K12[288]) {
+  double Pn[576];
+  for (int a = 0; a < 24; ++a)
+    for (int b = 0; b < 24; ++b) {
+      double s2 = 0.0;
+      for (int k = 0; k < 12; ++k) s2 = std::fma(K12[a * 12 + k], P[k * 24 + b], s2);
+      Pn[a * 24 + b] = P[a * 24 + b] - s2;
+    }
+  std::memcpy(P, Pn, sizeof(Pn));
+}
+
 }  // namespace
+
+// Information-form constants of one update (P_ is fixed until its end):
+// P11^-1 = (P[:12, :12])^-1 and G = P[:, :12] P11^-1.  The device-resident
+// update (slio_ikf_update_device) uses exactly these.
+bool slio::info_constants(const double* P, double P11i[144], double G[288]) {
+  double P11[144];
+  for (int r = 0; r < 12; ++r)
+    for (int q = 0; q < 12; ++q) P11[r * 12 + q] = P[r * 24 + q];
+  if (!invert<12>(P11, P11i)) return false;
+  for (int r = 0; r < 24; ++r)
+    for (int q = 0; q < 12; ++q) {
+      double v = 0.0;
+      for (int k = 0; k < 12; ++k) v += P[r * 24 + k] * P11i[k * 12 + q];
+      G[r * 12 + q] = v;
+    }
+  return true;
+}
+
 
 extern "C" {
 
@@ -161,8 +221,13 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
   const slio_state x_prop = *x;
   bool converge = true;  // dyn_share.converge (esekfom.hpp:282)
   int t = 0;
-  double KH[576];
+  double K12[288];
   double dx[24];
+  double P11i[144], G[288];
+  if (!info_constants(P, P11i, G)) {
+    set_error("slio_ikf_update: singular covariance block P[:12, :12]");
+    return SLIO_EINVAL;
+  }
   double sup[SLIO_NSUPER * SLIO_NPROD];
   const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
   double dev_ms = 0.0;
@@ -193,7 +258,7 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
       continue;
     }
     ++st.valid_passes;
-    if (!filter_step(x_prop, P, R, HTH, HTh, *x, KH, dx)) {
+    if (!filter_step(x_prop, P11i, G, R, HTH, HTh, *x, K12, dx)) {
       set_error("slio_ikf_update: singular covariance");
       return SLIO_EINVAL;
     }
@@ -210,31 +275,14 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
     if (converge) ++t;
     if (!t && i == maximum_iter - 2) converge = true;
     if (t > 1 || i == maximum_iter - 1) {
-      // P = (I - KH) * P  (esekfom.hpp:341-343)
-      double Pn[576];
-      for (int a = 0; a < 24; ++a)
-        for (int b = 0; b < 24; ++b) {
-          double s = 0.0;
-          for (int c = 0; c < 24; ++c) s += ((a == c ? 1.0 : 0.0) - KH[a * 24 + c]) * P[c * 24 + b];
-          Pn[a * 24 + b] = s;
-        }
-      std::memcpy(P, Pn, sizeof(Pn));
+      covariance_update(P, K12);
       st.converged = converge ? 1 : 0;
       st.device_ms = dev_ms;
       if (stats) *stats = st;
       return SLIO_OK;
     }
   }
-  if (mode == SLIO_MODE_FIXED && st.valid_passes > 0) {
-    double Pn[576];
-    for (int a = 0; a < 24; ++a)
-      for (int b = 0; b < 24; ++b) {
-        double s = 0.0;
-        for (int c = 0; c < 24; ++c) s += ((a == c ? 1.0 : 0.0) - KH[a * 24 + c]) * P[c * 24 + b];
-        Pn[a * 24 + b] = s;
-      }
-    std::memcpy(P, Pn, sizeof(Pn));
-  }
+  if (mode == SLIO_MODE_FIXED && st.valid_passes > 0) covariance_update(P, K12);
   st.converged = converge ? 1 : 0;
   st.device_ms = dev_ms;
   if (stats) *stats = st;

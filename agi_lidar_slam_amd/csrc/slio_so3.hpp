@@ -105,14 +105,26 @@ constexpr double kSmallEps = 1e-10;
 SLIO_HD inline Quat so3_exp(const double om[3]) {
   const double theta = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
   const double half = 0.5 * theta;
-  double imag;
-  const double real = cos(half);
+  double imag, real;
   if (theta < kSmallEps) {
     const double t2 = theta * theta;
     const double t4 = t2 * t2;
-    imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;
+    imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;  // Sophus a621ff's coefficients
+    real = cos(half);
+  } else if (half < 0.125) {
+    // IKF increments: sin(h) / h and cos(h) by their Taylor series through
+    // h^12 (remainder < 1e-22 relative at h = 0.125) -- no argument
+    // reduction, a short dependent chain on the GPU
+    const double u = half * half;
+    const double sh = 1.0 + u * (-1.0 / 6 + u * (1.0 / 120 + u * (-1.0 / 5040 + u * (1.0 / 362880 +
+                      u * (-1.0 / 39916800 + u * (1.0 / 6227020800.0))))));
+    real = 1.0 + u * (-0.5 + u * (1.0 / 24 + u * (-1.0 / 720 + u * (1.0 / 40320 +
+           u * (-1.0 / 3628800 + u * (1.0 / 479001600.0))))));
+    imag = 0.5 * sh;
   } else {
-    imag = sin(half) / theta;
+    double sh;
+    sincos(half, &sh, &real);  // one argument reduction for both
+    imag = sh / theta;
   }
   return qnormalized(Quat{real, imag * om[0], imag * om[1], imag * om[2]});
 }

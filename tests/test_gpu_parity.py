@@ -327,8 +327,11 @@ def test_full_size_c2_properties(L, oracle_mod):
 
 @pytest.mark.parametrize("mode,ext", [(0, False), (1, False), (0, True)])
 def test_device_loop_matches_host_loop(L, c1, mode, ext):
-    """slio_ikf_update_device (24x24 step on device) vs slio_ikf_update (host):
-    same operation order; only libm sin/cos/atan may differ by an ulp."""
+    """slio_ikf_update_device (filter step on device) vs slio_ikf_update (host):
+    the same information-form algebra in the same order; the device takes
+    1/sqrt from v_rsq_f64 + Newton and OCML sin/cos/atan, so single ulps
+    differ.  P = (I - K H) P cancels in well-observed directions, so P is held
+    to the same bar as against the oracle (1e-8 of max |P|)."""
     from agi_lidar_slam_amd.esekf import Esekf, KdTreeMap, StateIkfom
     mp, fr, _ = c1["avia"]
     st = state_of(fr)
@@ -348,5 +351,5 @@ def test_device_loop_matches_host_loop(L, c1, mode, ext):
     (x0, P0, s0), (x1, P1, s1) = out
     assert s0 == s1
     np.testing.assert_allclose(x1, x0, rtol=0, atol=1e-9)
-    np.testing.assert_allclose(P1, P0, rtol=0, atol=1e-9 * np.abs(P0).max())
+    np.testing.assert_allclose(P1, P0, rtol=0, atol=1e-8 * np.abs(P0).max())
     kd.close()
