@@ -266,45 +266,38 @@ __device__ __forceinline__ bool residual_gate(const float (&abcd)[4], float wx, 
 }
 
 // ---------------------------------------------------------------- top-5
-// A per-lane sorted list of the 5 best candidates.  Key = (float bits of the
-// squared distance << 32) | map index, so one u64 compare orders by distance
-// then index (squared distances are >= +0, whose bit patterns sort like the
-// values).  p[] holds the candidates' positions in the cell-sorted map.
+// Sorted top-5 list of 64-bit keys (float bits(squared distance) << 32) |
+// position in the cell-sorted map: one u64 compare orders by distance, then
+// by map position (squared distances are >= +0, whose bit patterns sort like
+// the values).  The map index is read back from the point (float4.w) only for
+// the five winners.
 struct Top5 {
   uint64_t k[5];
-  uint32_t p[5];
 };
 
 __device__ __forceinline__ void top5_clear(Top5& t) {
 #pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    t.k[j] = kInfKey;
-    t.p[j] = 0;
-  }
+  for (int j = 0; j < 5; ++j) t.k[j] = kInfKey;
 }
 
 // Branch-free insertion: slot j takes k[j-1] if key < k[j-1], key if
-// k[j-1] <= key < k[j], else keeps k[j].  All five slots update in parallel
-// (no serial compare-swap chain).
-__device__ __forceinline__ void top5_insert(Top5& t, uint64_t key, uint32_t pos) {
+// k[j-1] <= key < k[j], else keeps k[j]; a key >= k[4] changes nothing.  All
+// five slots update in parallel (no serial compare-swap chain, no divergent
+// branch: across a wavefront some lane nearly always inserts).
+__device__ __forceinline__ void top5_insert(Top5& t, uint64_t key) {
   bool c[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j) c[j] = key < t.k[j];
 #pragma unroll
-  for (int j = 4; j > 0; --j) {
-    t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
-    t.p[j] = c[j - 1] ? t.p[j - 1] : (c[j] ? pos : t.p[j]);
-  }
+  for (int j = 4; j > 0; --j) t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
   t.k[0] = c[0] ? key : t.k[0];
-  t.p[0] = c[0] ? pos : t.p[0];
 }
 
 __device__ __forceinline__ void consider(Top5& t, const float4 c, uint32_t pos, float qx, float qy,
                                          float qz) {
   const float ddx = qx - c.x, ddy = qy - c.y, ddz = qz - c.z;
   const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
-  const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c.w);
-  if (key < t.k[4]) top5_insert(t, key, pos);
+  top5_insert(t, ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)pos);
 }
 
 // butterfly merge of the LPQ per-lane lists of a query group (lanes of a
@@ -314,15 +307,10 @@ __device__ __forceinline__ void group_merge(Top5& t) {
 #pragma unroll
   for (int m = 1; m < LPQ; m <<= 1) {
     uint64_t ok[5];
-    uint32_t op[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      ok[j] = __shfl_xor(t.k[j], m);
-      op[j] = __shfl_xor(t.p[j], m);
-    }
+    for (int j = 0; j < 5; ++j) ok[j] = __shfl_xor(t.k[j], m);
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
-      if (ok[j] < t.k[4]) top5_insert(t, ok[j], op[j]);
+    for (int j = 0; j < 5; ++j) top5_insert(t, ok[j]);
   }
 }
 
@@ -440,17 +428,18 @@ __device__ __forceinline__ void run_range(const GridGeom& g, const RunCtx& rc, i
 // Strided, software-pipelined sweep of a flattened candidate list made of up
 // to 9 contiguous runs (rs = run starts, pre = prefix lengths, T = total): the
 // U loads of step k+1 are issued before step k's candidates are consumed.
+// Flat position tt lies in the last run q with pre[q] <= tt, at map position
+// tt + (rs[q] - pre[q]): one compare and one select per run.
 template <int LPQ, int U>
-__device__ __forceinline__ void flat_addr(const uint32_t (&rs)[9], const uint32_t (&pre)[10],
+__device__ __forceinline__ void flat_addr(const int32_t (&dl)[9], const uint32_t (&pre)[10],
                                           uint32_t T, uint32_t t0, uint32_t (&a)[U]) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t tt = t0 + u * LPQ;
-    uint32_t ad = 0;
+    int32_t d = dl[0];
 #pragma unroll
-    for (int q = 0; q < 9; ++q)
-      if (tt >= pre[q]) ad = rs[q] + (tt - pre[q]);
-    a[u] = ad;
+    for (int q = 1; q < 9; ++q) d = (tt >= pre[q]) ? dl[q] : d;
+    a[u] = tt + (uint32_t)d;
   }
   // slots past the end re-read slot 0's (valid) address: no branch per load
 #pragma unroll
@@ -463,9 +452,12 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
                                           float qx, float qy, float qz, Top5& t) {
   uint32_t t0 = sub;
   if (t0 >= T) return;
+  int32_t dl[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) dl[q] = (int32_t)(rs[q] - pre[q]);
   uint32_t a[U];
   float4 c[U];
-  flat_addr<LPQ, U>(rs, pre, T, t0, a);
+  flat_addr<LPQ, U>(dl, pre, T, t0, a);
 #pragma unroll
   for (int u = 0; u < U; ++u) c[u] = pts[a[u]];
   for (;;) {
@@ -474,13 +466,18 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
     uint32_t an[U];
     float4 cn[U];
     if (more) {
-      flat_addr<LPQ, U>(rs, pre, T, t1, an);
+      flat_addr<LPQ, U>(dl, pre, T, t1, an);
 #pragma unroll
       for (int u = 0; u < U; ++u) cn[u] = pts[an[u]];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (t0 + u * LPQ < T) consider(t, c[u], a[u], qx, qy, qz);
+    for (int u = 0; u < U; ++u) {
+      // past the end: a no-op key instead of a branch
+      const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
+      const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+      const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)a[u];
+      top5_insert(t, (t0 + u * LPQ < T) ? key : kInfKey);
+    }
     if (!more) break;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1178,29 +1175,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     top5_clear(t);
     const bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0 &&
                         !far_outside(g, cfg.far_sq, qx, qy, qz);
-#if defined(SLIO_ABL_IO) || defined(SLIO_ABL_NOCAND)
-    // diagnostic: synthetic neighbours (the first 5 map points), no search
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      t.k[j] = ((uint64_t)__float_as_uint(0.1f * (j + 1)) << 32) | (uint64_t)j;
-      t.p[j] = j;
-    }
-#endif
-#if defined(SLIO_ABL_NOCAND)
-    if (finite) {
-      const int cx = cell_coord(qx, g.ox, g.inv_h);
-      const int cy = cell_coord(qy, g.oy, g.inv_h);
-      const int cz = cell_coord(qz, g.oz, g.inv_h);
-      uint32_t acc = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) {
-        const int yy = min(max(cy - 1 + q % 3, 0), g.dy - 1), zz = min(max(cz - 1 + q / 3, 0), g.dz - 1);
-        const uint32_t rb = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
-        acc += start[rb + min(max(cx - 1, 0), g.dx - 1)] ^ start[rb + min(cx + 2, g.dx)];
-      }
-      t.p[0] += (acc == 0x7fffffffu) ? 1u : 0u;
-    }
-#elif !defined(SLIO_ABL_IO)
     if (finite) {
       const int cx = cell_coord(qx, g.ox, g.inv_h);
       const int cy = cell_coord(qy, g.oy, g.inv_h);
@@ -1277,16 +1251,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         done = covers || (t.k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
       }
     }
-#endif
     // Nearest_Points / pointSearchSqDis for this point
+    // (map indices are written by the fit phase, which loads the points)
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       if (j % LPQ == sub) {
         const uint64_t mk = t.k[j];
-        out.nbr_idx[i * 5 + j] = (mk == kInfKey) ? -1 : (int32_t)(uint32_t)mk;
         out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                  : __uint_as_float((uint32_t)(mk >> 32));
-        nb_pos[slot][j] = t.p[j];
+        nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
       }
     }
     if (sub == 0) {
@@ -1315,22 +1288,22 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       float pd2 = __int_as_float(0x7fc00000);
       const float4 q = qw[slot];
       const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
-      if (sel) {
-        float nb[5][3];
+      // the 5 neighbours: coordinates for the fit, map index for
+      // Nearest_Points (-1 when the map has fewer than 5 points)
+      float nb[5][3];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const float4 c = pts[nb_pos[slot][j]];
-          nb[j][0] = c.x;
-          nb[j][1] = c.y;
-          nb[j][2] = c.z;
-        }
+      for (int j = 0; j < 5; ++j) {
+        const uint32_t ps = nb_pos[slot][j];
+        float4 c = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+        if (ps != 0xFFFFFFFFu) c = pts[ps];
+        nb[j][0] = c.x;
+        nb[j][1] = c.y;
+        nb[j][2] = c.z;
+        out.nbr_idx[i * 5 + j] = (int32_t)__float_as_uint(c.w);
+      }
+      if (sel) {
         float pl[4];
-#ifdef SLIO_ABL_NOFIT
-        pl[0] = nb[0][0]; pl[1] = nb[1][1]; pl[2] = nb[2][2]; pl[3] = nb[3][0] + nb[4][1];
-        sel = true;
-#else
         sel = esti_plane_dev(nb, cfg.plane_thr, pl);
-#endif
         if (sel) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) abcd[j] = pl[j];
@@ -1355,11 +1328,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __syncthreads();
   if (tid == 0) STAMP(2);
   // ---------------- phase 3: fixed-order products
-#ifdef SLIO_ABL_NOPROD
-  if (tid < SLIO_NPROD) out.chunk_part[chunk * SLIO_NPROD + tid] = rows[tid][0];
-#else
   chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
-#endif
   if (tid == 0) STAMP(3);
 }
 
@@ -1681,7 +1650,6 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     set_error("slio pass: reuse pass before any search pass");
     return SLIO_ESTATE;
   }
-  const int64_t C = num_chunks(c.n);
   int64_t c0, c1;
   rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
   // pose: by value (host-driven passes and the first pass of a device-resident
@@ -1701,7 +1669,6 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.extrinsic = extrinsic_est ? 1 : 0;
   cfg.c_begin = c0;
   cfg.c_end = c1;
-  const int per = SLIO_NSUPER / c.prm.nranks;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   PassOut o{c.nbr_idx, c.nbr_sqd, c.plane, c.sel, c.resid, c.chunk_part};
   ScanDev s{c.bx, c.by, c.bz, c.n};
@@ -1795,6 +1762,7 @@ struct slio_ctx {
 
 namespace slio {
 void* internal_stream(slio_handle h) { return h ? (void*)h->c.stream : nullptr; }
+
 }  // namespace slio
 
 #define SLIO_CHECK_H(h)                                  \
@@ -1944,22 +1912,28 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
   }
   GridGeom g;
   float hcell = h->c.prm.grid_cell;
+  // kGridPad empty cells around the map's bounding box: scan points just
+  // outside it (ground returns below a flat map's lowest point, range noise)
+  // still get a query cell inside the grid, so they take the 3x3x3 fast path
+  // instead of the growing-cube fallback
+  constexpr int kGridPad = 2;
   for (;;) {
-    g.ox = mn[0];
-    g.oy = mn[1];
-    g.oz = mn[2];
+    g.ox = mn[0] - kGridPad * hcell;
+    g.oy = mn[1] - kGridPad * hcell;
+    g.oz = mn[2] - kGridPad * hcell;
     g.h = hcell;
     g.inv_h = 1.0f / hcell;
-    g.dx = cell_coord(mx[0], g.ox, g.inv_h) + 1;
-    g.dy = cell_coord(mx[1], g.oy, g.inv_h) + 1;
-    g.dz = cell_coord(mx[2], g.oz, g.inv_h) + 1;
+    g.dx = cell_coord(mx[0], g.ox, g.inv_h) + 1 + kGridPad;
+    g.dy = cell_coord(mx[1], g.oy, g.inv_h) + 1 + kGridPad;
+    g.dz = cell_coord(mx[2], g.oz, g.inv_h) + 1 + kGridPad;
     const int64_t nc = (int64_t)g.dx * g.dy * g.dz;
     if (nc <= h->c.prm.max_grid_cells && nc < (int64_t)0xFFFFFFF0ll) break;
     hcell *= 1.25f;  // grow cells until the dense table fits the budget
   }
-  float mag = 0.0f;
-  for (int a = 0; a < 3; ++a) mag = std::max(mag, std::max(std::fabs(mn[a]), std::fabs(mx[a])));
-  mag = std::max(mag, (float)std::max(g.dx, std::max(g.dy, g.dz)) * g.h);
+  // largest |coordinate| a cell face can have: |origin| + dims * h per axis
+  const float mag = std::max(std::fabs(g.ox) + (float)g.dx * g.h,
+                             std::max(std::fabs(g.oy) + (float)g.dy * g.h,
+                                      std::fabs(g.oz) + (float)g.dz * g.h));
   g.tol = mag * 3.814697265625e-06f + 1.0e-5f;  // 2^-18 relative: >= 64 ulps
   m->g = g;
   m->ncells = (int64_t)g.dx * g.dy * g.dz;

@@ -263,6 +263,19 @@ def make_problem(n_map: int, n_scan: int, seed: int = 20261015, pattern: str = "
     return mp, fr
 
 
+def voxel_order(body: np.ndarray, leaf: float = 0.2) -> np.ndarray:
+    """Permutation putting a scan in pcl::VoxelGrid output order: points sorted
+    by voxel index idx = i + j * div_x + k * div_x * div_y over the cloud's
+    bounding box (x fastest), the order in which laserMapping's
+    downSizeFilterSurf emits feats_down_body (laserMapping.cpp:737-739).  The
+    synthetic Avia scan is voxel-unique at `leaf`, so the order is total."""
+    ijk = np.floor(body.astype(np.float64) / leaf).astype(np.int64)
+    ijk -= ijk.min(axis=0)
+    div = ijk.max(axis=0) + 1
+    idx = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+    return np.argsort(idx, kind="stable")
+
+
 # ---------------------------------------------------------------- C3: Ouster
 OUSTER_FOV_DEG = 16.6  # OS1-64: elevation -16.6 .. +16.6 deg
 

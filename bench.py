@@ -177,6 +177,9 @@ def main():
     ap.add_argument("--map-points", type=int, default=10_000_000)
     ap.add_argument("--scan-points", type=int, default=100_000)
     ap.add_argument("--cell", type=float, default=1.25)
+    ap.add_argument("--scan-order", choices=["voxel", "capture"], default="voxel",
+                    help="voxel: pcl::VoxelGrid output order, as feats_down_body reaches "
+                         "h_share_model in the reference; capture: rosette firing order")
     ap.add_argument("--cpu-scans", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -223,6 +226,8 @@ def main():
     t0 = time.time()
     mp, fr = synth.make_problem(args.map_points, args.scan_points, pattern="avia",
                                 cache_dir=args.cache_dir)
+    if args.scan_order == "voxel":
+        fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
     log(f"[rank {rank}] synthetic problem {mp.shape[0]} map / {fr.body.shape[0]} scan "
         f"in {time.time() - t0:.1f}s")
 

@@ -15,10 +15,12 @@ from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 def main():
     lib = L.load(os.environ.get("SLIO_LIB", L.LIB_PATH))
     lpq = int(os.environ.get("LPQ", "2"))
-    cell = float(os.environ.get("CELL", "1.0"))
+    cell = float(os.environ.get("CELL", "1.25"))
     reps = int(os.environ.get("REPS", "20"))
     mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
     nscan = int(os.environ.get("NSCAN", "100000"))
+    if os.environ.get("ORDER", "voxel") == "voxel":
+        fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
     fr.body = np.ascontiguousarray(fr.body[:nscan])
     st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI])
     pose = L.SlioPose()
@@ -27,7 +29,7 @@ def main():
     p = L.SlioParams()
     lib.slio_params_default(C.byref(p))
     p.grid_cell, p.lanes_per_query = cell, lpq
-    p.search_radius = float(os.environ.get("RADIUS", "1.0"))
+    p.search_radius = float(os.environ.get("RADIUS", "0.0"))
     h = C.c_void_p()
     L.check(lib.slio_create(C.byref(h), C.byref(p)), "create")
     x, y, z = (np.ascontiguousarray(mp[:, k]) for k in range(3))

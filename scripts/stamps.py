@@ -13,7 +13,7 @@ lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
     for nscan in [25000, 100000]:
         mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
-        body = np.ascontiguousarray(fr.body[:nscan])
+        body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)][:nscan])
         st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI])
         pose = L.SlioPose()
         pose.pos[:] = list(st[0:3]); pose.rot[:] = list(st[3:7])
@@ -39,4 +39,7 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         for name, v in (("knn", ph1), ("fit", ph2), ("prod", ph3)):
             print(f"  {name}: mean {v.mean():.2f} p50 {np.median(v):.2f} p90 {np.quantile(v, .9):.2f} max {v.max():.2f} us")
         print(f"  wave kNN end: mean {wv.mean():.2f} max {wv.max():.2f}; per-block max-min wave {np.mean(wv.max(1) - wv.min(1)):.2f} us")
+        tot = us[:, 3] - us[:, 0]
+        print(f"  block total: p10 {np.quantile(tot, .1):.1f} p50 {np.median(tot):.1f} p90 {np.quantile(tot, .9):.1f} max {tot.max():.1f}; "
+              f"end times p50 {np.median(us[:, 3]):.1f} p90 {np.quantile(us[:, 3], .9):.1f}")
         lib.slio_destroy(h)
