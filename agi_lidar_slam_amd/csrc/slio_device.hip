@@ -429,62 +429,93 @@ __device__ __forceinline__ void run_range(const GridGeom& g, const RunCtx& rc, i
 // to 9 contiguous runs (rs = run starts, pre = prefix lengths, T = total): the
 // U loads of step k+1 are issued before step k's candidates are consumed.
 // Flat position tt lies in the last run q with pre[q] <= tt, at map position
-// tt + (rs[q] - pre[q]): one compare and one select per run.
+// tt + (rs[q] - pre[q]): one compare and one select per run.  The run bounds
+// p1..p8 and deltas d0..d8 are plain local scalars of scan_flat (a macro, not
+// an array or struct: from a memory object the compiler turns the select
+// chain into a select of an index plus a load from scratch memory).
+#define SLIO_FLAT_POS(tt, out)   \
+  do {                            \
+    int32_t d_ = d0;              \
+    d_ = (tt) >= p1 ? d1 : d_;    \
+    d_ = (tt) >= p2 ? d2 : d_;    \
+    d_ = (tt) >= p3 ? d3 : d_;    \
+    d_ = (tt) >= p4 ? d4 : d_;    \
+    d_ = (tt) >= p5 ? d5 : d_;    \
+    d_ = (tt) >= p6 ? d6 : d_;    \
+    d_ = (tt) >= p7 ? d7 : d_;    \
+    d_ = (tt) >= p8 ? d8 : d_;    \
+    (out) = (tt) + (uint32_t)d_;  \
+  } while (0)
+
+// U addresses of step t0; slots past the end re-read the list's last
+// candidate (valid: T >= 1), so loads need no branch
+#define SLIO_FLAT_ADDR(t0, a)                                          \
+  do {                                                                 \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                    \
+      const uint32_t tt_ = min((t0) + u * LPQ, T - 1);                 \
+      SLIO_FLAT_POS(tt_, a[u]);                                        \
+    }                                                                  \
+  } while (0)
+
+// distances of U loaded candidates into the lane's list (past the end: a
+// no-op key instead of a branch)
 template <int LPQ, int U>
-__device__ __forceinline__ void flat_addr(const int32_t (&dl)[9], const uint32_t (&pre)[10],
-                                          uint32_t T, uint32_t t0, uint32_t (&a)[U]) {
+__device__ __forceinline__ void consume(Top5& t, const float4 (&c)[U], const uint32_t (&a)[U],
+                                        uint32_t t0, uint32_t T, float qx, float qy, float qz) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const uint32_t tt = t0 + u * LPQ;
-    int32_t d = dl[0];
-#pragma unroll
-    for (int q = 1; q < 9; ++q) d = (tt >= pre[q]) ? dl[q] : d;
-    a[u] = tt + (uint32_t)d;
+    const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
+    const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+    const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)a[u];
+    top5_insert(t, (t0 + u * LPQ < T) ? key : kInfKey);
   }
-  // slots past the end re-read slot 0's (valid) address: no branch per load
-#pragma unroll
-  for (int u = 1; u < U; ++u) a[u] = (t0 + u * LPQ < T) ? a[u] : a[0];
 }
 
+// Two register sets (A, B) alternate, so the loads of step k+1 stay in flight
+// while step k is consumed: no loop-carried copy of loaded registers (a copy
+// makes the compiler wait for the loads at the end of the iteration).  The run
+// deltas are plain scalars (SLIO_FLAT_POS).
 template <int LPQ, int U>
 __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const uint32_t (&rs)[9],
                                           const uint32_t (&pre)[10], uint32_t T, int sub,
                                           float qx, float qy, float qz, Top5& t) {
   uint32_t t0 = sub;
   if (t0 >= T) return;
-  int32_t dl[9];
+  const uint32_t p1 = pre[1], p2 = pre[2], p3 = pre[3], p4 = pre[4], p5 = pre[5], p6 = pre[6],
+                 p7 = pre[7], p8 = pre[8];
+  const int32_t d0 = (int32_t)(rs[0] - pre[0]), d1 = (int32_t)(rs[1] - pre[1]),
+                d2 = (int32_t)(rs[2] - pre[2]), d3 = (int32_t)(rs[3] - pre[3]),
+                d4 = (int32_t)(rs[4] - pre[4]), d5 = (int32_t)(rs[5] - pre[5]),
+                d6 = (int32_t)(rs[6] - pre[6]), d7 = (int32_t)(rs[7] - pre[7]),
+                d8 = (int32_t)(rs[8] - pre[8]);
+  constexpr uint32_t kStep = U * LPQ;
+  uint32_t aA[U], aB[U];
+  float4 cA[U], cB[U];
+  SLIO_FLAT_ADDR(t0, aA);
 #pragma unroll
-  for (int q = 0; q < 9; ++q) dl[q] = (int32_t)(rs[q] - pre[q]);
-  uint32_t a[U];
-  float4 c[U];
-  flat_addr<LPQ, U>(dl, pre, T, t0, a);
-#pragma unroll
-  for (int u = 0; u < U; ++u) c[u] = pts[a[u]];
+  for (int u = 0; u < U; ++u) cA[u] = pts[aA[u]];
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   for (;;) {
-    const uint32_t t1 = t0 + U * LPQ;
-    const bool more = t1 < T;
-    uint32_t an[U];
-    float4 cn[U];
-    if (more) {
-      flat_addr<LPQ, U>(dl, pre, T, t1, an);
+    // set B is consumed even when it lies wholly past the end (its keys are
+    // then no-ops): a loop exit between its loads and their use would let the
+    // compiler sink the loads down to the use
+    const uint32_t t1 = t0 + kStep, t2 = t1 + kStep;
+    SLIO_FLAT_ADDR(t1, aB);
 #pragma unroll
-      for (int u = 0; u < U; ++u) cn[u] = pts[an[u]];
-    }
+    for (int u = 0; u < U; ++u) cB[u] = pts[aB[u]];
+    // keep the loads here: not merged with the other set's, not sunk to their use
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    consume<LPQ, U>(t, cA, aA, t0, T, qx, qy, qz);
+    SLIO_FLAT_ADDR(t2, aA);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      // past the end: a no-op key instead of a branch
-      const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
-      const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
-      const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)a[u];
-      top5_insert(t, (t0 + u * LPQ < T) ? key : kInfKey);
-    }
-    if (!more) break;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      a[u] = an[u];
-      c[u] = cn[u];
-    }
-    t0 = t1;
+    for (int u = 0; u < U; ++u) cA[u] = pts[aA[u]];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    consume<LPQ, U>(t, cB, aB, t1, T, qx, qy, qz);
+    if (t2 >= T) break;
+    t0 = t2;
   }
 }
 
