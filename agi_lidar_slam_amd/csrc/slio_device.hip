@@ -61,19 +61,37 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 constexpr int kBlock = 256;                      // threads per search workgroup
 constexpr int kDefaultLPQ = 2;                   // lanes per query (tuned on MI355X)
+#ifndef SLIO_SEARCH_U
+#define SLIO_SEARCH_U 2                          // candidate loads in flight per lane and step (A/B on MI355X: 2 < 4 < 6 < 8)
+#endif
 constexpr uint64_t kInfKey = ~0ull;
 
 #ifdef SLIO_ABL_STAMP
 // diagnostic build only: per-block phase timestamps (s_memrealtime, 100 MHz)
 __device__ unsigned long long g_stamps[8192][8];
-#define STAMP(slot)                                                                \
+__device__ uint32_t g_hwid[8192][2];  // HW_ID (cu, simd, se) and XCC_ID of wave 0
+__device__ unsigned long long g_wstamps[8192][4][4];  // per wave: refine start/end, fallback end, rounds
+#define WSTAMP(k, v)                                                               \
   do {                                                                             \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192)                              \
+      g_wstamps[blockIdx.x][threadIdx.x >> 6][k] = (v);                            \
+  } while (0)
+#define STAMP(slot)                                                                \
+  do {                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) {                            \
       g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();               \
+      if ((slot) == 0 && threadIdx.x == 0) {                                       \
+        g_hwid[blockIdx.x][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);         \
+        g_hwid[blockIdx.x][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);        \
+      }                                                                            \
+    }                                                                              \
   } while (0)
 #else
 #define STAMP(slot) \
   do {              \
+  } while (0)
+#define WSTAMP(k, v) \
+  do {               \
   } while (0)
 #endif
 
@@ -1195,26 +1213,32 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (tid == 0) STAMP(0);
 
   // ---------------- phase 1: exact 5-NN
+  // (no early exit per lane: the refinement below needs the whole wavefront)
   for (int pass = 0; pass < PASSES; ++pass) {
     const int slot = pass * QPP + grp;
     const int64_t i = chunk * SLIO_CHUNK + slot;
-    if (i >= scan.n) continue;
-    const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
-    float qx, qy, qz;
-    body_to_world(pose, bx, by, bz, qx, qy, qz);
+    const bool live = i < scan.n;
+    float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+    if (live) {
+      const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
+      body_to_world(pose, bx, by, bz, qx, qy, qz);
+    }
     Top5 t;
     top5_clear(t);
-    const bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0 &&
+    const bool finite = live && isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0 &&
                         !far_outside(g, cfg.far_sq, qx, qy, qz);
+    int cx = 0, cy = 0, cz = 0, r = 1;
+    bool done = !finite;
+    bool refine = false;   // exact 5x5x5 refinement wanted (lim = refine bound)
+    float lim = 0.0f;
     if (finite) {
-      const int cx = cell_coord(qx, g.ox, g.inv_h);
-      const int cy = cell_coord(qy, g.oy, g.inv_h);
-      const int cz = cell_coord(qz, g.oz, g.inv_h);
+      cx = cell_coord(qx, g.ox, g.inv_h);
+      cy = cell_coord(qy, g.oy, g.inv_h);
+      cz = cell_coord(qz, g.oz, g.inv_h);
       const int ex = max(max(-cx, cx - (g.dx - 1)), 0);
       const int ey = max(max(-cy, cy - (g.dy - 1)), 0);
       const int ez = max(max(-cz, cz - (g.dz - 1)), 0);
-      int r = max(1, max(ex, max(ey, ez)));
-      bool done = false;
+      r = max(1, max(ex, max(ey, ez)));
       if (r == 1 && !SPHERE) {
         // (1) the 3x3x3 block around the query cell: 9 runs, one batch
         RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
@@ -1225,20 +1249,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
         done = covers || (t.k[4] != kInfKey && b1 > 0.0f && d5 < (b1 * b1) * 0.99999f);
         if (!done && t.k[4] != kInfKey) {
-          // (2) exact refinement: every cell of the 5x5x5 cube whose
+          // (2) exact refinement (below): every cell of the 5x5x5 cube whose
           // conservative box gap is within the current 5th distance, minus
           // the block already scanned (valid while that sphere stays inside
           // the 5x5x5 cube; otherwise the general fallback takes over)
           bool covers2;
           const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, covers2);
           if (covers2 || (b2 > 0.0f && d5 < (b2 * b2) * 0.99999f)) {
-            rc.mode = 2;
-            rc.lim = d5 * 1.00001f;
-            if (sub != 0) top5_clear(t);  // lane 0 keeps the merged list
-            const uint64_t rows = sphere_rows(g, rc, rc.lim);
-            scan_runs<LPQ, U>(pts, start, g, rc, rows | ((rows & 0x739c0ull) << 32), sub, t);
-            group_merge<LPQ>(t);
-            done = true;
+            refine = true;
+            lim = d5 * 1.00001f;
           }
         }
         r = 2;
@@ -1271,22 +1290,75 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         }
         r = 2;
       }
-      // (3) general fallback: full cubes r, r+1, ... rescanned from scratch
-      for (; !done; ++r) {
-        top5_clear(t);
-        scan_cube<LPQ, U>(pts, start, g, cx, cy, cz, r, sub, qx, qy, qz, t);
-        group_merge<LPQ>(t);
-        bool covers;
-        const float b = outside_bound(g, cx, cy, cz, r, qx, qy, qz, covers);
-        const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
-        done = covers || (t.k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
-      }
     }
+    if (!SPHERE) {
+      // (2) the refinements of this wavefront, re-grouped: up to 8 queries
+      // per round, kRefLanes lanes each, every lane with its own share of the
+      // region's runs (the 2 lanes of a query group alone went through up to
+      // 6 batches of run bounds and ~60 dependent candidate steps, holding the
+      // wavefront that long); the owner merges the region's top 5 into its list
+      constexpr int kRefLanes = 8;
+      const int lane = tid & 63;
+      const int rslot = lane / kRefLanes, rsub = lane % kRefLanes;
+      uint64_t need = __ballot(refine && sub == 0);
+      WSTAMP(0, __builtin_amdgcn_s_memrealtime());
+      WSTAMP(3, __popcll(need));
+      while (need) {
+        const uint64_t round = need;
+        int src = -1;
+        uint64_t m = need;
+#pragma unroll
+        for (int k = 0; k < 64 / kRefLanes; ++k) {
+          if (m) {
+            if (k == rslot) src = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+          }
+        }
+        need = m;
+        const int sl = max(src, 0);
+        const RunCtx rq{__shfl(cx, sl, 64), __shfl(cy, sl, 64), __shfl(cz, sl, 64),
+                        __shfl(qx, sl, 64), __shfl(qy, sl, 64), __shfl(qz, sl, 64), 2, 0.0f,
+                        __shfl(lim, sl, 64)};
+        Top5 tr;
+        top5_clear(tr);
+        if (src >= 0) {
+          const uint64_t rows = sphere_rows(g, rq, rq.lim);
+          // lane rsub of the slot takes runs rsub, rsub + 8, ... of the region:
+          // at most 8 runs, so ONE batch (one round trip for all run bounds)
+          const uint64_t runs = rows | ((rows & 0x739c0ull) << 32);
+          scan_runs<1, U>(pts, start, g, rq, runs & (0x0101010101010101ull << rsub), 0, tr);
+        }
+        group_merge<kRefLanes>(tr);
+        // owner group of a query refined this round: its slot is its rank
+        const int own = lane & ~(LPQ - 1);
+        const bool mine = refine && ((round >> own) & 1ull) && ((m >> own) & 1ull) == 0;
+        const int rank = __popcll(round & ((1ull << own) - 1ull));
+        const int from = min(rank, 64 / kRefLanes - 1) * kRefLanes;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const uint64_t k = __shfl(tr.k[j], from, 64);
+          if (mine) top5_insert(t, k);
+        }
+        if (mine) done = true;
+      }
+      WSTAMP(1, __builtin_amdgcn_s_memrealtime());
+    }
+    // (3) general fallback: full cubes r, r+1, ... rescanned from scratch
+    for (; !done; ++r) {
+      top5_clear(t);
+      scan_cube<LPQ, U>(pts, start, g, cx, cy, cz, r, sub, qx, qy, qz, t);
+      group_merge<LPQ>(t);
+      bool covers;
+      const float b = outside_bound(g, cx, cy, cz, r, qx, qy, qz, covers);
+      const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+      done = covers || (t.k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
+    }
+    WSTAMP(2, __builtin_amdgcn_s_memrealtime());
     // Nearest_Points / pointSearchSqDis for this point
     // (map indices are written by the fit phase, which loads the points)
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      if (j % LPQ == sub) {
+      if (j % LPQ == sub && live) {
         const uint64_t mk = t.k[j];
         out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                  : __uint_as_float((uint32_t)(mk >> 32));
@@ -1724,7 +1796,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     const bool sph = cfg.radius_sq > 0.0f;
     const dim3 nb((unsigned)nblk);
 #define SLIO_LAUNCH(L, SPH, DEV)                                                                   \
-  hipExtLaunchKernelGGL(k_search_pass<L, 4, SPH, DEV>, nb, dim3(search_block<L>()), 0, c.stream, \
+  hipExtLaunchKernelGGL(k_search_pass<L, SLIO_SEARCH_U, SPH, DEV>, nb, dim3(search_block<L>()), 0, c.stream, \
                         ev.first, ev.second, 0, mv, s, P, cfg, o)
 #define SLIO_LAUNCH2(L, SPH) \
   do {                        \
@@ -1811,6 +1883,17 @@ extern "C" {
 int slio_debug_stamps(unsigned long long* out, int nblocks) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * nblocks) ==
                  hipSuccess
+             ? 0
+             : -3;
+}
+int slio_debug_wstamps(unsigned long long* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(unsigned long long) * 16 * nblocks) ==
+                 hipSuccess
+             ? 0
+             : -3;
+}
+int slio_debug_hwid(uint32_t* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hwid), sizeof(uint32_t) * 2 * nblocks) == hipSuccess
              ? 0
              : -3;
 }

@@ -1,0 +1,10 @@
+# diagnostic / ablation builds into agi_lidar_slam_amd/_abl: bash scripts/build_abl.sh NAME "-DFLAG ..." [NAME "FLAGS"]...
+cd "$(dirname "$0")/.."
+mkdir -p agi_lidar_slam_amd/_abl
+S=agi_lidar_slam_amd/csrc
+while [ $# -ge 2 ]; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math $2 -I include \
+    $S/slio_device.hip $S/slio_ikf.cpp $S/slio_lio.hip -o agi_lidar_slam_amd/_abl/libslio_$1.so &
+  shift 2
+done
+wait

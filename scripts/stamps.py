@@ -31,6 +31,16 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         buf = (C.c_ulonglong * (8 * nb))()
         assert lib.slio_debug_stamps(buf, nb) == 0
         a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
+        hw = (C.c_uint32 * (2 * nb))()
+        lib.slio_debug_hwid.argtypes = [C.POINTER(C.c_uint32), C.c_int]
+        assert lib.slio_debug_hwid(hw, nb) == 0
+        ws = (C.c_ulonglong * (16 * nb))()
+        lib.slio_debug_wstamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+        assert lib.slio_debug_wstamps(ws, nb) == 0
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez(f"gpurun_out/stamps_{lpq}_{nscan}.npz", stamps=a,
+                 hwid=np.frombuffer(hw, dtype=np.uint32).reshape(nb, 2),
+                 wstamps=np.frombuffer(ws, dtype=np.uint64).reshape(nb, 4, 4))
         t0 = a[:, 0].min()
         us = (a - t0) / 100.0   # 100 MHz -> us
         ph1 = us[:, 1] - us[:, 0]; ph2 = us[:, 2] - us[:, 1]; ph3 = us[:, 3] - us[:, 2]
