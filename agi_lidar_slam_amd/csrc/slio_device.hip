@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
@@ -112,10 +113,19 @@ struct MapDev {
   int64_t ncells = 0;
   float4* pts = nullptr;          // sorted by cell: x, y, z, bits(map index)
   uint32_t* start = nullptr;      // ncells + 1 prefix offsets
+  // block rows (optional, ~9x the points): entry (x, y, z) holds the points
+  // of the 9 cells (x, y + j, z + k), j, k in {-1, 0, 1}, with .w = their
+  // position in pts; entries are laid out in cell order, so the 3x3x3 block
+  // around a cell is ONE contiguous range [bstart[c - 1], bstart[c + 2])
+  float4* blk = nullptr;
+  uint32_t* bstart = nullptr;     // ncells + 1 prefix offsets into blk
+  int64_t nblk = 0;
   int device = 0;
   ~MapDev() {
     if (pts) (void)hipFree(pts);
     if (start) (void)hipFree(start);
+    if (blk) (void)hipFree(blk);
+    if (bstart) (void)hipFree(bstart);
   }
 };
 
@@ -125,7 +135,28 @@ struct MapView {
   int64_t n;
   const float4* pts;
   const uint32_t* start;
+  const float4* blk;       // null: the 3x3x3 block is scanned as 9 runs of pts
+  const uint32_t* bstart;
+  int64_t nblk;
+  int64_t ncells;
 };
+
+#ifdef SLIO_BOUNDS_CHECK
+__constant__ int64_t c_dbg_npts, c_dbg_ncells;  // set by slio_map_upload
+// diagnostic build only: report and neutralise an out-of-range index
+#define SLIO_BCHK(idx, lim, what)                                                       \
+  do {                                                                                  \
+    if ((int64_t)(idx) < 0 || (int64_t)(idx) >= (int64_t)(lim)) {                       \
+      printf("slio bounds: %s idx %lld lim %lld block %d thread %d\n", what,             \
+             (long long)(idx), (long long)(lim), (int)blockIdx.x, (int)threadIdx.x);     \
+      idx = 0;                                                                          \
+    }                                                                                   \
+  } while (0)
+#else
+#define SLIO_BCHK(idx, lim, what) \
+  do {                            \
+  } while (0)
+#endif
 
 __device__ __host__ __forceinline__ int cell_coord(float p, float o, float inv_h) {
   float t = floorf((p - o) * inv_h);
@@ -159,6 +190,47 @@ __global__ void k_gather_sorted(const float* __restrict__ x, const float* __rest
   if (i >= n) return;
   uint32_t o = order[i];
   pts[i] = make_float4(x[o], y[o], z[o], __uint_as_float(o));
+}
+
+// block rows: entry sizes, then the fill (one thread per cell; the 9 source
+// cells in (z, y) order, each cell's points in pts order)
+__global__ void k_blk_count(const uint32_t* __restrict__ start, GridGeom g, int64_t ncells,
+                            uint32_t* __restrict__ cnt9) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncells) return;
+  const int x = (int)(c % g.dx);
+  const int y = (int)((c / g.dx) % g.dy);
+  const int z = (int)(c / ((int64_t)g.dx * g.dy));
+  uint32_t s = 0;
+  for (int k = -1; k <= 1; ++k)
+    for (int j = -1; j <= 1; ++j) {
+      const int yy = y + j, zz = z + k;
+      if (yy < 0 || yy >= g.dy || zz < 0 || zz >= g.dz) continue;
+      const int64_t sc = ((int64_t)zz * g.dy + yy) * g.dx + x;
+      s += start[sc + 1] - start[sc];
+    }
+  cnt9[c] = s;
+}
+
+__global__ void k_blk_fill(const float4* __restrict__ pts, const uint32_t* __restrict__ start,
+                           const uint32_t* __restrict__ bstart, GridGeom g, int64_t ncells,
+                           float4* __restrict__ blk) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncells) return;
+  const int x = (int)(c % g.dx);
+  const int y = (int)((c / g.dx) % g.dy);
+  const int z = (int)(c / ((int64_t)g.dx * g.dy));
+  uint32_t o = bstart[c];
+  for (int k = -1; k <= 1; ++k)
+    for (int j = -1; j <= 1; ++j) {
+      const int yy = y + j, zz = z + k;
+      if (yy < 0 || yy >= g.dy || zz < 0 || zz >= g.dz) continue;
+      const int64_t sc = ((int64_t)zz * g.dy + yy) * g.dx + x;
+      for (uint32_t p = start[sc]; p < start[sc + 1]; ++p) {
+        const float4 v = pts[p];
+        blk[o++] = make_float4(v.x, v.y, v.z, __uint_as_float(p));
+      }
+    }
 }
 
 // ---------------------------------------------------------------- math helpers
@@ -510,6 +582,9 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
   uint32_t aA[U], aB[U];
   float4 cA[U], cB[U];
   SLIO_FLAT_ADDR(t0, aA);
+#ifdef SLIO_BOUNDS_CHECK
+  for (int u = 0; u < U; ++u) SLIO_BCHK(aA[u], c_dbg_npts, "flat0");
+#endif
 #pragma unroll
   for (int u = 0; u < U; ++u) cA[u] = pts[aA[u]];
   asm volatile("" ::: "memory");
@@ -520,6 +595,9 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
     // compiler sink the loads down to the use
     const uint32_t t1 = t0 + kStep, t2 = t1 + kStep;
     SLIO_FLAT_ADDR(t1, aB);
+#ifdef SLIO_BOUNDS_CHECK
+    for (int u = 0; u < U; ++u) SLIO_BCHK(aB[u], c_dbg_npts, "flatB");
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) cB[u] = pts[aB[u]];
     // keep the loads here: not merged with the other set's, not sunk to their use
@@ -527,11 +605,55 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
     __builtin_amdgcn_sched_barrier(0);
     consume<LPQ, U>(t, cA, aA, t0, T, qx, qy, qz);
     SLIO_FLAT_ADDR(t2, aA);
+#ifdef SLIO_BOUNDS_CHECK
+    for (int u = 0; u < U; ++u) SLIO_BCHK(aA[u], c_dbg_npts, "flatA");
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) cA[u] = pts[aA[u]];
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     consume<LPQ, U>(t, cB, aB, t1, T, qx, qy, qz);
+    if (t2 >= T) break;
+    t0 = t2;
+  }
+}
+
+// The 3x3x3 block from the block rows: one contiguous range, so a flat
+// position is an address (no run lookup); keys carry the pts position (.w),
+// identical to the keys of the 9-run scan.  Same pipeline as scan_flat.
+template <int LPQ, int U>
+__device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, uint32_t s,
+                                                uint32_t T, int sub, float qx, float qy, float qz,
+                                                Top5& t) {
+  uint32_t t0 = sub;
+  if (t0 >= T) return;
+  constexpr uint32_t kStep = U * LPQ;
+  float4 cA[U], cB[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) cA[u] = blk[s + min(t0 + u * LPQ, T - 1)];
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  auto eat = [&](const float4 (&c)[U], uint32_t tb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
+      const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+      const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c[u].w);
+      top5_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
+    }
+  };
+  for (;;) {
+    const uint32_t t1 = t0 + kStep, t2 = t1 + kStep;
+#pragma unroll
+    for (int u = 0; u < U; ++u) cB[u] = blk[s + min(t1 + u * LPQ, T - 1)];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    eat(cA, t0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) cA[u] = blk[s + min(t2 + u * LPQ, T - 1)];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    eat(cB, t1);
     if (t2 >= T) break;
     t0 = t2;
   }
@@ -556,6 +678,11 @@ __device__ __forceinline__ void scan_runs(const float4* __restrict__ pts, const 
         run_range(g, rc, bit, yy, zz, xa, xb);
         if (xa <= xb) {
           const uint32_t rb = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
+#ifdef SLIO_BOUNDS_CHECK
+          uint32_t j0 = rb + xa, j1 = rb + xb + 1;
+          SLIO_BCHK(j0, c_dbg_ncells + 1, "runs0");
+          SLIO_BCHK(j1, c_dbg_ncells + 1, "runs1");
+#endif
           s = start[rb + xa];
           e = start[rb + xb + 1];
         }
@@ -610,6 +737,9 @@ __device__ __forceinline__ void scan_cube(const float4* __restrict__ pts, const 
 #pragma unroll
       for (int u = 1; u < U; ++u) a[u] = (t0 + u * LPQ < T) ? a[u] : a[0];
       float4 c[U];
+#ifdef SLIO_BOUNDS_CHECK
+      for (int u = 0; u < U; ++u) SLIO_BCHK(a[u], c_dbg_npts, "cube");
+#endif
 #pragma unroll
       for (int u = 0; u < U; ++u) c[u] = pts[a[u]];
 #pragma unroll
@@ -1241,8 +1371,24 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       r = max(1, max(ex, max(ey, ez)));
       if (r == 1 && !SPHERE) {
         // (1) the 3x3x3 block around the query cell: 9 runs, one batch
-        RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
-        scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
+        // (r == 1 also covers query cells one step outside the grid: the
+        // block rows exist only for cells inside it)
+        if (map.blk && (ex | ey | ez) == 0) {
+          const uint32_t rb = ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx;
+          uint32_t i0 = rb + max(cx - 1, 0), i1 = rb + min(cx + 1, g.dx - 1) + 1;
+          SLIO_BCHK(i0, map.ncells + 1, "bstart0");
+          SLIO_BCHK(i1, map.ncells + 1, "bstart1");
+          const uint32_t b0 = map.bstart[i0];
+          const uint32_t b1 = map.bstart[i1];
+#ifdef SLIO_BOUNDS_CHECK
+          if (b1 < b0 || (int64_t)b1 > map.nblk)
+            printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
+#endif
+          scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+        } else {
+          RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
+          scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
+        }
         group_merge<LPQ>(t);
         bool covers;
         const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
@@ -1398,6 +1544,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       for (int j = 0; j < 5; ++j) {
         const uint32_t ps = nb_pos[slot][j];
         float4 c = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+#ifdef SLIO_BOUNDS_CHECK
+        if (ps != 0xFFFFFFFFu && ps >= map.n) {
+          printf("slio bounds: nb_pos %u n %lld block %d slot %d j %d\n", ps, (long long)map.n,
+                 (int)blockIdx.x, slot, j);
+          continue;
+        }
+#endif
         if (ps != 0xFFFFFFFFu) c = pts[ps];
         nb[j][0] = c.x;
         nb[j][1] = c.y;
@@ -1792,7 +1945,8 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   };
   if (nblk > 0 && run_search) {
     const auto ev = timing(SLIO_KERNEL_SEARCH);
-    const MapView mv{c.map->g, c.map->n, c.map->pts, c.map->start};
+    const MapView mv{c.map->g,     c.map->n,      c.map->pts,  c.map->start,
+                     c.map->blk,   c.map->bstart, c.map->nblk, c.map->ncells};
     const bool sph = cfg.radius_sq > 0.0f;
     const dim3 nb((unsigned)nblk);
 #define SLIO_LAUNCH(L, SPH, DEV)                                                                   \
@@ -2121,6 +2275,41 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
       fail("build kernels", e);
       break;
     }
+    // block rows (speed only): skipped when disabled, when their positions
+    // would overflow 32 bits or when the device memory is not there
+    const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
+    if ((nb9 && nb9[0] && nb9[0] != '0') || 9 * n >= (int64_t)0xFFFFFFF0ll) break;
+    const int ncb = (int)((m->ncells + 255) / 256);
+    if ((e = hipMalloc(&m->bstart, sizeof(uint32_t) * (m->ncells + 1)))) {
+      (void)hipGetLastError();
+      m->bstart = nullptr;
+      break;
+    }
+    k_blk_count<<<ncb, 256, 0, st>>>(m->start, g, m->ncells, cnt);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, m->bstart, (int)(m->ncells + 1), st))) {
+      fail("block-row scan", e);
+      break;
+    }
+    uint32_t total = 0;  // <= 9 n < 2^32 (checked above): the scan cannot wrap
+    if ((e = hipMemcpyAsync(&total, m->bstart + m->ncells, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            st)) ||
+        (e = hipStreamSynchronize(st))) {
+      fail("block-row total", e);
+      break;
+    }
+    if (hipMalloc(&m->blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
+      (void)hipGetLastError();
+      m->blk = nullptr;
+      (void)hipFree(m->bstart);
+      m->bstart = nullptr;
+      break;
+    }
+    m->nblk = (int64_t)total;
+    k_blk_fill<<<ncb, 256, 0, st>>>(m->pts, m->start, m->bstart, g, m->ncells, m->blk);
+    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+      fail("block-row kernels", e);
+      break;
+    }
   } while (0);
   (void)hipFree(dx_);
   (void)hipFree(dy_);
@@ -2132,6 +2321,13 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
   (void)hipFree(cnt);
   (void)hipFree(tmp);
   if (rc) return rc;
+#ifdef SLIO_BOUNDS_CHECK
+  {
+    const int64_t nc = m->ncells;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_npts), &n, sizeof(n));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_ncells), &nc, sizeof(nc));
+  }
+#endif
   h->c.map = m;
   h->c.searched = false;
   return SLIO_OK;

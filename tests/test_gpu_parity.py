@@ -150,6 +150,28 @@ def test_knn_grid_geometry_invariant(L, oracle_mod, c1, cell, max_cells, radius,
         L.load().slio_destroy(h)
 
 
+@pytest.mark.parametrize("cell,lpq", [(0.75, 0), (1.25, 0), (1.25, 1), (1.0, 4)])
+def test_knn_nine_run_path(L, oracle_mod, c1, monkeypatch, cell, lpq):
+    """Without the block rows (SLIO_NO_BLOCK_ROWS, or a map too large for
+    them) the 3x3x3 block is scanned as 9 runs of the cell-sorted map: the
+    same candidates and keys, so the same bit-exact result."""
+    monkeypatch.setenv("SLIO_NO_BLOCK_ROWS", "1")
+    mp, fr, T = c1["avia"]
+    st = state_of(fr)
+    q = oracle_mod.body_to_world(st, fr.body)
+    ridx, rsqd = T.knn(q, 5)
+    h = mk(L, cell=cell, lpq=lpq)
+    try:
+        upload_map(L, h, mp)
+        upload_scan(L, h, fr.body)
+        iterate(L, h, st, True)
+        idx, sqd, *_ = results(L, h, q.shape[0])
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_array_equal(sqd, rsqd)
+    finally:
+        L.load().slio_destroy(h)
+
+
 # ------------------------------------------------------------------ repeated search
 @pytest.mark.parametrize("shift", [[0.03, -0.02, 0.01], [0.3, 0.2, -0.1], [2.0, -1.5, 0.4]])
 def test_repeated_search_bitexact(L, oracle_mod, c1, shift):
