@@ -71,7 +71,8 @@ struct IkfCtl {
   int32_t converge, t, done, search_now;
   int32_t passes, searches, valid_passes, mode;
   int64_t last_m;
-  int32_t singular, pad;
+  int32_t singular;
+  int32_t published;  // mapped host block: set (release, system scope) after x, P and the flags
   double LM[300];    // Cholesky factor of S = P11i + H^T H / R, H^T H / R and
                      // 1 / diag of the factor, of the last valid pass (device only)
 };

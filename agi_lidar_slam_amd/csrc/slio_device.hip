@@ -19,6 +19,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -1152,6 +1153,7 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
       hblk->singular = 1;
       hblk->done = 1;
       __threadfence_system();
+      __hip_atomic_store(&hblk->published, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return;
   }
@@ -1240,7 +1242,10 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
       hblk->last_m = m;
       hblk->singular = 0;
     }
+    // every thread's stores, then one release store the host polls for
     __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(&hblk->published, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   SSTAMP(8);
 }
@@ -1879,6 +1884,32 @@ static hipError_t wait_stream(Ctx& c) {
   return e;
 }
 
+// Wait for the device-resident update to publish its result in the mapped
+// host block (one release store after x, P and the flags), which the host
+// sees ~1 us after it happens; the stream's completion event is polled now
+// and then so that a failed launch (no publication) still ends the wait.
+// Kernels of the update still queued behind the publication exit at once
+// (ctl->done) and touch neither the mapped block nor the caller's buffers.
+static hipError_t wait_published(Ctx& c) {
+  hipError_t e;
+  if (!c.done_ev && (e = hipEventCreateWithFlags(&c.done_ev, hipEventDisableTiming))) return e;
+  if ((e = hipEventRecord(c.done_ev, c.stream))) return e;
+  volatile int32_t* pub = &c.h_ctl->published;
+  for (uint32_t it = 1;; ++it) {
+    if (*pub) break;
+    if ((it & 255) == 0) {
+      e = hipEventQuery(c.done_ev);
+      if (e != hipErrorNotReady) {
+        if (e != hipSuccess) return e;
+        break;  // all work done: the flags tell whether it published
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return hipSuccess;
+}
+
 // Fused filter step of a single-rank device-resident update.
 struct SolveArgs {
   int on;        // run the filter step in the super-sum kernel (single rank)
@@ -2447,6 +2478,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   hc.mode = mode;
   hc.last_m = 0;
   hc.singular = 0;
+  hc.published = 0;
   for (int k = 0; k < 24; ++k) hc.dxn[k] = 0.0;  // x == x_propagated on pass 0
   // The control block comes in and goes out through the mapped host block:
   // pass 0 takes its pose by value and its filter step reads the block over
@@ -2493,7 +2525,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     }
   }
   SLIO_HIP(hipGetLastError());
-  SLIO_HIP(wait_stream(c));
+  SLIO_HIP(wait_published(c));
   if (!c.h_ctl->done) {
     set_error("slio_ikf_update_device: the update did not complete");
     return SLIO_EDEVICE;
