@@ -391,12 +391,36 @@ __device__ __forceinline__ void consider(Top5& t, const float4 c, uint32_t pos, 
   top5_insert(t, ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)pos);
 }
 
+// 64-bit lane exchange by DPP (a VALU operand modifier, no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo;
+}
+
+template <int CTRL>
+__device__ __forceinline__ void merge_round_dpp(Top5& t) {
+  uint64_t ok[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) ok[j] = dpp64<CTRL>(t.k[j]);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) top5_insert(t, ok[j]);
+}
+
 // butterfly merge of the LPQ per-lane lists of a query group (lanes of a
-// group are consecutive and aligned, so xor partners stay in the group)
+// group are consecutive and aligned, and all active or all inactive).  Up to
+// 16 lanes by DPP: quad_perm [1,0,3,2] and [2,3,0,1] merge each quad, then
+// row_half_mirror (lane i <-> 7 - i) pairs the two quads of 8 lanes and
+// row_mirror (i <-> 15 - i) the two halves of 16; wider groups by ds_bpermute.
 template <int LPQ>
 __device__ __forceinline__ void group_merge(Top5& t) {
+  if (LPQ >= 2) merge_round_dpp<0xB1>(t);
+  if (LPQ >= 4) merge_round_dpp<0x4E>(t);
+  if (LPQ >= 8) merge_round_dpp<0x141>(t);
+  if (LPQ >= 16) merge_round_dpp<0x140>(t);
 #pragma unroll
-  for (int m = 1; m < LPQ; m <<= 1) {
+  for (int m = 16; m < LPQ; m <<= 1) {
     uint64_t ok[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) ok[j] = __shfl_xor(t.k[j], m);
@@ -1453,7 +1477,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       const int rslot = lane / kRefLanes, rsub = lane % kRefLanes;
       uint64_t need = __ballot(refine && sub == 0);
       WSTAMP(0, __builtin_amdgcn_s_memrealtime());
+#ifndef SLIO_REFINE_STAMP
       WSTAMP(3, __popcll(need));
+#endif
       while (need) {
         const uint64_t round = need;
         int src = -1;
@@ -1472,6 +1498,10 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
                         __shfl(lim, sl, 64)};
         Top5 tr;
         top5_clear(tr);
+#ifdef SLIO_REFINE_STAMP
+        const bool first_round = round == __ballot(refine && sub == 0);
+        if (first_round) WSTAMP(2, __builtin_amdgcn_s_memrealtime());
+#endif
         if (src >= 0) {
           const uint64_t rows = sphere_rows(g, rq, rq.lim);
           // lane rsub of the slot takes runs rsub, rsub + 8, ... of the region:
@@ -1479,6 +1509,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           const uint64_t runs = rows | ((rows & 0x739c0ull) << 32);
           scan_runs<1, U>(pts, start, g, rq, runs & (0x0101010101010101ull << rsub), 0, tr);
         }
+#ifdef SLIO_REFINE_STAMP
+        if (first_round) WSTAMP(3, __builtin_amdgcn_s_memrealtime());
+#endif
         group_merge<kRefLanes>(tr);
         // owner group of a query refined this round: its slot is its rank
         const int own = lane & ~(LPQ - 1);
@@ -1504,7 +1537,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
       done = covers || (t.k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
     }
+#ifndef SLIO_REFINE_STAMP
     WSTAMP(2, __builtin_amdgcn_s_memrealtime());
+#endif
     // Nearest_Points / pointSearchSqDis for this point
     // (map indices are written by the fit phase, which loads the points)
 #pragma unroll
