@@ -64,7 +64,7 @@ void set_error(const std::string& msg) { g_err = msg; }
 constexpr int kBlock = 256;                      // threads per search workgroup
 constexpr int kDefaultLPQ = 2;                   // lanes per query (tuned on MI355X)
 #ifndef SLIO_SEARCH_U
-#define SLIO_SEARCH_U 2                          // candidate loads in flight per lane and step (A/B on MI355X: 2 < 4 < 6 < 8)
+#define SLIO_SEARCH_U 3                          // candidate loads in flight per lane and step (A/B on MI355X, block rows: 3 < 4 < 2)
 #endif
 constexpr uint64_t kInfKey = ~0ull;
 
