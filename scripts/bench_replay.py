@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""C5 batched replay on one GPU: R scan updates in flight at once on a shared map.
+
+SURVEY.md §8(e) C5: "replicas only" across scans — every replica is its own
+`slio_handle` (own non-blocking HIP stream, own mapped control block, own scan),
+all reading one device map through `slio_map_share` (include/slio.h). Each
+replica runs `slio_ikf_update_device` (the whole `update_iterated_dyn_share_modified`,
+esekfom.hpp:270-346) from its own host thread; ctypes drops the GIL for the call,
+so the R updates overlap on the device. No collective: replicas are independent.
+
+value = IKF iterations of all replicas / wall time of the timed region. Every
+replica's result is checked bitwise against the same scan run alone first
+(identical inputs => identical x and P), so concurrency cannot change results.
+
+  python scripts/bench_replay.py --replicas 4 --steps 50
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--replicas", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--map-points", type=int, default=10_000_000)
+    ap.add_argument("--scan-points", type=int, default=100_000)
+    ap.add_argument("--cell", type=float, default=1.25)
+    ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
+    args = ap.parse_args()
+
+    from agi_lidar_slam_amd import _lib as L, synth
+
+    lib = L.load()
+    mp, fr = synth.make_problem(args.map_points, args.scan_points, pattern="avia",
+                                cache_dir=args.cache_dir)
+    fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
+    R = args.replicas
+
+    handles = []
+    for r in range(R):
+        p = L.SlioParams()
+        lib.slio_params_default(C.byref(p))
+        p.device, p.max_points, p.rank, p.nranks = 0, args.scan_points, 0, 1
+        p.grid_cell = args.cell
+        h = C.c_void_p()
+        L.check(lib.slio_create(C.byref(h), C.byref(p)), "create")
+        handles.append(h)
+    x, y, z = (np.ascontiguousarray(mp[:, k]) for k in range(3))
+    L.check(lib.slio_map_upload(handles[0], L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")
+    for h in handles[1:]:
+        L.check(lib.slio_map_share(h, handles[0]), "share")
+    bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
+    for h in handles:
+        L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]),
+                "scan")
+
+    st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9),
+                          [0, 0, -9.81]])
+    P0 = np.eye(24) * 1e-2
+    xs0 = L.SlioState()
+    xs0.pos[:] = list(st0[0:3])
+    xs0.rot[:] = list(st0[3:7])
+    xs0.rli[:] = list(st0[7:11])
+    xs0.tli[:] = list(st0[11:14])
+    xs0.grav[:] = list(st0[23:26])
+    reduce_cb = L.ALLREDUCE_FN()
+
+    class Rep:
+        def __init__(self, h):
+            self.h = h
+            self.xs = L.SlioState()
+            self.P = np.empty_like(P0)
+            self.stats = L.SlioIkfStats()
+            self.err = None
+
+        def step(self):
+            C.memmove(C.addressof(self.xs), C.addressof(xs0), C.sizeof(self.xs))
+            self.P[...] = P0
+            rc = lib.slio_ikf_update_device(self.h, C.byref(self.xs), L.dptr(self.P), 0.001,
+                                            args.iters, 0, L.SLIO_MODE_FIXED, reduce_cb, None,
+                                            C.byref(self.stats))
+            L.check(rc, "ikf")
+
+    reps = [Rep(h) for h in handles]
+    # reference result: replica 0 alone
+    reps[0].step()
+    ref_x = bytes(memoryview(reps[0].xs))
+    ref_P = reps[0].P.copy()
+    # single-replica rate (same harness) for the comparison line
+    for _ in range(args.warmup):
+        reps[0].step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        reps[0].step()
+    single = args.steps * args.iters / (time.perf_counter() - t0)
+
+    go = threading.Barrier(R + 1)
+
+    def run(rep):
+        try:
+            for _ in range(args.warmup):
+                rep.step()
+            go.wait()
+            go.wait()
+            for _ in range(args.steps):
+                rep.step()
+        except Exception as e:  # reported after the join
+            rep.err = e
+            try:
+                go.abort()
+            except Exception:
+                pass
+
+    th = [threading.Thread(target=run, args=(rep,)) for rep in reps]
+    for t in th:
+        t.start()
+    go.wait()
+    t0 = time.perf_counter()
+    go.wait()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    for rep in reps:
+        if rep.err:
+            raise rep.err
+    same = all(bytes(memoryview(rep.xs)) == ref_x and np.array_equal(rep.P, ref_P)
+               for rep in reps)
+    for h in reversed(handles):
+        lib.slio_destroy(h)
+    total = R * args.steps * args.iters / el
+    print(json.dumps({
+        "metric": "IKF iterations/sec, batched replay (C5), 100k-pt scans vs shared map",
+        "value": total, "unit": "IKF iterations/s", "replicas": R, "steps": args.steps,
+        "map_points": args.map_points, "scan_points": args.scan_points,
+        "single_replica_value": single, "speedup_vs_single": total / single,
+        "results_identical_to_single": bool(same),
+    }))
+    if not same:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

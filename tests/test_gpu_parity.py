@@ -400,3 +400,60 @@ def test_device_loop_matches_host_loop(L, c1, mode, ext):
     np.testing.assert_allclose(x1, x0, rtol=0, atol=1e-9)
     np.testing.assert_allclose(P1, P0, rtol=0, atol=5e-8 * np.abs(P0).max())
     kd.close()
+
+
+@pytest.mark.gpu
+def test_batched_replay_concurrent_bitwise(L, c1):
+    """C5 batched replay: 4 handles share one map (slio_map_share),
+    each on its own stream, running slio_ikf_update_device from 4 host threads at
+    once; every replica's x and P equal the update run alone, bit for bit."""
+    import threading
+    lib = L.load()
+    mp, fr, _ = c1["avia"]
+    st = state_of(fr)
+    xs0 = L.SlioState()
+    xs0.pos[:] = list(st[0:3])
+    xs0.rot[:] = list(st[3:7])
+    xs0.rli[:] = list(st[7:11])
+    xs0.tli[:] = list(st[11:14])
+    xs0.vel[:] = list(st[14:17])
+    xs0.bg[:] = list(st[17:20])
+    xs0.ba[:] = list(st[20:23])
+    xs0.grav[:] = list(st[23:26])
+    cb = L.ALLREDUCE_FN()
+    hs = [mk(L) for _ in range(4)]
+    try:
+        upload_map(L, hs[0], mp)
+        for h in hs[1:]:
+            L.check(lib.slio_map_share(h, hs[0]), "share")
+        for h in hs:
+            upload_scan(L, h, fr.body)
+
+        def run(h, out, reps):
+            for _ in range(reps):
+                xs = L.SlioState()
+                C.memmove(C.addressof(xs), C.addressof(xs0), C.sizeof(xs))
+                P = np.eye(24) * 1e-2
+                stt = L.SlioIkfStats()
+                rc = lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, 4, 0,
+                                                L.SLIO_MODE_FIXED, cb, None, C.byref(stt))
+                out.append((rc, bytes(memoryview(xs)), P.copy()))
+
+        ref = []
+        run(hs[0], ref, 1)
+        assert ref[0][0] == 0, L.load().slio_last_error()
+        outs = [[] for _ in hs]
+        th = [threading.Thread(target=run, args=(h, o, 3)) for h, o in zip(hs, outs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for o in outs:
+            assert len(o) == 3
+            for rc, xb, P in o:
+                assert rc == 0
+                assert xb == ref[0][1]
+                np.testing.assert_array_equal(P, ref[0][2])
+    finally:
+        for h in reversed(hs):
+            lib.slio_destroy(h)
