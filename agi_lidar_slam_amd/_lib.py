@@ -170,6 +170,7 @@ SIGNATURES = {
     "slio_reduce_super": (C.c_int, [_DP, _DP, _DP, _I64P]),
     "slio_iterate": (C.c_int, [_P, C.POINTER(SlioPose), C.c_int, C.c_int, _DP, _DP, _I64P]),
     "slio_get_neighbors": (C.c_int, [_P, _IP, _FP, _U8P]),
+    "slio_far_queries": (C.c_int, [_P, _I64P]),
     "slio_get_planes": (C.c_int, [_P, _FP]),
     "slio_get_residuals": (C.c_int, [_P, _FP]),
     "slio_profile": (C.c_int, [_P, C.c_int]),

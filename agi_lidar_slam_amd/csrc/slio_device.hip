@@ -108,12 +108,33 @@ struct GridGeom {
   int dx, dy, dz;     // dims
 };
 
+// Coarse level for the queries the fine grid cannot finish cheaply (5th
+// neighbour beyond the 5x5x5 fine cube, query cells outside the grid): cells
+// of edge 4h on the fine grid's origin, the points sorted by coarse cell, and
+// the TIGHT bounding box of every coarse cell's points (exact pruning: a
+// float distance to a point is never below the float distance to a box that
+// contains it, both rounded monotonically).
+struct CoarseView {
+  GridGeom g;               // h = 4 x the fine cell edge
+  const float4* pts;        // sorted by coarse cell: x, y, z, bits(position in the fine pts)
+  const uint32_t* start;    // ncells + 1 prefix offsets
+  const float4* lo;         // per coarse cell: min x, y, z, bits(point count)
+  const float4* hi;         // per coarse cell: max x, y, z
+};
+
 struct MapDev {
   GridGeom g;
   int64_t n = 0;
   int64_t ncells = 0;
   float4* pts = nullptr;          // sorted by cell: x, y, z, bits(map index)
   uint32_t* start = nullptr;      // ncells + 1 prefix offsets
+  // coarse level (CoarseView)
+  GridGeom cg;
+  int64_t nccells = 0;
+  float4* cpts = nullptr;
+  uint32_t* cstart = nullptr;
+  float4* clo = nullptr;
+  float4* chi = nullptr;
   // block rows (optional, ~9x the points): entry (x, y, z) holds the points
   // of the 9 cells (x, y + j, z + k), j, k in {-1, 0, 1}, with .w = their
   // position in pts; entries are laid out in cell order, so the 3x3x3 block
@@ -127,6 +148,10 @@ struct MapDev {
     if (start) (void)hipFree(start);
     if (blk) (void)hipFree(blk);
     if (bstart) (void)hipFree(bstart);
+    if (cpts) (void)hipFree(cpts);
+    if (cstart) (void)hipFree(cstart);
+    if (clo) (void)hipFree(clo);
+    if (chi) (void)hipFree(chi);
   }
 };
 
@@ -140,6 +165,7 @@ struct MapView {
   const uint32_t* bstart;
   int64_t nblk;
   int64_t ncells;
+  CoarseView cl;
 };
 
 #ifdef SLIO_BOUNDS_CHECK
@@ -232,6 +258,51 @@ __global__ void k_blk_fill(const float4* __restrict__ pts, const uint32_t* __res
         blk[o++] = make_float4(v.x, v.y, v.z, __uint_as_float(p));
       }
     }
+}
+
+// coarse level: cell keys of the fine-sorted points, then the gather (values
+// are fine positions, ascending inside a coarse cell after the stable sort)
+__global__ void k_coarse_keys(const float4* __restrict__ pts, int64_t n, GridGeom cg,
+                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = pts[i];
+  int cx = min(max(cell_coord(p.x, cg.ox, cg.inv_h), 0), cg.dx - 1);
+  int cy = min(max(cell_coord(p.y, cg.oy, cg.inv_h), 0), cg.dy - 1);
+  int cz = min(max(cell_coord(p.z, cg.oz, cg.inv_h), 0), cg.dz - 1);
+  keys[i] = ((uint32_t)cz * (uint32_t)cg.dy + (uint32_t)cy) * (uint32_t)cg.dx + (uint32_t)cx;
+  vals[i] = (uint32_t)i;
+}
+
+__global__ void k_coarse_gather(const float4* __restrict__ pts, const uint32_t* __restrict__ order,
+                                int64_t n, float4* __restrict__ cpts) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t o = order[i];
+  const float4 p = pts[o];
+  cpts[i] = make_float4(p.x, p.y, p.z, __uint_as_float(o));
+}
+
+// tight bounding box and count of every coarse cell (one thread per cell)
+__global__ void k_coarse_boxes(const float4* __restrict__ cpts, const uint32_t* __restrict__ cstart,
+                               int64_t nc, float4* __restrict__ lo, float4* __restrict__ hi) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const uint32_t s = cstart[c], e = cstart[c + 1];
+  const float INF = __int_as_float(0x7f800000);
+  float4 l = make_float4(INF, INF, INF, __uint_as_float(e - s));
+  float4 u = make_float4(-INF, -INF, -INF, 0.0f);
+  for (uint32_t p = s; p < e; ++p) {
+    const float4 v = cpts[p];
+    l.x = fminf(l.x, v.x);
+    l.y = fminf(l.y, v.y);
+    l.z = fminf(l.z, v.z);
+    u.x = fmaxf(u.x, v.x);
+    u.y = fmaxf(u.y, v.y);
+    u.z = fmaxf(u.z, v.z);
+  }
+  lo[c] = l;
+  hi[c] = u;
 }
 
 // ---------------------------------------------------------------- math helpers
@@ -807,6 +878,7 @@ struct ScanDev {
   int64_t n;
 };
 
+struct FarQueue;
 struct PassOut {
   int32_t* nbr_idx;  // n * 5
   float* nbr_sqd;    // n * 5
@@ -814,6 +886,12 @@ struct PassOut {
   uint8_t* sel;      // n
   float* resid;      // n
   double* chunk_part;  // C * NPROD (global chunk index)
+  uint64_t* far_in;    // FarQueue (deferred queries), see far_search
+  uint64_t* far_out;
+  uint32_t* far_ready;
+  uint32_t* far_claim;
+  uint32_t* far_ctr;
+  uint32_t* far_pending;
 };
 
 // far_query_margin: squared distance from the query to the grid's bounding box
@@ -836,7 +914,301 @@ struct PassCfg {
   int extrinsic;
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
+  uint32_t epoch;          // this launch's tag for the far-queue ready words (never 0)
 };
+
+// ---------------------------------------------------------------- far queries
+// A query the fine grid cannot finish (its 5th neighbour lies beyond the
+// 5x5x5 fine cube, its cell lies outside the grid, or its block holds fewer
+// than 5 points) is DEFERRED: its chunk's workgroup appends it to a global
+// queue and every workgroup with deferred queries -- and every other one
+// that saw the queue non-empty -- drains the queue one query per wavefront
+// (far_search, all 64 lanes on one query).  The owner then waits for its
+// chunk's answers and runs the fit and products as usual.  The queries that
+// need this are rare and clustered in scan order (e.g. returns with no map
+// support nearby), so handling them inline on their own 2 lanes serialised
+// the wavefront that held them; spread over the chip they cost a few us.
+// Waiting is deadlock-free: a workgroup only waits for entries already
+// claimed by running wavefronts, and a far search waits for nothing but its
+// entry's ready word, which the running owner writes right after reserving.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+struct FarQueue {
+  uint64_t* in;       // 3 words per entry: (qx, qy), (qz, bound), (point index, 0)
+  uint64_t* out;      // 8 words per entry: the 5 sorted keys
+  uint32_t* ready;    // per entry: epoch of the launch that wrote it
+  uint32_t* claim;    // per entry: epoch of the launch in which it was claimed
+  uint32_t* ctr;      // [0] head (next ticket), [1] tail; zero between launches;
+                      // [4..7] first failed wait (kind, index, value seen, tail)
+  uint32_t* pending;  // per chunk: deferred queries not answered yet
+};
+
+// -DSLIO_FAR_TRACE (diagnostic builds only): events into mapped host memory,
+// readable by the host while a kernel runs (slio_dbg_far_trace)
+#ifdef SLIO_FAR_TRACE
+__device__ uint32_t* g_ftrace;
+#define FTRACE(a, b, c)                                                                      \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0 && g_ftrace) {                                               \
+      const uint32_t k_ = __hip_atomic_fetch_add(g_ftrace, 1u, __ATOMIC_RELAXED,            \
+                                                 __HIP_MEMORY_SCOPE_SYSTEM);                 \
+      if (k_ < 4095) {                                                                       \
+        uint32_t* r_ = g_ftrace + 4 + 4 * k_;                                                \
+        __hip_atomic_store(r_ + 0, (blockIdx.x << 8) | (threadIdx.x >> 6), __ATOMIC_RELAXED, \
+                           __HIP_MEMORY_SCOPE_SYSTEM);                                       \
+        __hip_atomic_store(r_ + 1, (uint32_t)(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+        __hip_atomic_store(r_ + 2, (uint32_t)(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+        __hip_atomic_store(r_ + 3, (uint32_t)(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+      }                                                                                      \
+    }                                                                                        \
+  } while (0)
+#else
+#define FTRACE(a, b, c) \
+  do {                  \
+  } while (0)
+#endif
+
+// Every wait on another workgroup is bounded: ~2^21 polls with s_sleep (well
+// over 100 ms) and the wait gives up, records what it waited for and the
+// pass reports SLIO_EDEVICE (slio_far_queries) instead of hanging the GPU.
+constexpr uint32_t kSpinLimit = 1u << 21;
+__device__ __noinline__ void far_wait_failed(uint32_t* ctr, uint32_t kind, uint32_t idx, uint32_t seen) {
+  if (__hip_atomic_fetch_add((gu32*)(ctr + 4), kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    __hip_atomic_store((gu32*)(ctr + 5), idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(ctr + 6), seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(ctr + 7),
+                       __hip_atomic_load((gu32*)(ctr + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ void st_sc1_u64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t pack2f(float a, float b) {
+  return ((uint64_t)__float_as_uint(b) << 32) | (uint64_t)__float_as_uint(a);
+}
+
+// exclusive prefix sum over the wavefront's 64 lanes; total to every lane
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t s = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(s, d, 64);
+    if (lane >= d) s += o;
+  }
+  total = __shfl(s, 63, 64);
+  return s - v;
+}
+
+// The exact 5-NN of one query by a whole wavefront on the coarse level:
+// Chebyshev rings R = 0, 1, ... of coarse cells around the query's (clamped)
+// cell; a cell is scanned unless its tight box lies farther than the bound
+// (the 5th distance found so far, or bound0: the 5th distance of 5 real map
+// points, or +inf).  The candidate cells of a batch of 64 ring positions are
+// flattened into one list (lane prefix sums in LDS, a 6-step binary search
+// per candidate) and swept with U loads in flight per lane.  The search ends
+// when every unscanned cell lies beyond the 5th distance: the bound over the
+// six slabs outside the ring's cube is per-axis exact (face distance on the
+// slab's axis, distance to the grid's range on the other two).  Keys carry
+// the fine pts position (.w), so results equal the fine grid's.  Returns the
+// list in every lane.
+template <int U>
+__device__ __forceinline__ void far_search(const CoarseView& cv, float qx, float qy, float qz,
+                                        float bound, uint32_t* __restrict__ pre,
+                                        uint32_t* __restrict__ beg, Top5& t) {
+  const int lane = threadIdx.x & 63;
+  const GridGeom g = cv.g;
+  const float INF = __int_as_float(0x7f800000);
+  top5_clear(t);
+  bool full = false;
+  float d5 = INF;
+  const int CX = min(max(cell_coord(qx, g.ox, g.inv_h), 0), g.dx - 1);
+  const int CY = min(max(cell_coord(qy, g.oy, g.inv_h), 0), g.dy - 1);
+  const int CZ = min(max(cell_coord(qz, g.oz, g.inv_h), 0), g.dz - 1);
+  // distance of q to the grid's range on each axis (every map point lies in it)
+  auto range_gap = [&](float q, float o, int d) {
+    const float lo = o - g.tol, hi = o + (float)d * g.h + g.tol;
+    return fmaxf(fmaxf(lo - q, q - hi), 0.0f);
+  };
+  const float ax = range_gap(qx, g.ox, g.dx), ay = range_gap(qy, g.oy, g.dy),
+              az = range_gap(qz, g.oz, g.dz);
+  for (int R = 0;; ++R) {
+    const int x0 = max(CX - R, 0), x1 = min(CX + R, g.dx - 1);
+    const int y0 = max(CY - R, 0), y1 = min(CY + R, g.dy - 1);
+    const int z0 = max(CZ - R, 0), z1 = min(CZ + R, g.dz - 1);
+    const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+    const int total = nx * ny * nz;
+    for (int base = 0; base < total; base += 64) {
+      const int p = base + lane;
+      uint32_t s = 0, k = 0;
+      if (p < total) {
+        const int x = x0 + p % nx, y = y0 + (p / nx) % ny, z = z0 + p / (nx * ny);
+        if (max(abs(x - CX), max(abs(y - CY), abs(z - CZ))) == R) {
+          const uint32_t c = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx + (uint32_t)x;
+          const float4 lo = cv.lo[c];
+          const uint32_t cnt = __float_as_uint(lo.w);
+          if (cnt) {
+            const float4 hi = cv.hi[c];
+            const float gx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
+            const float gy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
+            const float gz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
+            const float gd = (gx * gx + gy * gy) + gz * gz;
+            if (!(gd > fminf(bound, d5))) {  // a point at exactly d5 may still win on position
+              s = cv.start[c];
+              k = cnt;
+            }
+          }
+        }
+      }
+      if (!__any(k != 0)) continue;
+      uint32_t tot;
+      const uint32_t ex = wave_excl_scan(k, tot);
+      pre[lane] = ex;
+      beg[lane] = s;
+      wave_fence();
+      for (uint32_t f0 = 0; f0 < tot; f0 += 64 * U) {
+        uint32_t a[U];
+        float4 c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t f = min(f0 + (uint32_t)(u * 64 + lane), tot - 1);
+          int j = 0;
+#pragma unroll
+          for (int st = 32; st > 0; st >>= 1)
+            if (pre[j + st] <= f) j += st;
+          a[u] = beg[j] + (f - pre[j]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = cv.pts[a[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
+          const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+          const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c[u].w);
+          top5_insert(t, (f0 + (uint32_t)(u * 64 + lane) < tot) ? key : kInfKey);
+        }
+      }
+      group_merge<64>(t);  // every lane: the merged list
+      full = t.k[4] != kInfKey;
+      if (full) d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+      if (lane != 0) top5_clear(t);  // lane 0 keeps it
+      wave_fence();                  // pre / beg are rewritten by the next batch
+    }
+    // lower bound of the squared distance to every cell outside this cube
+    float lb = INF;
+    bool covers = true;
+    auto slab = [&](bool open, float face_gap, float o1, float o2) {
+      if (!open) return;
+      covers = false;
+      const float f = fmaxf(face_gap, 0.0f);
+      lb = fminf(lb, (f * f + o1 * o1) + o2 * o2);
+    };
+    slab(x0 > 0, qx - (g.ox + (float)x0 * g.h + g.tol), ay, az);
+    slab(x1 < g.dx - 1, (g.ox + (float)(x1 + 1) * g.h - g.tol) - qx, ay, az);
+    slab(y0 > 0, qy - (g.oy + (float)y0 * g.h + g.tol), ax, az);
+    slab(y1 < g.dy - 1, (g.oy + (float)(y1 + 1) * g.h - g.tol) - qy, ax, az);
+    slab(z0 > 0, qz - (g.oz + (float)z0 * g.h + g.tol), ax, ay);
+    slab(z1 < g.dz - 1, (g.oz + (float)(z1 + 1) * g.h - g.tol) - qz, ax, ay);
+    if (covers || (full && d5 < lb * 0.99999f)) break;
+    if (R > g.dx + g.dy + g.dz) break;  // unreachable: the cube covers the grid long before
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) t.k[j] = __shfl(t.k[j], 0, 64);
+}
+
+// Answer far-queue entry e (claimed): wait for its ready word, search,
+// publish the 5 keys write-through and drained, count it off its chunk.
+template <int U>
+__device__ __forceinline__ void far_answer(const CoarseView& cv, const FarQueue& fq, uint32_t epoch,
+                                           uint32_t e, uint32_t* pre, uint32_t* beg) {
+  const int lane = threadIdx.x & 63;
+  FTRACE(10, e, 0);
+  if (lane == 0) {
+    uint32_t it = 0, v;
+    while ((v = ld_sc1_u32(fq.ready + e)) != epoch) {
+      if (++it > kSpinLimit) {
+        far_wait_failed(fq.ctr, 1u, e, v);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  const uint64_t w0 = ld_sc1_u64(fq.in + 3 * (size_t)e), w1 = ld_sc1_u64(fq.in + 3 * (size_t)e + 1),
+                 w2 = ld_sc1_u64(fq.in + 3 * (size_t)e + 2);
+  const float qx = __uint_as_float((uint32_t)w0), qy = __uint_as_float((uint32_t)(w0 >> 32));
+  const float qz = __uint_as_float((uint32_t)w1), bound = __uint_as_float((uint32_t)(w1 >> 32));
+  const uint32_t i = (uint32_t)w2;
+  Top5 t;
+  FTRACE(11, e, i);
+  far_search<U>(cv, qx, qy, qz, bound, pre, beg, t);
+  FTRACE(12, e, (uint32_t)(t.k[4] >> 32));
+  uint64_t mine = t.k[0];
+#pragma unroll
+  for (int j = 1; j < 5; ++j) mine = (lane == j) ? t.k[j] : mine;
+  if (lane < 5) st_sc1_u64(fq.out + 8 * (size_t)e + lane, mine);
+  drain_stores();
+  if (lane == 0)
+    __hip_atomic_fetch_add((gu32*)(fq.pending + i / SLIO_CHUNK), 0xFFFFFFFFu, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Claim entry e for this wavefront: one exchange on its claim word (the
+// owner's leftover pass and a ticket holder may both try).
+__device__ __forceinline__ bool far_claim(const FarQueue& fq, uint32_t epoch, uint32_t e) {
+  uint32_t prev = 0;
+  if ((threadIdx.x & 63) == 0)
+    prev = __hip_atomic_exchange((gu32*)(fq.claim + e), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __shfl(prev, 0, 64) != epoch;
+}
+
+// One wavefront drains the far queue by tickets: one fetch-and-add on the
+// head per entry (no compare-and-swap retries: thousands of wavefronts
+// retrying on one word cost milliseconds); a ticket past the tail ends the
+// loop.  Entries appended after the head overtook the tail get no ticket:
+// their owner answers them itself (far_own_leftovers).
+template <int U>
+__device__ __forceinline__ void far_worker(const CoarseView& cv, const FarQueue& fq, uint32_t epoch,
+                                           uint32_t* pre, uint32_t* beg) {
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    uint32_t e = 0xFFFFFFFFu;
+    if (lane == 0) {
+      const uint32_t tk = __hip_atomic_fetch_add((gu32*)fq.ctr, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if (tk < ld_sc1_u32(fq.ctr + 1)) e = tk;
+    }
+    e = __shfl(e, 0, 64);
+    FTRACE(20, e, 0);
+    if (e == 0xFFFFFFFFu) break;
+    if (far_claim(fq, epoch, e)) far_answer<U>(cv, fq, epoch, e, pre, beg);
+  }
+}
+
+// The owner's own entries [base, base + n) that no ticket holder claimed,
+// wavefront w of the workgroup taking entries w, w + waves, ...
+template <int U, int NT>
+__device__ __forceinline__ void far_own_leftovers(const CoarseView& cv, const FarQueue& fq, uint32_t epoch,
+                                                  uint32_t base, int n, uint32_t* pre, uint32_t* beg) {
+  for (int k = threadIdx.x >> 6; k < n; k += NT / 64)
+    if (far_claim(fq, epoch, base + k)) far_answer<U>(cv, fq, epoch, base + k, pre, beg);
+}
 
 __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
   // blocks b and b+8 share an XCD: give each XCD group a contiguous chunk range
@@ -865,11 +1237,6 @@ __device__ __forceinline__ uint32_t arrive(uint32_t* p) {
 }
 __device__ __forceinline__ void reset_counter(uint32_t* p) {
   __hip_atomic_store((guint*)p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wave_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
 }
 
 // LDS of the filter step.
@@ -1362,6 +1729,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __shared__ uint32_t nb_pos[SLIO_CHUNK][5];
   __shared__ float nb_d5[SLIO_CHUNK];
   __shared__ float4 qw[SLIO_CHUNK];
+  // deferred (far) queries of this chunk and the far workers' scratch
+  __shared__ int far_cnt;
+  __shared__ uint32_t far_base;
+  __shared__ float4 far_q[SLIO_CHUNK];
+  __shared__ uint8_t far_slot[SLIO_CHUNK];
+  __shared__ uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
+  const FarQueue fq{out.far_in, out.far_out, out.far_ready, out.far_claim, out.far_ctr, out.far_pending};
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
   const int tid = threadIdx.x;
   const int sub = tid & (LPQ - 1);
@@ -1370,6 +1744,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   const float4* __restrict__ pts = map.pts;
   const uint32_t* __restrict__ start = map.start;
   if (tid == 0) STAMP(0);
+  if (tid == 0) far_cnt = 0;
+  __syncthreads();
 
   // ---------------- phase 1: exact 5-NN
   // (no early exit per lane: the refinement below needs the whole wavefront)
@@ -1436,6 +1812,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           }
         }
         r = 2;
+#ifndef SLIO_NO_R2_REFINE
+      } else if (r == 2 && !SPHERE) {
+        // query cell two cells outside the grid (e.g. a long-range ground
+        // return below the padded grid at a slightly wrong pose): its 3x3x3
+        // block is empty; the 5x5x5 cube is the refinement with no limit,
+        // exact if the 5th distance then lies within the cube's bound
+        refine = true;
+        lim = __int_as_float(0x7f800000);
+#endif
       } else if (r == 1) {
         // sphere-first search: (1) cells of the 5x5x5 cube whose box gap^2 <=
         // rho0^2, exact once 5 neighbours lie within rho0; (2) the shell out
@@ -1523,19 +1908,25 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           const uint64_t k = __shfl(tr.k[j], from, 64);
           if (mine) top5_insert(t, k);
         }
-        if (mine) done = true;
+        if (mine) {
+          // exact once the 5th distance lies inside the 5x5x5 cube's bound
+          // (always, when the block's own 5th distance did: lim = d5)
+          bool cov2;
+          const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, cov2);
+          const float d5n = __uint_as_float((uint32_t)(t.k[4] >> 32));
+          done = cov2 || (t.k[4] != kInfKey && b2 > 0.0f && d5n < (b2 * b2) * 0.99999f);
+        }
       }
       WSTAMP(1, __builtin_amdgcn_s_memrealtime());
     }
-    // (3) general fallback: full cubes r, r+1, ... rescanned from scratch
-    for (; !done; ++r) {
-      top5_clear(t);
-      scan_cube<LPQ, U>(pts, start, g, cx, cy, cz, r, sub, qx, qy, qz, t);
-      group_merge<LPQ>(t);
-      bool covers;
-      const float b = outside_bound(g, cx, cy, cz, r, qx, qy, qz, covers);
-      const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
-      done = covers || (t.k[4] != kInfKey && b > 0.0f && d5 < (b * b) * 0.99999f);
+    // (3) not finished on the fine grid: deferred to the far queue (the
+    // group's list is merged: its 5th distance, if any, bounds the search)
+    if (!done && sub == 0) {
+      const int k = atomicAdd(&far_cnt, 1);
+      far_slot[k] = (uint8_t)slot;
+      far_q[k] = make_float4(qx, qy, qz,
+                             t.k[4] != kInfKey ? __uint_as_float((uint32_t)(t.k[4] >> 32))
+                                               : __int_as_float(0x7f800000));
     }
 #ifndef SLIO_REFINE_STAMP
     WSTAMP(2, __builtin_amdgcn_s_memrealtime());
@@ -1544,7 +1935,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     // (map indices are written by the fit phase, which loads the points)
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      if (j % LPQ == sub && live) {
+      if (j % LPQ == sub && live && done) {
         const uint64_t mk = t.k[j];
         out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                  : __uint_as_float((uint32_t)(mk >> 32));
@@ -1561,6 +1952,68 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if ((tid >> 6) < 4) STAMP(4 + (tid >> 6));  // per-wave end of the kNN phase
   __syncthreads();
   if (tid == 0) STAMP(1);
+  const int nfar = far_cnt;
+  uint32_t tail_peek = 0;
+  FTRACE(1, nfar, chunk);
+  if (nfar > 0) {
+    // publish this chunk's deferred queries: the pending count first (a
+    // worker may answer as soon as an entry is ready), then the entries
+    if (tid == 0) {
+      st_sc1_u32(fq.pending + chunk, (uint32_t)nfar);
+      drain_stores();
+      far_base = __hip_atomic_fetch_add((gu32*)(fq.ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (tid < nfar) {
+      const size_t e = far_base + tid;
+      const float4 q = far_q[tid];
+      st_sc1_u64(fq.in + 3 * e, pack2f(q.x, q.y));
+      st_sc1_u64(fq.in + 3 * e + 1, pack2f(q.z, q.w));
+      st_sc1_u64(fq.in + 3 * e + 2, (uint64_t)(chunk * SLIO_CHUNK + far_slot[tid]));
+      drain_stores();
+      st_sc1_u32(fq.ready + e, cfg.epoch);
+    }
+    // help drain the queue, answer what is left of this chunk's entries,
+    // then wait for all of this chunk's answers
+    far_worker<4>(map.cl, fq, cfg.epoch, far_pre[tid >> 6], far_beg[tid >> 6]);
+    far_own_leftovers<4, NT>(map.cl, fq, cfg.epoch, far_base, nfar, far_pre[tid >> 6], far_beg[tid >> 6]);
+    __syncthreads();
+    FTRACE(30, far_base, nfar);
+    if (tid == 0) {
+      uint32_t it = 0, v;
+      while ((v = ld_sc1_u32(fq.pending + chunk)) != 0u) {
+        if (++it > kSpinLimit) {
+          far_wait_failed(fq.ctr, 2u, (uint32_t)chunk, v);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain_stores();
+    }
+    __syncthreads();
+    if (tid < nfar) {
+      const size_t e = far_base + tid;
+      const int slot = far_slot[tid];
+      const int64_t i = chunk * SLIO_CHUNK + slot;
+      uint64_t k4 = kInfKey;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const uint64_t mk = ld_sc1_u64(fq.out + 8 * e + j);
+        out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+                                                 : __uint_as_float((uint32_t)(mk >> 32));
+        nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
+        k4 = mk;
+      }
+      nb_d5[slot] = (k4 != kInfKey) ? __uint_as_float((uint32_t)(k4 >> 32)) : __int_as_float(0x7f800000);
+    }
+    __syncthreads();
+  } else if (tid == 0) {
+    // a look at the queue, in flight behind the fit phase's loads: if
+    // other chunks deferred queries, this workgroup helps once it is done
+    tail_peek = ld_sc1_u32(fq.ctr + 1);
+  }
 
   // ---------------- phase 2: plane fit, residual gate, Jacobian row
   if (tid < SLIO_CHUNK) {
@@ -1624,8 +2077,21 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __syncthreads();
   if (tid == 0) STAMP(2);
   // ---------------- phase 3: fixed-order products
+  FTRACE(40, 0, 0);
   chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
   if (tid == 0) STAMP(3);
+  if (nfar == 0) {
+    // about one helping wavefront per queued query: every stride-th
+    // workgroup joins (all of them when the queue is long)
+    __shared__ uint32_t help;
+    if (tid == 0) {
+      const uint32_t waves = gridDim.x * (NT / 64);
+      const uint32_t stride = tail_peek ? max(1u, waves / tail_peek) : 0u;
+      help = tail_peek && (blockIdx.x % stride) == 0;
+    }
+    __syncthreads();
+    if (help) far_worker<4>(map.cl, fq, cfg.epoch, far_pre[tid >> 6], far_beg[tid >> 6]);
+  }
 }
 
 // Non-search pass: reuse neighbours/plane/selection (esekfom.hpp:138-150 with
@@ -1696,6 +2162,13 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
   const int s = blockIdx.x;
   const int t = threadIdx.x;
   if (ctl) SSTAMP(0);
+  // the pass kernel before this one is complete: keep its number of far
+  // queries (slio_far_queries), reset the queue's head and tail
+  if (s == 0 && t == 0) {
+    st_sc1_u32(cnt + 6, ld_sc1_u32(cnt + 5));
+    st_sc1_u32(cnt + 4, 0u);
+    st_sc1_u32(cnt + 5, 0u);
+  }
   {
     // pair p = g * NPROD + kk: segment g, product kk; chunk c0 + g + 8 j of
     // pair p sits at chunk_part[(c0 + 8 j) * NPROD + p]
@@ -1796,9 +2269,17 @@ struct Ctx {
   uint8_t* sel = nullptr;
   float* resid = nullptr;
   double* chunk_part = nullptr;
+  // far queue (deferred queries, see far_search)
+  uint64_t* far_in = nullptr;
+  uint64_t* far_out = nullptr;
+  uint32_t* far_ready = nullptr;
+  uint32_t* far_claim = nullptr;
+  uint32_t* far_pending = nullptr;
+  uint32_t far_epoch = 0;
   double* d_super = nullptr;
   double* d_super_own = nullptr;
-  uint32_t* count = nullptr;  // k_super_sums arrival counter (zero between launches)
+  uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
+                              // (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
   IkfCtl* h_ctl = nullptr;  // mapped, coherent host block: update input and output
   IkfCtl* d_hctl = nullptr; // its device view
@@ -1894,6 +2375,13 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->sel);
   (void)hipFree(c->resid);
   (void)hipFree(c->chunk_part);
+  (void)hipFree(c->far_in);
+  (void)hipFree(c->far_out);
+  (void)hipFree(c->far_ready);
+  (void)hipFree(c->far_claim);
+  (void)hipFree(c->far_pending);
+  c->far_in = c->far_out = nullptr;
+  c->far_ready = c->far_claim = c->far_pending = nullptr;
   c->bx = c->by = c->bz = nullptr;
   c->nbr_idx = nullptr;
   c->nbr_sqd = nullptr;
@@ -1992,7 +2480,11 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_begin = c0;
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
-  PassOut o{c.nbr_idx, c.nbr_sqd, c.plane, c.sel, c.resid, c.chunk_part};
+  PassOut o{c.nbr_idx,  c.nbr_sqd,   c.plane,     c.sel,     c.resid,
+            c.chunk_part, c.far_in, c.far_out, c.far_ready, c.far_claim, c.count + 4,
+            c.far_pending};
+  if (++c.far_epoch == 0) c.far_epoch = 1;  // ready words are 0 when allocated
+  cfg.epoch = c.far_epoch;
   ScanDev s{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
@@ -2011,8 +2503,9 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   };
   if (nblk > 0 && run_search) {
     const auto ev = timing(SLIO_KERNEL_SEARCH);
-    const MapView mv{c.map->g,     c.map->n,      c.map->pts,  c.map->start,
-                     c.map->blk,   c.map->bstart, c.map->nblk, c.map->ncells};
+    const CoarseView cv{c.map->cg, c.map->cpts, c.map->cstart, c.map->clo, c.map->chi};
+    const MapView mv{c.map->g,   c.map->n,    c.map->pts,    c.map->start, c.map->blk,
+                     c.map->bstart, c.map->nblk, c.map->ncells, cv};
     const bool sph = cfg.radius_sq > 0.0f;
     const dim3 nb((unsigned)nblk);
 #define SLIO_LAUNCH(L, SPH, DEV)                                                                   \
@@ -2133,7 +2626,7 @@ int slio_params_default(slio_params* p) {
   p->plane_threshold = 0.1f;
   p->max_match_sqd = 5.0f;
   p->max_grid_cells = (int64_t)1 << 29;
-  p->far_query_margin = 100.0f;
+  p->far_query_margin = 0.0f;  // exact everywhere (ikd-Tree has no cut)
   return SLIO_OK;
 }
 
@@ -2341,6 +2834,62 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
       fail("build kernels", e);
       break;
     }
+    // coarse level: cells of edge 4h on the same origin, points re-sorted by
+    // coarse cell (stable: fine positions ascend inside a cell), tight boxes
+    {
+      GridGeom cg = g;
+      cg.h = 4.0f * g.h;
+      cg.inv_h = 1.0f / cg.h;
+      cg.dx = (g.dx + 3) / 4;
+      cg.dy = (g.dy + 3) / 4;
+      cg.dz = (g.dz + 3) / 4;
+      m->cg = cg;
+      m->nccells = (int64_t)cg.dx * cg.dy * cg.dz;
+      int cbits = 1;
+      while (cbits < 32 && ((int64_t)1 << cbits) < m->nccells) ++cbits;
+      size_t t1 = 0, t2 = 0;
+      if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, cbits, st)) ||
+          (e = hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cnt, m->cstart, (int)(m->nccells + 1), st))) {
+        fail("coarse sizes", e);
+        break;
+      }
+      if (std::max(t1, t2) > tb) {
+        (void)hipFree(tmp);
+        tmp = nullptr;
+        tb = std::max(t1, t2);
+        if ((e = hipMalloc(&tmp, tb))) {
+          fail("hipMalloc tmp", e);
+          rc = SLIO_ENOMEM;
+          break;
+        }
+      }
+      if ((e = hipMalloc(&m->cpts, sizeof(float4) * n)) ||
+          (e = hipMalloc(&m->cstart, sizeof(uint32_t) * (m->nccells + 1))) ||
+          (e = hipMalloc(&m->clo, sizeof(float4) * m->nccells)) ||
+          (e = hipMalloc(&m->chi, sizeof(float4) * m->nccells))) {
+        fail("hipMalloc coarse", e);
+        rc = SLIO_ENOMEM;
+        break;
+      }
+      k_coarse_keys<<<nb, 256, 0, st>>>(m->pts, n, cg, k0, v0);
+      if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, cbits, st)) ||
+          (e = hipMemsetAsync(cnt, 0, 4 * (m->nccells + 1), st))) {
+        fail("coarse sort", e);
+        break;
+      }
+      k_cell_hist<<<nb, 256, 0, st>>>(k1, n, cnt);
+      if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, m->cstart, (int)(m->nccells + 1), st))) {
+        fail("coarse scan", e);
+        break;
+      }
+      k_coarse_gather<<<nb, 256, 0, st>>>(m->pts, v1, n, m->cpts);
+      k_coarse_boxes<<<(int)((m->nccells + 255) / 256), 256, 0, st>>>(m->cpts, m->cstart, m->nccells,
+                                                                      m->clo, m->chi);
+      if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+        fail("coarse kernels", e);
+        break;
+      }
+    }
     // block rows (speed only): skipped when disabled, when their positions
     // would overflow 32 bits or when the device memory is not there
     const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
@@ -2445,7 +2994,11 @@ int slio_scan_upload(slio_handle h, const float* x, const float* y, const float*
         (e = hipMalloc(&c.bz, 4 * cap)) || (e = hipMalloc(&c.nbr_idx, 4 * 5 * cap)) ||
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
-        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {
+        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
+        (e = hipMalloc(&c.far_in, 8 * 3 * cap)) || (e = hipMalloc(&c.far_out, 8 * 8 * cap)) ||
+        (e = hipMalloc(&c.far_ready, 4 * cap)) || (e = hipMalloc(&c.far_claim, 4 * cap)) ||
+        (e = hipMalloc(&c.far_pending, 4 * capc)) || (e = hipMemset(c.far_ready, 0, 4 * cap)) ||
+        (e = hipMemset(c.far_claim, 0, 4 * cap)) || (e = hipMemset(c.far_pending, 0, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio_scan_upload: hipMalloc: ") + hipGetErrorString(e));
       return SLIO_ENOMEM;
@@ -2666,6 +3219,24 @@ int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel) {
   return SLIO_OK;
 }
 
+int slio_far_queries(slio_handle h, int64_t* n) {
+  SLIO_CHECK_H(h);
+  uint32_t v[16] = {};
+  SLIO_HIP(hipStreamSynchronize(h->c.stream));
+  SLIO_HIP(hipMemcpy(v, h->c.count, sizeof(v), hipMemcpyDeviceToHost));
+  if (n) *n = v[6];
+  if (v[8]) {
+    // a bounded wait of the far queue gave up (count + 8: FarQueue::ctr[4..7])
+    char msg[160];
+    std::snprintf(msg, sizeof msg, "far queue wait timed out: kind %u index %u seen %u tail %u", v[8],
+                  v[9], v[10], v[11]);
+    set_error(msg);
+    SLIO_HIP(hipMemset(h->c.count + 8, 0, 4 * sizeof(uint32_t)));
+    return SLIO_EDEVICE;
+  }
+  return SLIO_OK;
+}
+
 int slio_get_planes(slio_handle h, float* abcd) {
   SLIO_CHECK_H(h);
   Ctx& c = h->c;
@@ -2691,6 +3262,14 @@ int slio_get_residuals(slio_handle h, float* pd2) {
 }
 
 }  // extern "C"
+
+#ifdef SLIO_FAR_TRACE
+extern "C" int slio_dbg_far_trace(void* host_mapped) {
+  void* d = nullptr;
+  if (host_mapped && hipHostGetDevicePointer(&d, host_mapped, 0) != hipSuccess) return -3;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace), &d, sizeof(d)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 #ifdef SLIO_SOLVE_STAMP
 extern "C" int slio_dbg_solve_stamps(unsigned long long* out) {

@@ -73,11 +73,11 @@ typedef struct slio_params {
                               speed.                                           */
   float far_query_margin;  /* scan points farther than this (metres) outside
                               the map grid's bounding box get no neighbours
-                              (index -1, never selected) instead of an exact
-                              but unbounded far search; default 100.  They
-                              cannot pass the max_match_sqd gate anyway, so
-                              only Nearest_Points differs from ikd-Tree.
-                              0 disables the cut (exact everywhere).          */
+                              (index -1, never selected) instead of the exact
+                              coarse-level far search.  They cannot pass the
+                              max_match_sqd gate anyway, so only
+                              Nearest_Points would differ from ikd-Tree.
+                              Default 0: no cut, exact everywhere.            */
 } slio_params;
 
 /* Pose slice of state_ikfom used by the measurement model
@@ -167,6 +167,12 @@ int slio_iterate(slio_handle h, const slio_pose* x, int do_search,
  * fewer than 5 map points exist), f32 squared distances ascending (the
  * pointSearchSqDis of esekfom.hpp:135-141), final selection flag. */
 int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel);
+/* Number of scan points of the last pass (of this handle's shard) whose
+ * 5-NN search did not finish on the fine grid -- 5th neighbour beyond the
+ * 5x5x5 fine-cell cube, query cell outside the grid, or fewer than 5 points
+ * in the 3x3x3 block -- and went to the coarse-level far search instead
+ * (diagnostic; synchronises the stream). */
+int slio_far_queries(slio_handle h, int64_t* n);
 /* Plane (a, b, c, d) per point; (a,b,c) unit normal, d offset, or NaNs where
  * esti_plane failed or the point was gated out before the fit. */
 int slio_get_planes(slio_handle h, float* abcd);

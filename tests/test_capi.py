@@ -53,7 +53,7 @@ def test_params_default(lib):
     assert lib.slio_params_default(C.byref(p)) == 0
     assert p.max_points == 100000 and p.nranks == 1
     assert abs(p.plane_threshold - 0.1) < 1e-7 and p.max_match_sqd == 5.0
-    assert p.far_query_margin == 100.0 and p.search_radius == 0.0
+    assert p.far_query_margin == 0.0 and p.search_radius == 0.0
 
 
 def test_bad_arguments_fail_loudly(lib):

@@ -1,0 +1,145 @@
+"""GPU parity of the far-query path (coarse-level search through the far queue).
+
+A scan point whose 5-NN the fine grid cannot finish -- 5th neighbour beyond
+the 5x5x5 fine cube, query cell outside the grid, fewer than 5 points in the
+3x3x3 block -- is deferred to the far queue and answered by a whole
+wavefront on the coarse level (slio_device.hip, far_search).  ikd-Tree has no
+such split (ikd_Tree.cpp:960-1101 visits the tree the same way for every
+query), so the bar is the same as for every other query: indices and squared
+distances bit-exact vs the oracle's ikd-Tree restatement.
+
+The hard case is a scan taken from inside a building (synth sensor="origin"):
+its ground returns under the building's footprint have no map support, so
+their 5th neighbour lies metres away (2.5-13.5 m at the 50M-point scene).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_gpu_parity import (IDENT, L, mk, results, state_of, upload_map,  # noqa: E402,F401
+                             upload_scan, iterate)
+
+pytestmark = pytest.mark.gpu
+
+
+def far_count(L, h):
+    n = C.c_int64()
+    L.check(L.load().slio_far_queries(h, C.byref(n)), "far")
+    return n.value
+
+
+@pytest.fixture(scope="module")
+def inside(oracle_mod):
+    from agi_lidar_slam_amd import synth
+    mp, fr = synth.make_problem(200000, 20000, pattern="avia", sensor="origin")
+    return mp, fr, oracle_mod.Tree(mp)
+
+
+@pytest.mark.parametrize("cell,lpq,radius,blockrows", [
+    (1.25, 0, None, True), (0.75, 0, None, True), (0.37, 0, None, True), (2.5, 0, None, True),
+    (1.25, 1, None, True), (1.25, 8, None, True), (0.75, 0, 1.0, True), (1.25, 0, None, False)])
+def test_far_queries_inside_building_bitexact(L, oracle_mod, inside, monkeypatch, cell, lpq, radius,
+                                              blockrows):
+    """Every query of a scan with unsupported returns, over cell edges, lanes per
+    query, the sphere-first search and the 9-run path: bit-exact, and the far
+    queue was used."""
+    if not blockrows:
+        monkeypatch.setenv("SLIO_NO_BLOCK_ROWS", "1")
+    mp, fr, T = inside
+    st = state_of(fr)
+    q = oracle_mod.body_to_world(st, fr.body)
+    ridx, rsqd = T.knn(q, 5)
+    h = mk(L, cell=cell, lpq=lpq, radius=radius)
+    try:
+        upload_map(L, h, mp)
+        upload_scan(L, h, fr.body)
+        iterate(L, h, st, True)
+        nfar = far_count(L, h)
+        idx, sqd, *_ = results(L, h, q.shape[0])
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_array_equal(sqd, rsqd)
+        # unsupported returns exist (5th neighbour > 2 m); those beyond any
+        # 5x5x5 cube went to the far path
+        assert (rsqd[:, 4] > 4.0).sum() > 50
+        must = int((rsqd[:, 4] > 9.1 * cell * cell).sum())  # beyond any 5x5x5 cube
+        assert nfar >= must
+        if cell <= 0.75:
+            assert must > 0
+        # the queue is reset between launches: a second pass gives the same answer
+        iterate(L, h, st, True)
+        assert far_count(L, h) == nfar
+        idx2, sqd2, *_ = results(L, h, q.shape[0])
+        np.testing.assert_array_equal(idx2, ridx)
+    finally:
+        L.load().slio_destroy(h)
+
+
+def test_far_queue_random_queries(L, oracle_mod, inside):
+    """Queries anywhere: in empty air inside the grid, just outside it, km away
+    (the old far_query_margin cut is off by default).  Most are deferred; the
+    queue is drained by every workgroup; results are bit-exact."""
+    mp, _, T = inside
+    rng = np.random.default_rng(5)
+    lo, hi = mp.min(0), mp.max(0)
+    q = np.concatenate([
+        rng.uniform(lo, hi, (6000, 3)),
+        rng.uniform(lo - 40, hi + 40, (3000, 3)),
+        mp[rng.choice(mp.shape[0], 3000)] + rng.normal(0, 2.0, (3000, 3)),
+        np.array([[2e3, 0, 5], [-1e3, 1e3, 0], [0, 0, 400], [0, 0, -300]]),
+    ]).astype(np.float32)
+    ridx, rsqd = T.knn(q, 5)
+    h = mk(L, cell=1.25, n_max=q.shape[0])
+    try:
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, q) == 0
+        iterate(L, h, IDENT, True)
+        assert far_count(L, h) > 3000
+        idx, sqd, *_ = results(L, h, q.shape[0])
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_array_equal(sqd, rsqd)
+    finally:
+        L.load().slio_destroy(h)
+
+
+def test_far_tiny_maps(L, oracle_mod):
+    """Maps of 1..7 points (every query deferred, fewer than 5 neighbours for
+    some) and a degenerate flat map."""
+    rng = np.random.default_rng(9)
+    for npts in (1, 4, 5, 7):
+        mp = rng.uniform(-3, 3, (npts, 3)).astype(np.float32)
+        q = rng.uniform(-10, 10, (300, 3)).astype(np.float32)
+        h = mk(L, cell=1.0, n_max=300)
+        try:
+            upload_map(L, h, mp)
+            upload_scan(L, h, q)
+            iterate(L, h, IDENT, True)
+            idx, sqd, *_ = results(L, h, q.shape[0])
+            d = ((q[:, None, :] - mp[None]) ** 2)
+            d32 = (d[..., 0] + d[..., 1]) + d[..., 2]
+            order = np.lexsort((np.broadcast_to(np.arange(npts), d32.shape), d32), axis=1)
+            k = min(5, npts)
+            np.testing.assert_array_equal(idx[:, :k], order[:, :k])
+            np.testing.assert_array_equal(sqd[:, :k], np.take_along_axis(d32, order, 1)[:, :k])
+            assert (idx[:, k:] == -1).all()
+        finally:
+            L.load().slio_destroy(h)
+    # flat map (z = 0 plane), queries high above it
+    g = np.stack(np.meshgrid(np.arange(40.0), np.arange(40.0), indexing="ij"), -1).reshape(-1, 2)
+    mp = np.concatenate([g * 0.5, np.zeros((g.shape[0], 1))], 1).astype(np.float32)
+    q = np.concatenate([rng.uniform(0, 20, (500, 2)), rng.uniform(3, 60, (500, 1))], 1).astype(np.float32)
+    T = oracle_mod.Tree(mp)
+    ridx, rsqd = T.knn(q, 5)
+    h = mk(L, cell=0.5, n_max=500)
+    try:
+        upload_map(L, h, mp)
+        upload_scan(L, h, q)
+        iterate(L, h, IDENT, True)
+        idx, sqd, *_ = results(L, h, q.shape[0])
+        # the flat grid has exact distance ties: compare the distance lists
+        np.testing.assert_array_equal(sqd, rsqd)
+    finally:
+        L.load().slio_destroy(h)

@@ -272,10 +272,10 @@ def test_ikf_update_vs_oracle(L, oracle_mod, c1, pat, maxit, mode, device_loop):
 
 
 # ------------------------------------------------------------------ edges
-@pytest.mark.parametrize("far", [0.0, None])
+@pytest.mark.parametrize("far", [None, 100.0])
 def test_edge_cases(L, far):
-    """far=0: exact everywhere (ikd-Tree semantics); default far_query_margin
-    (100 m): the query ~1.4e6 m outside the map gets no neighbours."""
+    """default far_query_margin 0: exact everywhere (ikd-Tree semantics);
+    100 m: the query ~1.4e6 m outside the map gets no neighbours."""
     lib = L.load()
     h = mk(L, n_max=1000, far=far)
     try:
@@ -291,10 +291,10 @@ def test_edge_cases(L, far):
         s = iterate(L, h, IDENT, True)
         assert s[90] == 0
         idx, sqd, sel, pl, rs = results(L, h, 4)
-        near = [0, 1, 3] if far == 0.0 else [0, 1]
+        near = [0, 1, 3] if far is None else [0, 1]
         assert (idx[near, :3] >= 0).all() and (idx[:, 3:] == -1).all()
         assert (idx[2] == -1).all() and not sel.any()
-        if far != 0.0:
+        if far is not None:
             assert (idx[3] == -1).all()
         assert list(idx[0, :3]) == [0, 1, 2]
         # capacity
