@@ -1049,18 +1049,76 @@ __device__ __forceinline__ void far_search(const CoarseView& cv, float qx, float
   };
   const float ax = range_gap(qx, g.ox, g.dx), ay = range_gap(qy, g.oy, g.dy),
               az = range_gap(qz, g.oz, g.dz);
+  // conservative squared gap from q to the cells [a0, a1] of one axis
+  auto span_gap = [&](float q, float o, int a0, int a1) {
+    const float lo = o + (float)a0 * g.h - g.tol, hi = o + (float)(a1 + 1) * g.h + g.tol;
+    const float d = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
+    return d * d;
+  };
   for (int R = 0;; ++R) {
     const int x0 = max(CX - R, 0), x1 = min(CX + R, g.dx - 1);
     const int y0 = max(CY - R, 0), y1 = min(CY + R, g.dy - 1);
     const int z0 = max(CZ - R, 0), z1 = min(CZ + R, g.dz - 1);
-    const int nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
-    const int total = nx * ny * nz;
+    // the ring's shell (cube R minus cube R-1, clipped to the grid) as up to
+    // six face rectangles: x faces over the full (y, z) span, y faces over
+    // the inner x span, z faces over the inner x and y spans.  A face whose
+    // box lies beyond the bound is skipped whole (its cells would all fail
+    // the per-cell test below).
+    const int xi0 = max(CX - R + 1, 0), xi1 = min(CX + R - 1, g.dx - 1);
+    const int yi0 = max(CY - R + 1, 0), yi1 = min(CY + R - 1, g.dy - 1);
+    const float lim_f = fminf(bound, d5);
+    int fa[6], fna[6], fb[6], fv[6], cum[7];
+    cum[0] = 0;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      const int fax = f >> 1;                              // fixed axis
+      const int C = fax == 0 ? CX : fax == 1 ? CY : CZ;
+      const int D = fax == 0 ? g.dx : fax == 1 ? g.dy : g.dz;
+      const int v = (f & 1) ? C + R : C - R;
+      const bool ok = (f == 0 || R > 0) && v >= 0 && v < D;
+      int a0, a1, b0, b1;
+      float gsum;
+      if (fax == 0) {
+        a0 = y0; a1 = y1; b0 = z0; b1 = z1;
+        gsum = (span_gap(qx, g.ox, v, v) + span_gap(qy, g.oy, a0, a1)) + span_gap(qz, g.oz, b0, b1);
+      } else if (fax == 1) {
+        a0 = xi0; a1 = xi1; b0 = z0; b1 = z1;
+        gsum = (span_gap(qx, g.ox, a0, a1) + span_gap(qy, g.oy, v, v)) + span_gap(qz, g.oz, b0, b1);
+      } else {
+        a0 = xi0; a1 = xi1; b0 = yi0; b1 = yi1;
+        gsum = (span_gap(qx, g.ox, a0, a1) + span_gap(qy, g.oy, b0, b1)) + span_gap(qz, g.oz, v, v);
+      }
+      const bool live_f = ok && a0 <= a1 && b0 <= b1 && !(gsum * 0.99999f > lim_f);
+      fa[f] = a0;
+      fb[f] = b0;
+      fv[f] = v;
+      fna[f] = live_f ? a1 - a0 + 1 : 0;
+      cum[f + 1] = cum[f] + (live_f ? (a1 - a0 + 1) * (b1 - b0 + 1) : 0);
+    }
+    const int total = cum[6];
     for (int base = 0; base < total; base += 64) {
       const int p = base + lane;
       uint32_t s = 0, k = 0;
       if (p < total) {
-        const int x = x0 + p % nx, y = y0 + (p / nx) % ny, z = z0 + p / (nx * ny);
-        if (max(abs(x - CX), max(abs(y - CY), abs(z - CZ))) == R) {
+        int f = 0;
+#pragma unroll
+        for (int j = 1; j < 6; ++j) f = p >= cum[j] ? j : f;
+        int A = 0, B = 0, V = 0, NA = 1;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (f == j) {
+            A = fa[j];
+            B = fb[j];
+            V = fv[j];
+            NA = fna[j];
+          }
+        const int l = p - (f == 0 ? 0 : f == 1 ? cum[1] : f == 2 ? cum[2] : f == 3 ? cum[3] : f == 4 ? cum[4] : cum[5]);
+        const int ua = A + l % NA, ub = B + l / NA;
+        const int fax = f >> 1;
+        const int x = fax == 0 ? V : ua;
+        const int y = fax == 0 ? ua : fax == 1 ? V : ub;
+        const int z = fax == 2 ? V : ub;
+        {
           const uint32_t c = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx + (uint32_t)x;
           const float4 lo = cv.lo[c];
           const uint32_t cnt = __float_as_uint(lo.w);
@@ -1799,17 +1857,22 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
         const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
         done = covers || (t.k[4] != kInfKey && b1 > 0.0f && d5 < (b1 * b1) * 0.99999f);
-        if (!done && t.k[4] != kInfKey) {
+        if (!done) {
           // (2) exact refinement (below): every cell of the 5x5x5 cube whose
           // conservative box gap is within the current 5th distance, minus
-          // the block already scanned (valid while that sphere stays inside
-          // the 5x5x5 cube; otherwise the general fallback takes over)
+          // the block already scanned.  When the block held fewer than 5
+          // points (e.g. a long-range ground return a metre below the ground
+          // at a slightly wrong pose: its block lies under the ground
+          // cells) or its 5th distance reaches past the cube, the whole cube
+          // is scanned (no limit); the result is exact if its 5th distance
+          // then lies within the cube's bound, else the query is deferred
+          // to the far queue (3) with that bound.
           bool covers2;
           const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, covers2);
-          if (covers2 || (b2 > 0.0f && d5 < (b2 * b2) * 0.99999f)) {
-            refine = true;
-            lim = d5 * 1.00001f;
-          }
+          refine = true;
+          lim = (t.k[4] != kInfKey && (covers2 || (b2 > 0.0f && d5 < (b2 * b2) * 0.99999f)))
+                    ? d5 * 1.00001f
+                    : __int_as_float(0x7f800000);
         }
         r = 2;
 #ifndef SLIO_NO_R2_REFINE

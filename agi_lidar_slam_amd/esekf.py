@@ -99,6 +99,9 @@ class KdTreeMap(_Handle):
     def __init__(self, device: int = 0, grid_cell: float = 1.0):
         super().__init__(_params(device, 1, 0, 1, grid_cell, 0.1, 5.0))
         self.points = np.zeros((0, 3), np.float32)
+        # bumped by every Build: a filter bound to this map re-shares it (a
+        # share holds the device map of the moment it was made)
+        self.generation = 0
 
     def Build(self, points: np.ndarray) -> None:
         pts = np.ascontiguousarray(np.asarray(points, dtype=np.float32)[:, :3])
@@ -106,6 +109,7 @@ class KdTreeMap(_Handle):
         L.check(self.lib.slio_map_upload(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0]),
                 "KdTreeMap.Build")
         self.points = pts
+        self.generation += 1
 
     def size(self) -> int:
         return int(self.points.shape[0])
@@ -138,6 +142,7 @@ class Esekf(_Handle):
         self.x_ = StateIkfom()
         self.P_ = np.eye(24)
         self._map_src = None
+        self._map_gen = -1
         self._scan_ref = None
         self.last_stats = L.SlioIkfStats()
 
@@ -156,9 +161,10 @@ class Esekf(_Handle):
 
     # --- plumbing
     def _bind(self, feats_down_body: np.ndarray, ikdtree: KdTreeMap) -> int:
-        if self._map_src is not ikdtree:
+        if self._map_src is not ikdtree or self._map_gen != ikdtree.generation:
             L.check(self.lib.slio_map_share(self.h, ikdtree.h), "map_share")
             self._map_src = ikdtree
+            self._map_gen = ikdtree.generation
         pts = np.ascontiguousarray(np.asarray(feats_down_body, dtype=np.float32)[:, :3])
         x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
         L.check(self.lib.slio_scan_upload(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0]),
@@ -183,7 +189,8 @@ class Esekf(_Handle):
                       ikdtree: KdTreeMap, Nearest_Points: dict | None,
                       extrinsic_est: bool) -> None:
         """One measurement pass (esekfom.hpp:106-227); search iff ekfom_data.converge."""
-        if feats_down_body is not self._scan_ref or self._map_src is not ikdtree:
+        if (feats_down_body is not self._scan_ref or self._map_src is not ikdtree
+                or self._map_gen != ikdtree.generation):
             self._bind(feats_down_body, ikdtree)
         pose = L.SlioPose()
         pose.rot[:] = list(self.x_.rot)

@@ -124,7 +124,11 @@ const char* slio_last_error(void);
  * results are identical either way. */
 int slio_map_upload(slio_handle h, const float* x, const float* y,
                     const float* z, int64_t n);
-/* Share src's read-only device map with h (same device; batched replay). */
+/* Share src's read-only device map with h (same device; batched replay).
+ * The share holds the map src had at the time of the call (reference-
+ * counted): a later slio_map_upload on src gives src a new map and leaves h
+ * on the old one until h shares again (esekf.Esekf re-shares when its
+ * KdTreeMap's generation changes). */
 int slio_map_share(slio_handle h, slio_handle src);
 /* Grid diagnostics: dims[3], cell edge, number of map points. */
 int slio_map_info(slio_handle h, int32_t dims[3], float* cell, int64_t* n);
