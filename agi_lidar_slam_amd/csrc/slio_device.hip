@@ -878,7 +878,6 @@ struct ScanDev {
   int64_t n;
 };
 
-struct FarQueue;
 struct PassOut {
   int32_t* nbr_idx;  // n * 5
   float* nbr_sqd;    // n * 5
@@ -886,12 +885,7 @@ struct PassOut {
   uint8_t* sel;      // n
   float* resid;      // n
   double* chunk_part;  // C * NPROD (global chunk index)
-  uint64_t* far_in;    // FarQueue (deferred queries), see far_search
-  uint64_t* far_out;
-  uint32_t* far_ready;
-  uint32_t* far_claim;
-  uint32_t* far_ctr;
-  uint32_t* far_pending;
+  uint32_t* far_ctr;   // [1]: deferred (far) queries of this pass, all chunks
 };
 
 // far_query_margin: squared distance from the query to the grid's bounding box
@@ -914,72 +908,20 @@ struct PassCfg {
   int extrinsic;
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
-  uint32_t epoch;          // this launch's tag for the far-queue ready words (never 0)
 };
 
 // ---------------------------------------------------------------- far queries
 // A query the fine grid cannot finish (its 5th neighbour lies beyond the
-// 5x5x5 fine cube, its cell lies outside the grid, or its block holds fewer
-// than 5 points) is DEFERRED: its chunk's workgroup appends it to a global
-// queue and every workgroup with deferred queries -- and every other one
-// that saw the queue non-empty -- drains the queue one query per wavefront
-// (far_search, all 64 lanes on one query).  The owner then waits for its
-// chunk's answers and runs the fit and products as usual.  The queries that
-// need this are rare and clustered in scan order (e.g. returns with no map
-// support nearby), so handling them inline on their own 2 lanes serialised
-// the wavefront that held them; spread over the chip they cost a few us.
-// Waiting is deadlock-free: a workgroup only waits for entries already
-// claimed by running wavefronts, and a far search waits for nothing but its
-// entry's ready word, which the running owner writes right after reserving.
+// 5x5x5 fine cube, or its cell lies outside the grid) is DEFERRED to the end
+// of the kNN phase of its workgroup, where the workgroup's wavefronts answer
+// the chunk's deferred queries one per wavefront (far_search, all 64 lanes
+// on one query).  Such queries are rare (returns with no map support within
+// a few metres, e.g. a scan taken from inside a building or far outside the
+// map); handled inline on their own 2 lanes they serialised the wavefront
+// that held them.  (An earlier global work queue spread them over the chip
+// but made workgroups wait on each other; this keeps every workgroup
+// independent.)
 typedef __attribute__((address_space(1))) uint32_t gu32;
-struct FarQueue {
-  uint64_t* in;       // 3 words per entry: (qx, qy), (qz, bound), (point index, 0)
-  uint64_t* out;      // 8 words per entry: the 5 sorted keys
-  uint32_t* ready;    // per entry: epoch of the launch that wrote it
-  uint32_t* claim;    // per entry: epoch of the launch in which it was claimed
-  uint32_t* ctr;      // [0] head (next ticket), [1] tail; zero between launches;
-                      // [4..7] first failed wait (kind, index, value seen, tail)
-  uint32_t* pending;  // per chunk: deferred queries not answered yet
-};
-
-// -DSLIO_FAR_TRACE (diagnostic builds only): events into mapped host memory,
-// readable by the host while a kernel runs (slio_dbg_far_trace)
-#ifdef SLIO_FAR_TRACE
-__device__ uint32_t* g_ftrace;
-#define FTRACE(a, b, c)                                                                      \
-  do {                                                                                       \
-    if ((threadIdx.x & 63) == 0 && g_ftrace) {                                               \
-      const uint32_t k_ = __hip_atomic_fetch_add(g_ftrace, 1u, __ATOMIC_RELAXED,            \
-                                                 __HIP_MEMORY_SCOPE_SYSTEM);                 \
-      if (k_ < 4095) {                                                                       \
-        uint32_t* r_ = g_ftrace + 4 + 4 * k_;                                                \
-        __hip_atomic_store(r_ + 0, (blockIdx.x << 8) | (threadIdx.x >> 6), __ATOMIC_RELAXED, \
-                           __HIP_MEMORY_SCOPE_SYSTEM);                                       \
-        __hip_atomic_store(r_ + 1, (uint32_t)(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-        __hip_atomic_store(r_ + 2, (uint32_t)(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-        __hip_atomic_store(r_ + 3, (uint32_t)(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-      }                                                                                      \
-    }                                                                                        \
-  } while (0)
-#else
-#define FTRACE(a, b, c) \
-  do {                  \
-  } while (0)
-#endif
-
-// Every wait on another workgroup is bounded: ~2^21 polls with s_sleep (well
-// over 100 ms) and the wait gives up, records what it waited for and the
-// pass reports SLIO_EDEVICE (slio_far_queries) instead of hanging the GPU.
-constexpr uint32_t kSpinLimit = 1u << 21;
-__device__ __noinline__ void far_wait_failed(uint32_t* ctr, uint32_t kind, uint32_t idx, uint32_t seen) {
-  if (__hip_atomic_fetch_add((gu32*)(ctr + 4), kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-    __hip_atomic_store((gu32*)(ctr + 5), idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu32*)(ctr + 6), seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu32*)(ctr + 7),
-                       __hip_atomic_load((gu32*)(ctr + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wave_fence() {
@@ -987,21 +929,11 @@ __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
-typedef __attribute__((address_space(1))) uint64_t gu64;
-__device__ __forceinline__ void st_sc1_u64(uint64_t* p, uint64_t v) {
-  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
-  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void st_sc1_u32(uint32_t* p, uint32_t v) {
   __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
   return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t pack2f(float a, float b) {
-  return ((uint64_t)__float_as_uint(b) << 32) | (uint64_t)__float_as_uint(a);
 }
 
 // exclusive prefix sum over the wavefront's 64 lanes; total to every lane
@@ -1189,83 +1121,6 @@ __device__ __forceinline__ void far_search(const CoarseView& cv, float qx, float
   }
 #pragma unroll
   for (int j = 0; j < 5; ++j) t.k[j] = __shfl(t.k[j], 0, 64);
-}
-
-// Answer far-queue entry e (claimed): wait for its ready word, search,
-// publish the 5 keys write-through and drained, count it off its chunk.
-template <int U>
-__device__ __forceinline__ void far_answer(const CoarseView& cv, const FarQueue& fq, uint32_t epoch,
-                                           uint32_t e, uint32_t* pre, uint32_t* beg) {
-  const int lane = threadIdx.x & 63;
-  FTRACE(10, e, 0);
-  if (lane == 0) {
-    uint32_t it = 0, v;
-    while ((v = ld_sc1_u32(fq.ready + e)) != epoch) {
-      if (++it > kSpinLimit) {
-        far_wait_failed(fq.ctr, 1u, e, v);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  const uint64_t w0 = ld_sc1_u64(fq.in + 3 * (size_t)e), w1 = ld_sc1_u64(fq.in + 3 * (size_t)e + 1),
-                 w2 = ld_sc1_u64(fq.in + 3 * (size_t)e + 2);
-  const float qx = __uint_as_float((uint32_t)w0), qy = __uint_as_float((uint32_t)(w0 >> 32));
-  const float qz = __uint_as_float((uint32_t)w1), bound = __uint_as_float((uint32_t)(w1 >> 32));
-  const uint32_t i = (uint32_t)w2;
-  Top5 t;
-  FTRACE(11, e, i);
-  far_search<U>(cv, qx, qy, qz, bound, pre, beg, t);
-  FTRACE(12, e, (uint32_t)(t.k[4] >> 32));
-  uint64_t mine = t.k[0];
-#pragma unroll
-  for (int j = 1; j < 5; ++j) mine = (lane == j) ? t.k[j] : mine;
-  if (lane < 5) st_sc1_u64(fq.out + 8 * (size_t)e + lane, mine);
-  drain_stores();
-  if (lane == 0)
-    __hip_atomic_fetch_add((gu32*)(fq.pending + i / SLIO_CHUNK), 0xFFFFFFFFu, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Claim entry e for this wavefront: one exchange on its claim word (the
-// owner's leftover pass and a ticket holder may both try).
-__device__ __forceinline__ bool far_claim(const FarQueue& fq, uint32_t epoch, uint32_t e) {
-  uint32_t prev = 0;
-  if ((threadIdx.x & 63) == 0)
-    prev = __hip_atomic_exchange((gu32*)(fq.claim + e), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __shfl(prev, 0, 64) != epoch;
-}
-
-// One wavefront drains the far queue by tickets: one fetch-and-add on the
-// head per entry (no compare-and-swap retries: thousands of wavefronts
-// retrying on one word cost milliseconds); a ticket past the tail ends the
-// loop.  Entries appended after the head overtook the tail get no ticket:
-// their owner answers them itself (far_own_leftovers).
-template <int U>
-__device__ __forceinline__ void far_worker(const CoarseView& cv, const FarQueue& fq, uint32_t epoch,
-                                           uint32_t* pre, uint32_t* beg) {
-  const int lane = threadIdx.x & 63;
-  for (;;) {
-    uint32_t e = 0xFFFFFFFFu;
-    if (lane == 0) {
-      const uint32_t tk = __hip_atomic_fetch_add((gu32*)fq.ctr, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-      if (tk < ld_sc1_u32(fq.ctr + 1)) e = tk;
-    }
-    e = __shfl(e, 0, 64);
-    FTRACE(20, e, 0);
-    if (e == 0xFFFFFFFFu) break;
-    if (far_claim(fq, epoch, e)) far_answer<U>(cv, fq, epoch, e, pre, beg);
-  }
-}
-
-// The owner's own entries [base, base + n) that no ticket holder claimed,
-// wavefront w of the workgroup taking entries w, w + waves, ...
-template <int U, int NT>
-__device__ __forceinline__ void far_own_leftovers(const CoarseView& cv, const FarQueue& fq, uint32_t epoch,
-                                                  uint32_t base, int n, uint32_t* pre, uint32_t* beg) {
-  for (int k = threadIdx.x >> 6; k < n; k += NT / 64)
-    if (far_claim(fq, epoch, base + k)) far_answer<U>(cv, fq, epoch, base + k, pre, beg);
 }
 
 __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
@@ -1789,11 +1644,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __shared__ float4 qw[SLIO_CHUNK];
   // deferred (far) queries of this chunk and the far workers' scratch
   __shared__ int far_cnt;
-  __shared__ uint32_t far_base;
   __shared__ float4 far_q[SLIO_CHUNK];
   __shared__ uint8_t far_slot[SLIO_CHUNK];
   __shared__ uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
-  const FarQueue fq{out.far_in, out.far_out, out.far_ready, out.far_claim, out.far_ctr, out.far_pending};
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
   const int tid = threadIdx.x;
   const int sub = tid & (LPQ - 1);
@@ -1869,7 +1722,11 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           // to the far queue (3) with that bound.
           bool covers2;
           const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, covers2);
+#ifdef SLIO_NO_STARVED_REFINE
+          refine = t.k[4] != kInfKey && (covers2 || (b2 > 0.0f && d5 < (b2 * b2) * 0.99999f));
+#else
           refine = true;
+#endif
           lim = (t.k[4] != kInfKey && (covers2 || (b2 > 0.0f && d5 < (b2 * b2) * 0.99999f)))
                     ? d5 * 1.00001f
                     : __int_as_float(0x7f800000);
@@ -2016,66 +1873,32 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __syncthreads();
   if (tid == 0) STAMP(1);
   const int nfar = far_cnt;
-  uint32_t tail_peek = 0;
-  FTRACE(1, nfar, chunk);
   if (nfar > 0) {
-    // publish this chunk's deferred queries: the pending count first (a
-    // worker may answer as soon as an entry is ready), then the entries
-    if (tid == 0) {
-      st_sc1_u32(fq.pending + chunk, (uint32_t)nfar);
-      drain_stores();
-      far_base = __hip_atomic_fetch_add((gu32*)(fq.ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (tid < nfar) {
-      const size_t e = far_base + tid;
-      const float4 q = far_q[tid];
-      st_sc1_u64(fq.in + 3 * e, pack2f(q.x, q.y));
-      st_sc1_u64(fq.in + 3 * e + 1, pack2f(q.z, q.w));
-      st_sc1_u64(fq.in + 3 * e + 2, (uint64_t)(chunk * SLIO_CHUNK + far_slot[tid]));
-      drain_stores();
-      st_sc1_u32(fq.ready + e, cfg.epoch);
-    }
-    // help drain the queue, answer what is left of this chunk's entries,
-    // then wait for all of this chunk's answers
-    far_worker<4>(map.cl, fq, cfg.epoch, far_pre[tid >> 6], far_beg[tid >> 6]);
-    far_own_leftovers<4, NT>(map.cl, fq, cfg.epoch, far_base, nfar, far_pre[tid >> 6], far_beg[tid >> 6]);
-    __syncthreads();
-    FTRACE(30, far_base, nfar);
-    if (tid == 0) {
-      uint32_t it = 0, v;
-      while ((v = ld_sc1_u32(fq.pending + chunk)) != 0u) {
-        if (++it > kSpinLimit) {
-          far_wait_failed(fq.ctr, 2u, (uint32_t)chunk, v);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      drain_stores();
-    }
-    __syncthreads();
-    if (tid < nfar) {
-      const size_t e = far_base + tid;
-      const int slot = far_slot[tid];
+    // (3) this chunk's deferred queries, one per wavefront on the coarse
+    // level (far_search); no other workgroup is involved or waited for
+    if (tid == 0)
+      __hip_atomic_fetch_add((gu32*)(out.far_ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    const int lane = tid & 63;
+    for (int k = tid >> 6; k < nfar; k += NT / 64) {
+      const float4 q = far_q[k];
+      Top5 tf;
+      far_search<4>(map.cl, q.x, q.y, q.z, q.w, far_pre[tid >> 6], far_beg[tid >> 6], tf);
+      const int slot = far_slot[k];
       const int64_t i = chunk * SLIO_CHUNK + slot;
-      uint64_t k4 = kInfKey;
+      uint64_t mk = tf.k[0];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const uint64_t mk = ld_sc1_u64(fq.out + 8 * e + j);
-        out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
-                                                 : __uint_as_float((uint32_t)(mk >> 32));
-        nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
-        k4 = mk;
+      for (int j = 1; j < 5; ++j) mk = (lane == j) ? tf.k[j] : mk;
+      if (lane < 5) {
+        out.nbr_sqd[i * 5 + lane] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+                                                    : __uint_as_float((uint32_t)(mk >> 32));
+        nb_pos[slot][lane] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
       }
-      nb_d5[slot] = (k4 != kInfKey) ? __uint_as_float((uint32_t)(k4 >> 32)) : __int_as_float(0x7f800000);
+      if (lane == 0)
+        nb_d5[slot] = (tf.k[4] != kInfKey) ? __uint_as_float((uint32_t)(tf.k[4] >> 32))
+                                           : __int_as_float(0x7f800000);
     }
     __syncthreads();
-  } else if (tid == 0) {
-    // a look at the queue, in flight behind the fit phase's loads: if
-    // other chunks deferred queries, this workgroup helps once it is done
-    tail_peek = ld_sc1_u32(fq.ctr + 1);
   }
 
   // ---------------- phase 2: plane fit, residual gate, Jacobian row
@@ -2140,21 +1963,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __syncthreads();
   if (tid == 0) STAMP(2);
   // ---------------- phase 3: fixed-order products
-  FTRACE(40, 0, 0);
   chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
   if (tid == 0) STAMP(3);
-  if (nfar == 0) {
-    // about one helping wavefront per queued query: every stride-th
-    // workgroup joins (all of them when the queue is long)
-    __shared__ uint32_t help;
-    if (tid == 0) {
-      const uint32_t waves = gridDim.x * (NT / 64);
-      const uint32_t stride = tail_peek ? max(1u, waves / tail_peek) : 0u;
-      help = tail_peek && (blockIdx.x % stride) == 0;
-    }
-    __syncthreads();
-    if (help) far_worker<4>(map.cl, fq, cfg.epoch, far_pre[tid >> 6], far_beg[tid >> 6]);
-  }
 }
 
 // Non-search pass: reuse neighbours/plane/selection (esekfom.hpp:138-150 with
@@ -2333,12 +2143,6 @@ struct Ctx {
   float* resid = nullptr;
   double* chunk_part = nullptr;
   // far queue (deferred queries, see far_search)
-  uint64_t* far_in = nullptr;
-  uint64_t* far_out = nullptr;
-  uint32_t* far_ready = nullptr;
-  uint32_t* far_claim = nullptr;
-  uint32_t* far_pending = nullptr;
-  uint32_t far_epoch = 0;
   double* d_super = nullptr;
   double* d_super_own = nullptr;
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
@@ -2438,13 +2242,6 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->sel);
   (void)hipFree(c->resid);
   (void)hipFree(c->chunk_part);
-  (void)hipFree(c->far_in);
-  (void)hipFree(c->far_out);
-  (void)hipFree(c->far_ready);
-  (void)hipFree(c->far_claim);
-  (void)hipFree(c->far_pending);
-  c->far_in = c->far_out = nullptr;
-  c->far_ready = c->far_claim = c->far_pending = nullptr;
   c->bx = c->by = c->bz = nullptr;
   c->nbr_idx = nullptr;
   c->nbr_sqd = nullptr;
@@ -2544,10 +2341,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   PassOut o{c.nbr_idx,  c.nbr_sqd,   c.plane,     c.sel,     c.resid,
-            c.chunk_part, c.far_in, c.far_out, c.far_ready, c.far_claim, c.count + 4,
-            c.far_pending};
-  if (++c.far_epoch == 0) c.far_epoch = 1;  // ready words are 0 when allocated
-  cfg.epoch = c.far_epoch;
+            c.chunk_part, c.count + 4};
   ScanDev s{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
@@ -3057,11 +2851,7 @@ int slio_scan_upload(slio_handle h, const float* x, const float* y, const float*
         (e = hipMalloc(&c.bz, 4 * cap)) || (e = hipMalloc(&c.nbr_idx, 4 * 5 * cap)) ||
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
-        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
-        (e = hipMalloc(&c.far_in, 8 * 3 * cap)) || (e = hipMalloc(&c.far_out, 8 * 8 * cap)) ||
-        (e = hipMalloc(&c.far_ready, 4 * cap)) || (e = hipMalloc(&c.far_claim, 4 * cap)) ||
-        (e = hipMalloc(&c.far_pending, 4 * capc)) || (e = hipMemset(c.far_ready, 0, 4 * cap)) ||
-        (e = hipMemset(c.far_claim, 0, 4 * cap)) || (e = hipMemset(c.far_pending, 0, 4 * capc))) {
+        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {
       free_scan(&c);
       set_error(std::string("slio_scan_upload: hipMalloc: ") + hipGetErrorString(e));
       return SLIO_ENOMEM;
@@ -3288,15 +3078,6 @@ int slio_far_queries(slio_handle h, int64_t* n) {
   SLIO_HIP(hipStreamSynchronize(h->c.stream));
   SLIO_HIP(hipMemcpy(v, h->c.count, sizeof(v), hipMemcpyDeviceToHost));
   if (n) *n = v[6];
-  if (v[8]) {
-    // a bounded wait of the far queue gave up (count + 8: FarQueue::ctr[4..7])
-    char msg[160];
-    std::snprintf(msg, sizeof msg, "far queue wait timed out: kind %u index %u seen %u tail %u", v[8],
-                  v[9], v[10], v[11]);
-    set_error(msg);
-    SLIO_HIP(hipMemset(h->c.count + 8, 0, 4 * sizeof(uint32_t)));
-    return SLIO_EDEVICE;
-  }
   return SLIO_OK;
 }
 
@@ -3326,13 +3107,6 @@ int slio_get_residuals(slio_handle h, float* pd2) {
 
 }  // extern "C"
 
-#ifdef SLIO_FAR_TRACE
-extern "C" int slio_dbg_far_trace(void* host_mapped) {
-  void* d = nullptr;
-  if (host_mapped && hipHostGetDevicePointer(&d, host_mapped, 0) != hipSuccess) return -3;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace), &d, sizeof(d)) == hipSuccess ? 0 : -3;
-}
-#endif
 
 #ifdef SLIO_SOLVE_STAMP
 extern "C" int slio_dbg_solve_stamps(unsigned long long* out) {

@@ -173,9 +173,9 @@ int slio_iterate(slio_handle h, const slio_pose* x, int do_search,
 int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel);
 /* Number of scan points of the last pass (of this handle's shard) whose
  * 5-NN search did not finish on the fine grid -- 5th neighbour beyond the
- * 5x5x5 fine-cell cube, query cell outside the grid, or fewer than 5 points
- * in the 3x3x3 block -- and went to the coarse-level far search instead
- * (diagnostic; synchronises the stream). */
+ * 5x5x5 fine-cell cube, or query cell more than 2 cells outside the grid --
+ * and went to the coarse-level far search instead (diagnostic; synchronises
+ * the stream). */
 int slio_far_queries(slio_handle h, int64_t* n);
 /* Plane (a, b, c, d) per point; (a,b,c) unit normal, d offset, or NaNs where
  * esti_plane failed or the point was gated out before the fit. */

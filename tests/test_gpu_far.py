@@ -1,8 +1,8 @@
-"""GPU parity of the far-query path (coarse-level search through the far queue).
+"""GPU parity of the far-query path (coarse-level search).
 
 A scan point whose 5-NN the fine grid cannot finish -- 5th neighbour beyond
-the 5x5x5 fine cube, query cell outside the grid, fewer than 5 points in the
-3x3x3 block -- is deferred to the far queue and answered by a whole
+the 5x5x5 fine cube, query cell more than 2 cells outside the grid -- is
+deferred to the end of its workgroup's kNN phase and answered by a whole
 wavefront on the coarse level (slio_device.hip, far_search).  ikd-Tree has no
 such split (ikd_Tree.cpp:960-1101 visits the tree the same way for every
 query), so the bar is the same as for every other query: indices and squared
@@ -46,7 +46,7 @@ def test_far_queries_inside_building_bitexact(L, oracle_mod, inside, monkeypatch
                                               blockrows):
     """Every query of a scan with unsupported returns, over cell edges, lanes per
     query, the sphere-first search and the 9-run path: bit-exact, and the far
-    queue was used."""
+    path was used."""
     if not blockrows:
         monkeypatch.setenv("SLIO_NO_BLOCK_ROWS", "1")
     mp, fr, T = inside
@@ -69,7 +69,7 @@ def test_far_queries_inside_building_bitexact(L, oracle_mod, inside, monkeypatch
         assert nfar >= must
         if cell <= 0.75:
             assert must > 0
-        # the queue is reset between launches: a second pass gives the same answer
+        # the far counter is reset between launches: a second pass gives the same answer
         iterate(L, h, st, True)
         assert far_count(L, h) == nfar
         idx2, sqd2, *_ = results(L, h, q.shape[0])
@@ -80,8 +80,8 @@ def test_far_queries_inside_building_bitexact(L, oracle_mod, inside, monkeypatch
 
 def test_far_queue_random_queries(L, oracle_mod, inside):
     """Queries anywhere: in empty air inside the grid, just outside it, km away
-    (the old far_query_margin cut is off by default).  Most are deferred; the
-    queue is drained by every workgroup; results are bit-exact."""
+    (the old far_query_margin cut is off by default).  Most are deferred;
+    results are bit-exact."""
     mp, _, T = inside
     rng = np.random.default_rng(5)
     lo, hi = mp.min(0), mp.max(0)
