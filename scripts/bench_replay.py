@@ -8,9 +8,13 @@ replica runs `slio_ikf_update_device` (the whole `update_iterated_dyn_share_modi
 esekfom.hpp:270-346) from its own host thread; ctypes drops the GIL for the call,
 so the R updates overlap on the device. No collective: replicas are independent.
 
+Every replica runs a DIFFERENT scan of the same scene (own seed: own pose,
+own returns), as replaying a bag would; a replica's map reads therefore do
+not coincide with the others' in L2 / MALL.
+
 value = IKF iterations of all replicas / wall time of the timed region. Every
-replica's result is checked bitwise against the same scan run alone first
-(identical inputs => identical x and P), so concurrency cannot change results.
+replica's result is checked bitwise against its own scan run alone first, so
+concurrency cannot change results.
 
   python scripts/bench_replay.py --replicas 4 --steps 50
 """
@@ -43,10 +47,34 @@ def main():
     from agi_lidar_slam_amd import _lib as L, synth
 
     lib = L.load()
-    mp, fr = synth.make_problem(args.map_points, args.scan_points, pattern="avia",
-                                cache_dir=args.cache_dir)
-    fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
     R = args.replicas
+    seed = 20261015
+    t0 = time.time()
+    mp, _ = synth.make_problem(args.map_points, args.scan_points, pattern="avia", seed=seed,
+                               cache_dir=args.cache_dir)
+    scene = synth.make_scene(seed, args.map_points)
+    frames = []
+    next_seed = seed
+    for r in range(R):
+        fn = os.path.join(args.cache_dir, f"replay2_{args.map_points}_{args.scan_points}_{r}.npz")
+        if os.path.exists(fn):
+            z = np.load(fn)
+            fr = synth.Frame(body=z["body"], gt_rot=z["gt_rot"], gt_pos=z["gt_pos"],
+                             init_rot=z["init_rot"], init_pos=z["init_pos"])
+        else:
+            while True:   # a pose facing a wall may not yield enough voxel-unique returns
+                next_seed += 17
+                try:
+                    fr = synth.make_frame(scene, next_seed, args.scan_points, "avia")
+                    break
+                except ValueError:
+                    continue
+            os.makedirs(args.cache_dir, exist_ok=True)
+            np.savez(fn, body=fr.body, gt_rot=fr.gt_rot, gt_pos=fr.gt_pos, init_rot=fr.init_rot,
+                     init_pos=fr.init_pos)
+        fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
+        frames.append(fr)
+    print(f"[replay] map {mp.shape[0]} + {R} scans in {time.time() - t0:.1f}s", file=sys.stderr)
 
     handles = []
     for r in range(R):
@@ -61,43 +89,46 @@ def main():
     L.check(lib.slio_map_upload(handles[0], L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")
     for h in handles[1:]:
         L.check(lib.slio_map_share(h, handles[0]), "share")
-    bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
-    for h in handles:
+    for h, fr in zip(handles, frames):
+        bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
         L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]),
                 "scan")
 
-    st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9),
-                          [0, 0, -9.81]])
     P0 = np.eye(24) * 1e-2
-    xs0 = L.SlioState()
-    xs0.pos[:] = list(st0[0:3])
-    xs0.rot[:] = list(st0[3:7])
-    xs0.rli[:] = list(st0[7:11])
-    xs0.tli[:] = list(st0[11:14])
-    xs0.grav[:] = list(st0[23:26])
+
+    def prior(fr):
+        xs0 = L.SlioState()
+        xs0.pos[:] = list(fr.init_pos)
+        xs0.rot[:] = list(fr.init_rot)
+        xs0.rli[:] = [1.0, 0.0, 0.0, 0.0]
+        xs0.tli[:] = list(synth.AVIA_T_LI)
+        xs0.grav[:] = [0.0, 0.0, -9.81]
+        return xs0
     reduce_cb = L.ALLREDUCE_FN()
 
     class Rep:
-        def __init__(self, h):
+        def __init__(self, h, fr):
             self.h = h
+            self.xs0 = prior(fr)
             self.xs = L.SlioState()
             self.P = np.empty_like(P0)
             self.stats = L.SlioIkfStats()
             self.err = None
 
         def step(self):
-            C.memmove(C.addressof(self.xs), C.addressof(xs0), C.sizeof(self.xs))
+            C.memmove(C.addressof(self.xs), C.addressof(self.xs0), C.sizeof(self.xs))
             self.P[...] = P0
             rc = lib.slio_ikf_update_device(self.h, C.byref(self.xs), L.dptr(self.P), 0.001,
                                             args.iters, 0, L.SLIO_MODE_FIXED, reduce_cb, None,
                                             C.byref(self.stats))
             L.check(rc, "ikf")
 
-    reps = [Rep(h) for h in handles]
-    # reference result: replica 0 alone
-    reps[0].step()
-    ref_x = bytes(memoryview(reps[0].xs))
-    ref_P = reps[0].P.copy()
+    reps = [Rep(h, fr) for h, fr in zip(handles, frames)]
+    # reference results: every replica alone, one after the other
+    ref = []
+    for rep in reps:
+        rep.step()
+        ref.append((bytes(memoryview(rep.xs)), rep.P.copy()))
     # single-replica rate (same harness) for the comparison line
     for _ in range(args.warmup):
         reps[0].step()
@@ -126,22 +157,25 @@ def main():
     th = [threading.Thread(target=run, args=(rep,)) for rep in reps]
     for t in th:
         t.start()
-    go.wait()
-    t0 = time.perf_counter()
-    go.wait()
+    try:
+        go.wait()
+        t0 = time.perf_counter()
+        go.wait()
+    except threading.BrokenBarrierError:
+        t0 = time.perf_counter()   # a replica failed: join, then report its error
     for t in th:
         t.join()
     el = time.perf_counter() - t0
     for rep in reps:
         if rep.err:
             raise rep.err
-    same = all(bytes(memoryview(rep.xs)) == ref_x and np.array_equal(rep.P, ref_P)
-               for rep in reps)
+    same = all(bytes(memoryview(rep.xs)) == rx and np.array_equal(rep.P, rP)
+               for rep, (rx, rP) in zip(reps, ref))
     for h in reversed(handles):
         lib.slio_destroy(h)
     total = R * args.steps * args.iters / el
     print(json.dumps({
-        "metric": "IKF iterations/sec, batched replay (C5), 100k-pt scans vs shared map",
+        "metric": "IKF iterations/sec, batched replay (C5), distinct 100k-pt scans vs shared map",
         "value": total, "unit": "IKF iterations/s", "replicas": R, "steps": args.steps,
         "map_points": args.map_points, "scan_points": args.scan_points,
         "single_replica_value": single, "speedup_vs_single": total / single,

@@ -303,3 +303,75 @@ def test_esekf_follows_map_rebuild(L, oracle_mod):
     finally:
         kf.close()
         kd.close()
+
+
+def test_c5_50M_map_exact_and_replay(L, oracle_mod):
+    """C5's 50M-point map: a 100k scan's pass is bit-exact vs the oracle on a
+    4000-query sample (plus sortedness / selection properties over the whole
+    scan), and 8 replicas with distinct scans on the shared 50M map, run
+    concurrently, each equal their own run alone."""
+    from agi_lidar_slam_amd import synth
+    lib = L.load()
+    seed = 20261015
+    mp, fr = synth.make_problem(50_000_000, 100_000, pattern="avia", seed=seed,
+                                cache_dir="/tmp/slio_cache")
+    fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
+    st = state_of(fr)
+    T = oracle_mod.Tree(mp)
+    base = mk(L, cell=C2_CELL)
+    hs = []
+    try:
+        upload_map(L, base, mp)
+        upload_scan(L, base, fr.body)
+        s = iterate(L, base, st, True)
+        idx, sqd, sel, pl, rs = results(L, base, fr.body.shape[0])
+        assert (np.diff(sqd, axis=1) >= 0).all() and (idx >= 0).all()
+        assert int(s[90]) == int(sel.sum()) and sel.mean() > 0.5
+        pick = np.random.default_rng(1).choice(fr.body.shape[0], 4000, replace=False)
+        q = oracle_mod.body_to_world(st, fr.body)[pick]
+        ridx, rsqd = T.knn(q, 5)
+        np.testing.assert_array_equal(idx[pick], ridx)
+        np.testing.assert_array_equal(sqd[pick], rsqd)
+        # replay: 8 distinct 50k-point scans of the same scene
+        scene = synth.make_scene(seed, 50_000_000)
+        frames = [synth.make_frame(scene, seed + 17 * k, 50_000, "avia") for k in range(8)]
+        hs = [mk(L, n_max=50_000, cell=C2_CELL) for _ in frames]
+        for h, f in zip(hs, frames):
+            L.check(lib.slio_map_share(h, base), "share")
+            assert upload_scan(L, h, f.body) == 0
+        cb = L.ALLREDUCE_FN()
+
+        def run(h, f, out, reps):
+            for _ in range(reps):
+                xs = slio_state(state_of(f))
+                P = np.eye(24) * 1e-2
+                stt = L.SlioIkfStats()
+                rc = lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, 4, 0,
+                                                L.SLIO_MODE_FIXED, cb, None, C.byref(stt))
+                out.append((rc, state_array(xs), P.copy()))
+
+        alone = []
+        for h, f in zip(hs, frames):
+            o = []
+            run(h, f, o, 1)
+            assert o[0][0] == 0, lib.slio_last_error()
+            alone.append(o[0])
+        outs = [[] for _ in hs]
+        th = [threading.Thread(target=run, args=(h, f, o, 2)) for h, f, o in zip(hs, frames, outs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for o, ref in zip(outs, alone):
+            assert len(o) == 2
+            for rc, x, P in o:
+                assert rc == 0
+                np.testing.assert_array_equal(x, ref[1])
+                np.testing.assert_array_equal(P, ref[2])
+        # the replicas converge near their own ground truth
+        for f, ref in zip(frames, alone):
+            assert np.abs(ref[1][0:3] - f.gt_pos).max() < 0.05
+    finally:
+        for h in reversed(hs):
+            lib.slio_destroy(h)
+        lib.slio_destroy(base)
