@@ -59,6 +59,7 @@ def main():
         fn = os.path.join(args.cache_dir, f"replay2_{args.map_points}_{args.scan_points}_{r}.npz")
         if os.path.exists(fn):
             z = np.load(fn)
+            next_seed = int(z["seed"])
             fr = synth.Frame(body=z["body"], gt_rot=z["gt_rot"], gt_pos=z["gt_pos"],
                              init_rot=z["init_rot"], init_pos=z["init_pos"])
         else:
@@ -70,7 +71,7 @@ def main():
                 except ValueError:
                     continue
             os.makedirs(args.cache_dir, exist_ok=True)
-            np.savez(fn, body=fr.body, gt_rot=fr.gt_rot, gt_pos=fr.gt_pos, init_rot=fr.init_rot,
+            np.savez(fn, seed=next_seed, body=fr.body, gt_rot=fr.gt_rot, gt_pos=fr.gt_pos, init_rot=fr.init_rot,
                      init_pos=fr.init_pos)
         fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
         frames.append(fr)
