@@ -180,7 +180,7 @@ def main():
     ap.add_argument("--scan-order", choices=["voxel", "capture"], default="voxel",
                     help="voxel: pcl::VoxelGrid output order, as feats_down_body reaches "
                          "h_share_model in the reference; capture: rosette firing order")
-    ap.add_argument("--cpu-scans", type=int, default=2)
+    ap.add_argument("--cpu-scans", type=int, default=12)
     ap.add_argument("--cpu-threads", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -341,15 +341,25 @@ def main():
             O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=1,
                          reference_gain=1, threads=args.cpu_threads)
         cel = time.perf_counter() - t0
+        # the same sample on every core this process may use (the reference's
+        # MP_PROC_NUM is 3; SURVEY.md 8(d) asks for both)
+        all_cores = len(os.sched_getaffinity(0))
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_scans):
+            O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=1,
+                         reference_gain=1, threads=all_cores)
+        cel_all = time.perf_counter() - t0
         cpu = {
             "value": args.cpu_scans * args.iters / cel,
             "unit": "IKF iterations/s",
+            "all_cores": {"value": args.cpu_scans * args.iters / cel_all, "cores": all_cores},
             "cores": args.cpu_threads,
             "kind": "port",
             "sample": (f"{args.cpu_scans} scan updates x {args.iters} IKF iterations (kNN every "
                        f"iteration, 24 x m gain formed as esekfom.hpp:314), "
                        f"{args.scan_points}-pt scan vs {args.map_points}-pt map, "
-                       f"{args.cpu_threads} OpenMP threads (MP_PROC_NUM); host {cpu_model()}, "
+                       f"{args.cpu_threads} OpenMP threads (MP_PROC_NUM), and all_cores = every "
+                       f"core in this process's affinity set; host {cpu_model()}, "
                        f"nproc {os.cpu_count()}"),
         }
 
