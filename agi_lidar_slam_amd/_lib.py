@@ -162,6 +162,11 @@ SIGNATURES = {
     "slio_map_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
     "slio_map_share": (C.c_int, [_P, _P]),
     "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),
+    "slio_map_add_points": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_int, C.c_float, _I64P]),
+    "slio_map_delete_boxes": (C.c_int, [_P, _FP, C.c_int64, _I64P]),
+    "slio_map_incremental": (C.c_int, [_P, C.POINTER(SlioState), C.c_double, C.c_int, _I64P]),
+    "slio_map_download": (C.c_int, [_P, _FP, _FP, _FP, C.POINTER(C.c_uint32), C.c_int64, _I64P]),
+    "slio_fov_segment": (C.c_int, [_DP, _FP, _FP, _IP, C.c_double, C.c_float, _FP, _IP]),
     "slio_scan_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
     "slio_shard_range": (C.c_int, [_P, _I64P, _I64P]),
     "slio_iterate_async": (C.c_int, [_P, C.POINTER(SlioPose), C.c_int, C.c_int, C.POINTER(_DP)]),
@@ -271,3 +276,7 @@ def u8ptr(a: np.ndarray):
 
 def u16ptr(a: np.ndarray):
     return a.ctypes.data_as(_U16P)
+
+
+def i64ptr(a: np.ndarray):
+    return a.ctypes.data_as(_I64P)

@@ -143,15 +143,39 @@ struct MapDev {
   uint32_t* bstart = nullptr;     // ncells + 1 prefix offsets into blk
   int64_t nblk = 0;
   int device = 0;
+  // map maintenance (slio_map_add_points / slio_map_delete_boxes /
+  // slio_map_incremental): deletions are flags on pts positions, additions
+  // wait in add4 (id order) until the next rebuild of the index (map_refresh,
+  // before the next search pass or download).  Point ids: 0..n-1 for the
+  // upload, then the next ids for every surviving added point.
+  uint8_t* keep = nullptr;        // n: 0 = deleted since the last build
+  float4* add4 = nullptr;         // x, y, z, bits(id)
+  uint8_t* akeep = nullptr;
+  int64_t nadd = 0, add_cap = 0;
+  uint32_t next_id = 0;
+  uint64_t version = 1;           // bumped by every rebuild (positions change)
+  bool dirty = false;
+  float cell0 = 1.0f;             // requested grid cell and cell budget (slio_params)
+  int64_t max_cells = 0;
+  void free_index() {
+    for (void* q : {(void*)pts, (void*)start, (void*)blk, (void*)bstart, (void*)cpts, (void*)cstart,
+                    (void*)clo, (void*)chi, (void*)keep})
+      if (q) (void)hipFree(q);
+    pts = nullptr;
+    start = nullptr;
+    blk = nullptr;
+    bstart = nullptr;
+    cpts = nullptr;
+    cstart = nullptr;
+    clo = nullptr;
+    chi = nullptr;
+    keep = nullptr;
+    n = ncells = nccells = nblk = 0;
+  }
   ~MapDev() {
-    if (pts) (void)hipFree(pts);
-    if (start) (void)hipFree(start);
-    if (blk) (void)hipFree(blk);
-    if (bstart) (void)hipFree(bstart);
-    if (cpts) (void)hipFree(cpts);
-    if (cstart) (void)hipFree(cstart);
-    if (clo) (void)hipFree(clo);
-    if (chi) (void)hipFree(chi);
+    free_index();
+    if (add4) (void)hipFree(add4);
+    if (akeep) (void)hipFree(akeep);
   }
 };
 
@@ -879,7 +903,8 @@ struct ScanDev {
 };
 
 struct PassOut {
-  int32_t* nbr_idx;  // n * 5
+  int32_t* nbr_idx;  // n * 5  (map point ids)
+  uint32_t* nbr_pos; // n * 5  (positions in the cell-sorted pts, for map_incremental)
   float* nbr_sqd;    // n * 5
   float4* plane;     // n
   uint8_t* sel;      // n
@@ -1935,6 +1960,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb[j][1] = c.y;
         nb[j][2] = c.z;
         out.nbr_idx[i * 5 + j] = (int32_t)__float_as_uint(c.w);
+        out.nbr_pos[i * 5 + j] = ps;
       }
       if (sel) {
         float pl[4];
@@ -2137,6 +2163,8 @@ struct Ctx {
   float* by = nullptr;
   float* bz = nullptr;
   int32_t* nbr_idx = nullptr;
+  uint32_t* nbr_pos = nullptr;
+  uint64_t search_version = 0;  // map version the last search pass ran on
   float* nbr_sqd = nullptr;
   float4* plane = nullptr;
   uint8_t* sel = nullptr;
@@ -2237,6 +2265,8 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->by);
   (void)hipFree(c->bz);
   (void)hipFree(c->nbr_idx);
+  (void)hipFree(c->nbr_pos);
+  c->nbr_pos = nullptr;
   (void)hipFree(c->nbr_sqd);
   (void)hipFree(c->plane);
   (void)hipFree(c->sel);
@@ -2304,6 +2334,7 @@ struct SolveArgs {
 };
 
 static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa);
+static int map_refresh(Ctx& c, bool adds_only = false);
 
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
                         int extrinsic_est, const SolveArgs* sa = nullptr,
@@ -2340,7 +2371,8 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_begin = c0;
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
-  PassOut o{c.nbr_idx,  c.nbr_sqd,   c.plane,     c.sel,     c.resid,
+  if (int rc = map_refresh(c); rc) return rc;
+  PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane, c.sel, c.resid,
             c.chunk_part, c.count + 4};
   ScanDev s{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
@@ -2402,7 +2434,10 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   }
   if (with_super) enqueue_super(c, ctl, sa);
   SLIO_HIP(hipGetLastError());
-  if (which != 0) c.searched = true;
+  if (which != 0) {
+    c.searched = true;
+    c.search_version = c.map->version;
+  }
   return SLIO_OK;
 }
 
@@ -2566,6 +2601,736 @@ int slio_set_stream(slio_handle h, void* s) {
   return SLIO_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------- map index build
+namespace slio {
+
+__global__ void k_pack_ids(const float* __restrict__ x, const float* __restrict__ y,
+                           const float* __restrict__ z, int64_t n, uint32_t id0, float4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = make_float4(x[i], y[i], z[i], __uint_as_float(id0 + (uint32_t)i));
+}
+
+// sort key (cell << idbits) | id: the cell-sorted map keeps ascending ids
+// inside a cell (the tie order of the kNN keys), whatever order the points
+// come in
+__global__ void k_cell_keys64(const float4* __restrict__ in, int64_t n, GridGeom g, int idbits,
+                              uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  const int cx = min(max(cell_coord(p.x, g.ox, g.inv_h), 0), g.dx - 1);
+  const int cy = min(max(cell_coord(p.y, g.oy, g.inv_h), 0), g.dy - 1);
+  const int cz = min(max(cell_coord(p.z, g.oz, g.inv_h), 0), g.dz - 1);
+  const uint64_t cell = ((uint64_t)cz * (uint64_t)g.dy + (uint64_t)cy) * (uint64_t)g.dx + (uint64_t)cx;
+  keys[i] = (cell << idbits) | (uint64_t)__float_as_uint(p.w);
+  vals[i] = (uint32_t)i;
+}
+
+__global__ void k_cell_hist64(const uint64_t* __restrict__ keys, int64_t n, int idbits,
+                              uint32_t* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  atomicAdd(&counts[keys[i] >> idbits], 1u);
+}
+
+__global__ void k_gather4(const float4* __restrict__ in, const uint32_t* __restrict__ order, int64_t n,
+                          float4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = in[order[i]];
+}
+
+// order-preserving float keys for atomic min / max
+__device__ __forceinline__ int32_t fkey(float f) {
+  const int32_t b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+static inline float fkey_inv(int32_t k) {
+  const int32_t b = k >= 0 ? k : k ^ 0x7FFFFFFF;
+  float f;
+  std::memcpy(&f, &b, 4);
+  return f;
+}
+
+// bounding box: out[0..2] min keys, out[3..5] max keys; out[6] = 1 if a
+// coordinate is not finite
+__global__ void k_bbox4(const float4* __restrict__ in, int64_t n, int32_t* __restrict__ out) {
+  int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  int bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 p = in[i];
+    const float c[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      bad |= !isfinite(c[a]);
+      const int32_t k = fkey(c[a]);
+      lo[a] = min(lo[a], k);
+      hi[a] = max(hi[a], k);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    for (int d = 32; d > 0; d >>= 1) {
+      lo[a] = min(lo[a], __shfl_xor(lo[a], d, 64));
+      hi[a] = max(hi[a], __shfl_xor(hi[a], d, 64));
+    }
+  }
+  bad = __any(bad);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(out + a, lo[a]);
+      atomicMax(out + 3 + a, hi[a]);
+    }
+    if (bad) atomicOr(out + 6, 1);
+  }
+}
+
+__global__ void k_fill_u8(uint8_t* __restrict__ p, int64_t n, uint8_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void k_widen_flags(const uint8_t* __restrict__ k, int64_t n, uint32_t* __restrict__ f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = k[i] ? 1u : 0u;
+}
+
+static int grid_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
+
+// Build the grid index of m from the n points in `in` (device, x y z
+// bits(id), any order, all ids distinct) with bounding box mn / mx: the cell
+// table, the cell-sorted points, the coarse level and (speed only) the
+// block rows; keep flags all set.  m's index arrays must be empty.
+static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3], const float mx[3],
+                       hipStream_t st, const char* who) {
+  GridGeom g;
+  float hcell = m.cell0;
+  // kGridPad empty cells around the map's bounding box: scan points just
+  // outside it (ground returns below a flat map's lowest point, range noise)
+  // still get a query cell inside the grid, so they take the 3x3x3 fast path
+  constexpr int kGridPad = 2;
+  for (;;) {
+    g.ox = mn[0] - kGridPad * hcell;
+    g.oy = mn[1] - kGridPad * hcell;
+    g.oz = mn[2] - kGridPad * hcell;
+    g.h = hcell;
+    g.inv_h = 1.0f / hcell;
+    g.dx = cell_coord(mx[0], g.ox, g.inv_h) + 1 + kGridPad;
+    g.dy = cell_coord(mx[1], g.oy, g.inv_h) + 1 + kGridPad;
+    g.dz = cell_coord(mx[2], g.oz, g.inv_h) + 1 + kGridPad;
+    const int64_t nc = (int64_t)g.dx * g.dy * g.dz;
+    if (nc <= m.max_cells && nc < (int64_t)0xFFFFFFF0ll) break;
+    hcell *= 1.25f;  // grow cells until the dense table fits the budget
+  }
+  // largest |coordinate| a cell face can have: |origin| + dims * h per axis
+  const float mag = std::max(std::fabs(g.ox) + (float)g.dx * g.h,
+                             std::max(std::fabs(g.oy) + (float)g.dy * g.h, std::fabs(g.oz) + (float)g.dz * g.h));
+  g.tol = mag * 3.814697265625e-06f + 1.0e-5f;  // 2^-18 relative: >= 64 ulps
+  m.g = g;
+  m.n = n;
+  m.ncells = (int64_t)g.dx * g.dy * g.dz;
+  // coarse level geometry (cells of edge 4h on the same origin)
+  GridGeom cg = g;
+  cg.h = 4.0f * g.h;
+  cg.inv_h = 1.0f / cg.h;
+  cg.dx = (g.dx + 3) / 4;
+  cg.dy = (g.dy + 3) / 4;
+  cg.dz = (g.dz + 3) / 4;
+  m.cg = cg;
+  m.nccells = (int64_t)cg.dx * cg.dy * cg.dz;
+
+  auto fail = [&](const char* what, hipError_t e) {
+    set_error(std::string(who) + ": " + what + ": " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? SLIO_ENOMEM : SLIO_EDEVICE;
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&m.start, sizeof(uint32_t) * (m.ncells + 1))) ||
+      (e = hipMalloc(&m.cstart, sizeof(uint32_t) * (m.nccells + 1))) ||
+      (e = hipMalloc(&m.clo, sizeof(float4) * m.nccells)) || (e = hipMalloc(&m.chi, sizeof(float4) * m.nccells)))
+    return fail("hipMalloc", e);
+  if (n == 0) {
+    if ((e = hipMemsetAsync(m.start, 0, sizeof(uint32_t) * (m.ncells + 1), st)) ||
+        (e = hipMemsetAsync(m.cstart, 0, sizeof(uint32_t) * (m.nccells + 1), st)) ||
+        (e = hipMemsetAsync(m.clo, 0, sizeof(float4) * m.nccells, st)) || (e = hipStreamSynchronize(st)))
+      return fail("empty map", e);
+    return SLIO_OK;
+  }
+  if ((e = hipMalloc(&m.pts, sizeof(float4) * n)) || (e = hipMalloc(&m.keep, n)) ||
+      (e = hipMalloc(&m.cpts, sizeof(float4) * n)))
+    return fail("hipMalloc", e);
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  uint32_t *v0 = nullptr, *v1 = nullptr, *cnt = nullptr, *c0 = nullptr, *c1 = nullptr;
+  void* tmp = nullptr;
+  int rc = SLIO_OK;
+  const int64_t maxc = std::max(m.ncells, m.nccells) + 1;
+  do {
+    if ((e = hipMalloc(&k0, 8 * n)) || (e = hipMalloc(&k1, 8 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
+        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&c0, 4 * n)) || (e = hipMalloc(&c1, 4 * n)) ||
+        (e = hipMalloc(&cnt, 4 * maxc))) {
+      rc = fail("hipMalloc", e);
+      break;
+    }
+    int idbits = 1;
+    while (idbits < 32 && ((int64_t)1 << idbits) <= (int64_t)m.next_id) ++idbits;
+    int cbits = 1;
+    while (cbits < 32 && ((int64_t)1 << cbits) < m.ncells) ++cbits;
+    int ccbits = 1;
+    while (ccbits < 32 && ((int64_t)1 << ccbits) < m.nccells) ++ccbits;
+    size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, idbits + cbits, st)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c0, c1, v0, v1, (int)n, 0, ccbits, st)) ||
+        (e = hipcub::DeviceScan::ExclusiveSum(nullptr, t3, cnt, m.start, (int)maxc, st))) {
+      rc = fail("sort size", e);
+      break;
+    }
+    t4 = std::max(std::max(t1, t2), t3);
+    if ((e = hipMalloc(&tmp, t4))) {
+      rc = fail("hipMalloc tmp", e);
+      break;
+    }
+    const int nb = grid_blocks(n);
+    k_cell_keys64<<<nb, 256, 0, st>>>(in, n, g, idbits, k0, v0);
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, k0, k1, v0, v1, (int)n, 0, idbits + cbits, st)) ||
+        (e = hipMemsetAsync(cnt, 0, 4 * (m.ncells + 1), st))) {
+      rc = fail("sort", e);
+      break;
+    }
+    k_cell_hist64<<<nb, 256, 0, st>>>(k1, n, idbits, cnt);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.start, (int)(m.ncells + 1), st))) {
+      rc = fail("scan", e);
+      break;
+    }
+    k_gather4<<<nb, 256, 0, st>>>(in, v1, n, m.pts);
+    k_fill_u8<<<nb, 256, 0, st>>>(m.keep, n, 1);
+    // coarse level: points re-sorted by coarse cell (stable: fine positions
+    // ascend inside a coarse cell), tight boxes
+    k_coarse_keys<<<nb, 256, 0, st>>>(m.pts, n, cg, c0, v0);
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, c0, c1, v0, v1, (int)n, 0, ccbits, st)) ||
+        (e = hipMemsetAsync(cnt, 0, 4 * (m.nccells + 1), st))) {
+      rc = fail("coarse sort", e);
+      break;
+    }
+    k_cell_hist<<<nb, 256, 0, st>>>(c1, n, cnt);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.cstart, (int)(m.nccells + 1), st))) {
+      rc = fail("coarse scan", e);
+      break;
+    }
+    k_coarse_gather<<<nb, 256, 0, st>>>(m.pts, v1, n, m.cpts);
+    k_coarse_boxes<<<grid_blocks(m.nccells), 256, 0, st>>>(m.cpts, m.cstart, m.nccells, m.clo, m.chi);
+    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+      rc = fail("build kernels", e);
+      break;
+    }
+    // block rows (speed only): skipped when disabled, when their positions
+    // would overflow 32 bits or when the device memory is not there
+    const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
+    if ((nb9 && nb9[0] && nb9[0] != '0') || 9 * n >= (int64_t)0xFFFFFFF0ll) break;
+    const int ncb = grid_blocks(m.ncells);
+    if (hipMalloc(&m.bstart, sizeof(uint32_t) * (m.ncells + 1))) {
+      (void)hipGetLastError();
+      m.bstart = nullptr;
+      break;
+    }
+    k_blk_count<<<ncb, 256, 0, st>>>(m.start, g, m.ncells, cnt);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.bstart, (int)(m.ncells + 1), st))) {
+      rc = fail("block-row scan", e);
+      break;
+    }
+    uint32_t total = 0;  // <= 9 n < 2^32 (checked above): the scan cannot wrap
+    if ((e = hipMemcpyAsync(&total, m.bstart + m.ncells, sizeof(uint32_t), hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st))) {
+      rc = fail("block-row total", e);
+      break;
+    }
+    if (hipMalloc(&m.blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
+      (void)hipGetLastError();
+      m.blk = nullptr;
+      (void)hipFree(m.bstart);
+      m.bstart = nullptr;
+      break;
+    }
+    m.nblk = (int64_t)total;
+    k_blk_fill<<<ncb, 256, 0, st>>>(m.pts, m.start, m.bstart, g, m.ncells, m.blk);
+    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+      rc = fail("block-row kernels", e);
+      break;
+    }
+  } while (0);
+  for (void* q : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)c0, (void*)c1, (void*)cnt, tmp})
+    if (q) (void)hipFree(q);
+#ifdef SLIO_BOUNDS_CHECK
+  if (!rc) {
+    const int64_t nc = m.ncells;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_npts), &n, sizeof(n));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_ncells), &nc, sizeof(nc));
+  }
+#endif
+  return rc;
+}
+
+// ---------------------------------------------------------------- map maintenance
+// Device mirror of the map changes laserMapping makes every scan
+// (map_incremental laserMapping.cpp:382-433, KD_TREE::Add_Points
+// ikd_Tree.cpp:419-512, Delete_Point_Boxes ikd_Tree.cpp:559-579), with the
+// set semantics the oracle (oracle/map_oracle.cpp) restates.
+
+__device__ __forceinline__ float map_dist(float ax, float ay, float az, float bx, float by, float bz) {
+  // calc_dist (ikd_Tree.cpp:1539-1544, common_lib.h:86-90)
+  return (ax - bx) * (ax - bx) + (ay - by) * (ay - by) + (az - bz) * (az - bz);
+}
+__device__ __forceinline__ bool map_same(float ax, float ay, float az, float bx, float by, float bz) {
+  // same_point (ikd_Tree.cpp:1533-1536), EPSS 1e-6
+  return fabsf(ax - bx) < 1e-6 && fabsf(ay - by) < 1e-6 && fabsf(az - bz) < 1e-6;
+}
+
+// Delete_Point_Boxes: half-open boxes [min, max) (the Delete_by_range
+// predicate); boxes in constant-size batches
+struct Boxes8 {
+  float b[8][6];
+  int n;
+};
+__global__ void k_map_delete(const float4* __restrict__ pts, uint8_t* __restrict__ keep, int64_t n, Boxes8 bx,
+                             unsigned long long* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool del = false;
+  if (i < n && keep[i]) {
+    const float4 p = pts[i];
+    for (int k = 0; k < bx.n; ++k) {
+      const float* b = bx.b[k];
+      if (b[0] <= p.x && b[3] > p.x && b[1] <= p.y && b[4] > p.y && b[2] <= p.z && b[5] > p.z) del = true;
+    }
+    if (del) keep[i] = 0;
+  }
+  const unsigned long long m = __ballot(del);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+}
+
+// downsample voxel key of a point: the three floor(p / ds) (ikd_Tree.cpp:430-441)
+__global__ void k_ds_keys(const float4* __restrict__ in, int64_t n, float ds, uint64_t* __restrict__ keys,
+                          uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  const int64_t kx = (int64_t)floorf(p.x / ds), ky = (int64_t)floorf(p.y / ds), kz = (int64_t)floorf(p.z / ds);
+  keys[i] = ((uint64_t)((kx + (1 << 20)) & 0x1FFFFF) << 42) | ((uint64_t)((ky + (1 << 20)) & 0x1FFFFF) << 21) |
+            (uint64_t)((kz + (1 << 20)) & 0x1FFFFF);
+  vals[i] = (uint32_t)i;
+}
+
+// One thread per voxel group of the sorted list (the points of one
+// Add_Points call that share a downsample box, in list order): the
+// sequential rules of Add_Points on the box's stored points and the group's
+// points.  Stored points in storage order = ascending id; a stored point
+// wins only when strictly nearer the box centre (ties: the lower id).
+__global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __restrict__ keys,
+                            const uint32_t* __restrict__ order, int64_t n, float ds, MapView map,
+                            uint8_t* __restrict__ keep, uint32_t* __restrict__ surv,
+                            unsigned long long* __restrict__ counter) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= n || (i0 > 0 && keys[i0] == keys[i0 - 1])) return;
+  const float4 q0 = in[order[i0]];
+  float lo[3], hi[3];
+  const float c0[3] = {q0.x, q0.y, q0.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = floorf(c0[a] / ds) * ds;
+    hi[a] = lo[a] + ds;
+  }
+  const float mx = (float)((double)lo[0] + (double)(hi[0] - lo[0]) / 2.0);
+  const float my = (float)((double)lo[1] + (double)(hi[1] - lo[1]) / 2.0);
+  const float mz = (float)((double)lo[2] + (double)(hi[2] - lo[2]) / 2.0);
+  const GridGeom g = map.g;
+  int ca[3], cb[3];
+  const float og[3] = {g.ox, g.oy, g.oz};
+  const int dg[3] = {g.dx, g.dy, g.dz};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    ca[a] = min(max(cell_coord(lo[a], og[a], g.inv_h), 0), dg[a] - 1);
+    cb[a] = min(max(cell_coord(hi[a], og[a], g.inv_h), 0), dg[a] - 1);
+  }
+  auto inside = [&](const float4& p) {
+    return lo[0] <= p.x && hi[0] > p.x && lo[1] <= p.y && hi[1] > p.y && lo[2] <= p.z && hi[2] > p.z;
+  };
+  // stored points in the box: count and the one nearest the centre
+  int64_t cnt = 0;
+  float bd = 0.0f;
+  uint32_t bid = 0xFFFFFFFFu;
+  int64_t bpos = -1;
+  float4 bp = make_float4(0, 0, 0, 0);
+  if (map.n > 0)
+    for (int z = ca[2]; z <= cb[2]; ++z)
+      for (int y = ca[1]; y <= cb[1]; ++y) {
+        const uint32_t rb = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx;
+        for (uint32_t ps = map.start[rb + ca[0]]; ps < map.start[rb + cb[0] + 1]; ++ps) {
+          if (!keep[ps]) continue;
+          const float4 p = map.pts[ps];
+          if (!inside(p)) continue;
+          ++cnt;
+          const float d = map_dist(p.x, p.y, p.z, mx, my, mz);
+          const uint32_t id = __float_as_uint(p.w);
+          if (bpos < 0 || d < bd || (d == bd && id < bid)) {
+            bd = d;
+            bid = id;
+            bpos = ps;
+            bp = p;
+          }
+        }
+      }
+  // the group's points, in list order
+  bool orig_all = true;       // every stored point still alive
+  int64_t orig_keep = -1;     // else: the one stored point kept (or none)
+  int64_t cur_new = -1;       // list index of this call's surviving new point
+  bool best_new = false;
+  unsigned long long ops = 0;
+  for (int64_t j = i0; j < n && keys[j] == keys[i0]; ++j) {
+    const uint32_t li = order[j];
+    const float4 q = in[li];
+    const float dq = map_dist(q.x, q.y, q.z, mx, my, mz);
+    const bool stored_wins = cnt > 0 && bd < dq;
+    const float4 w = stored_wins ? bp : q;
+    if (cnt > 1 || map_same(q.x, q.y, q.z, w.x, w.y, w.z)) {
+      ++ops;
+      if (!stored_wins) {
+        orig_all = false;
+        orig_keep = -1;
+        cur_new = li;
+        best_new = true;
+        bd = dq;
+        bp = q;
+      } else if (!best_new && orig_all) {
+        orig_all = false;
+        orig_keep = bpos;
+      }
+      cnt = 1;
+    }
+  }
+  if (!orig_all && map.n > 0)
+    for (int z = ca[2]; z <= cb[2]; ++z)
+      for (int y = ca[1]; y <= cb[1]; ++y) {
+        const uint32_t rb = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx;
+        for (uint32_t ps = map.start[rb + ca[0]]; ps < map.start[rb + cb[0] + 1]; ++ps)
+          if (keep[ps] && (int64_t)ps != orig_keep && inside(map.pts[ps])) keep[ps] = 0;
+      }
+  if (cur_new >= 0) surv[cur_new] = 1;
+  if (ops) atomicAdd(counter, ops);
+}
+
+// surviving points -> add4[base + rank] with id next_id + rank
+__global__ void k_append(const float4* __restrict__ in, const uint32_t* __restrict__ surv,
+                         const uint32_t* __restrict__ rank, int64_t n, float4* __restrict__ add4,
+                         uint8_t* __restrict__ akeep, int64_t base, uint32_t next_id) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (surv && !surv[i])) return;
+  const uint32_t r = rank ? rank[i] : (uint32_t)i;
+  const float4 p = in[i];
+  add4[base + r] = make_float4(p.x, p.y, p.z, __uint_as_float(next_id + r));
+  akeep[base + r] = 1;
+}
+
+// pointBodyToWorld (laserMapping.cpp:276-287) with the rotation matrices
+// (Sophus SO3::matrix = Eigen toRotationMatrix) and map_incremental's
+// classification (laserMapping.cpp:388-423): flag 1 = PointToAdd,
+// 2 = PointNoNeedDownsample, 0 = not added.
+struct WorldMat {
+  double R[9], RL[9], pos[3], tli[3];
+};
+__global__ void k_map_classify(const float* __restrict__ bx, const float* __restrict__ by,
+                               const float* __restrict__ bz, int64_t n, WorldMat W,
+                               const uint32_t* __restrict__ nbr_pos, const float4* __restrict__ pts, double fs,
+                               int ekf_inited, float4* __restrict__ wpts, uint32_t* __restrict__ f_add,
+                               uint32_t* __restrict__ f_no) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double pb[3] = {(double)bx[i], (double)by[i], (double)bz[i]};
+  double a[3], w[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) a[r] = ((W.RL[3 * r] * pb[0] + W.RL[3 * r + 1] * pb[1]) + W.RL[3 * r + 2] * pb[2]) + W.tli[r];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) w[r] = ((W.R[3 * r] * a[0] + W.R[3 * r + 1] * a[1]) + W.R[3 * r + 2] * a[2]) + W.pos[r];
+  const float px = (float)w[0], py = (float)w[1], pz = (float)w[2];
+  wpts[i] = make_float4(px, py, pz, 0.0f);
+  int nn = 0;
+  float4 nb[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const uint32_t ps = nbr_pos[i * 5 + j];
+    nb[j] = make_float4(0, 0, 0, 0);
+    if (ps != 0xFFFFFFFFu && nn == j) {
+      nb[j] = pts[ps];
+      ++nn;
+    }
+  }
+  uint32_t fa = 0, fn = 0;
+  if (nn > 0 && ekf_inited) {
+    const float mx = (float)(floor((double)px / fs) * fs + 0.5 * fs);
+    const float my = (float)(floor((double)py / fs) * fs + 0.5 * fs);
+    const float mz = (float)(floor((double)pz / fs) * fs + 0.5 * fs);
+    const float dist = map_dist(px, py, pz, mx, my, mz);
+    if ((double)fabsf(nb[0].x - mx) > 0.5 * fs && (double)fabsf(nb[0].y - my) > 0.5 * fs &&
+        (double)fabsf(nb[0].z - mz) > 0.5 * fs) {
+      fn = 1;
+    } else {
+      bool need_add = true;
+      if (nn >= 5) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (need_add && map_dist(nb[j].x, nb[j].y, nb[j].z, mx, my, mz) < dist) need_add = false;
+      }
+      fa = need_add ? 1 : 0;
+    }
+  } else {
+    fa = 1;
+  }
+  f_add[i] = fa;
+  f_no[i] = fn;
+}
+
+__global__ void k_compact4(const float4* __restrict__ in, const uint32_t* __restrict__ flag,
+                           const uint32_t* __restrict__ rank, int64_t n, float4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) out[rank[i]] = in[i];
+}
+
+// exclusive scan of n flags into rank; returns the total
+static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream_t st, uint32_t* total) {
+  *total = 0;
+  if (n == 0) return SLIO_OK;
+  size_t tb = 0;
+  void* tmp = nullptr;
+  hipError_t e;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, rank, (int)n, st)) || (e = hipMalloc(&tmp, tb)) ||
+      (e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, rank, (int)n, st))) {
+    (void)hipFree(tmp);
+    set_error(std::string("slio map: scan: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  uint32_t last[2] = {0, 0};
+  e = hipMemcpyAsync(&last[0], rank + n - 1, 4, hipMemcpyDeviceToHost, st);
+  if (!e) e = hipMemcpyAsync(&last[1], flag + n - 1, 4, hipMemcpyDeviceToHost, st);
+  if (!e) e = hipStreamSynchronize(st);
+  (void)hipFree(tmp);
+  if (e) {
+    set_error(std::string("slio map: scan total: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  *total = last[0] + last[1];
+  return SLIO_OK;
+}
+
+static int add_reserve(MapDev& m, int64_t more, hipStream_t st) {
+  if (m.nadd + more <= m.add_cap) return SLIO_OK;
+  const int64_t cap = std::max<int64_t>(2 * m.add_cap, m.nadd + more + 4096);
+  float4* a = nullptr;
+  uint8_t* k = nullptr;
+  hipError_t e;
+  if ((e = hipMalloc(&a, 16 * cap)) || (e = hipMalloc(&k, cap))) {
+    (void)hipFree(a);
+    set_error(std::string("slio map: hipMalloc adds: ") + hipGetErrorString(e));
+    return SLIO_ENOMEM;
+  }
+  if (m.nadd > 0 && ((e = hipMemcpyAsync(a, m.add4, 16 * m.nadd, hipMemcpyDeviceToDevice, st)) ||
+                     (e = hipMemcpyAsync(k, m.akeep, m.nadd, hipMemcpyDeviceToDevice, st)) ||
+                     (e = hipStreamSynchronize(st)))) {
+    (void)hipFree(a);
+    (void)hipFree(k);
+    set_error(std::string("slio map: grow adds: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  (void)hipFree(m.add4);
+  (void)hipFree(m.akeep);
+  m.add4 = a;
+  m.akeep = k;
+  m.add_cap = cap;
+  return SLIO_OK;
+}
+
+static MapView map_view(const MapDev& m) {
+  const CoarseView cv{m.cg, m.cpts, m.cstart, m.clo, m.chi};
+  return MapView{m.g, m.n, m.pts, m.start, m.blk, m.bstart, m.nblk, m.ncells, cv};
+}
+
+// KD_TREE::Add_Points on the device map: n points at `in` (device float4,
+// .w ignored); returns the downsample counter (tmp_counter).
+static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float ds, int64_t* counter) {
+  MapDev& m = *c.map;
+  hipStream_t st = c.stream;
+  *counter = 0;
+  if (n == 0) return SLIO_OK;
+  if ((int64_t)m.next_id + n >= (int64_t)0x7FFFFFFF) {
+    set_error("slio map: point ids exhausted (2^31)");
+    return SLIO_ECAPACITY;
+  }
+  if (!downsample) {
+    if (int rc = add_reserve(m, n, st)) return rc;
+    k_append<<<grid_blocks(n), 256, 0, st>>>(in, nullptr, nullptr, n, m.add4, m.akeep, m.nadd, m.next_id);
+    SLIO_HIP(hipGetLastError());
+    m.nadd += n;
+    m.next_id += (uint32_t)n;
+    m.dirty = true;
+    return SLIO_OK;
+  }
+  // the box searches need every stored point in the index
+  if (int rc = map_refresh(c, true)) return rc;
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  uint32_t *v0 = nullptr, *v1 = nullptr, *surv = nullptr, *rank = nullptr;
+  unsigned long long* dcount = nullptr;
+  void* tmp = nullptr;
+  int rc = SLIO_OK;
+  do {
+    hipError_t e;
+    if ((e = hipMalloc(&k0, 8 * n)) || (e = hipMalloc(&k1, 8 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
+        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&surv, 4 * n)) || (e = hipMalloc(&rank, 4 * n)) ||
+        (e = hipMalloc(&dcount, 8))) {
+      set_error(std::string("slio map: hipMalloc: ") + hipGetErrorString(e));
+      rc = SLIO_ENOMEM;
+      break;
+    }
+    size_t tb = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 63, st)) ||
+        (e = hipMalloc(&tmp, tb))) {
+      set_error(std::string("slio map: sort: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    const int nb = grid_blocks(n);
+    k_ds_keys<<<nb, 256, 0, st>>>(in, n, ds, k0, v0);
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 63, st)) ||
+        (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 8, st))) {
+      set_error(std::string("slio map: sort: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    k_ds_groups<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, surv, dcount);
+    uint32_t total = 0;
+    if ((rc = scan_flags(surv, rank, n, st, &total))) break;
+    unsigned long long ops = 0;
+    if ((e = hipMemcpyAsync(&ops, dcount, 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+      set_error(std::string("slio map: groups: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    *counter = (int64_t)ops;
+    if ((rc = add_reserve(m, total, st))) break;
+    k_append<<<nb, 256, 0, st>>>(in, surv, rank, n, m.add4, m.akeep, m.nadd, m.next_id);
+    if ((e = hipGetLastError())) {
+      set_error(std::string("slio map: append: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    m.nadd += total;
+    m.next_id += total;
+    m.dirty = true;  // deletions (keep flags) and / or additions
+  } while (0);
+  for (void* q : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)surv, (void*)rank, (void*)dcount, tmp})
+    if (q) (void)hipFree(q);
+  return rc;
+}
+
+// Rebuild the index from the surviving points and the pending additions
+// (when the map changed since the last build).  adds_only: only when points
+// were added (deletions alone are honoured through the keep flags).
+static int map_refresh(Ctx& c, bool adds_only) {
+  if (!c.map || !c.map->dirty) return SLIO_OK;
+  MapDev& m = *c.map;
+  if (adds_only && m.nadd == 0) return SLIO_OK;
+  hipStream_t st = c.stream;
+  SLIO_HIP(hipStreamSynchronize(st));
+  const int64_t n0 = m.n, n1 = m.nadd;
+  float4* in4 = nullptr;
+  uint32_t *flag = nullptr, *rank = nullptr;
+  int32_t* bb = nullptr;
+  int rc = SLIO_OK;
+  int64_t n = 0;
+  float mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+  do {
+    hipError_t e;
+    const int64_t nt = n0 + n1;
+    if ((e = hipMalloc(&in4, 16 * std::max<int64_t>(nt, 1))) || (e = hipMalloc(&flag, 4 * std::max<int64_t>(nt, 1))) ||
+        (e = hipMalloc(&rank, 4 * std::max<int64_t>(nt, 1))) || (e = hipMalloc(&bb, 32))) {
+      set_error(std::string("slio map rebuild: hipMalloc: ") + hipGetErrorString(e));
+      rc = SLIO_ENOMEM;
+      break;
+    }
+    // survivors: stored points in cell order, then additions in id order
+    // (the sort in build_index orders by (cell, id) anyway)
+    float4* all = nullptr;
+    if ((e = hipMalloc(&all, 16 * std::max<int64_t>(nt, 1)))) {
+      set_error("slio map rebuild: hipMalloc");
+      rc = SLIO_ENOMEM;
+      break;
+    }
+    if ((n0 && ((e = hipMemcpyAsync(all, m.pts, 16 * n0, hipMemcpyDeviceToDevice, st)))) ||
+        (n1 && ((e = hipMemcpyAsync(all + n0, m.add4, 16 * n1, hipMemcpyDeviceToDevice, st))))) {
+      (void)hipFree(all);
+      set_error("slio map rebuild: copy");
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    {
+      // keep flags (u8) -> u32 flags
+      uint8_t* kk = nullptr;
+      if ((e = hipMalloc(&kk, std::max<int64_t>(nt, 1)))) {
+        (void)hipFree(all);
+        rc = SLIO_ENOMEM;
+        break;
+      }
+      if (n0) (void)hipMemcpyAsync(kk, m.keep, n0, hipMemcpyDeviceToDevice, st);
+      if (n1) (void)hipMemcpyAsync(kk + n0, m.akeep, n1, hipMemcpyDeviceToDevice, st);
+      k_widen_flags<<<grid_blocks(nt), 256, 0, st>>>(kk, nt, flag);
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(kk);
+    }
+    uint32_t total = 0;
+    if ((rc = scan_flags(flag, rank, nt, st, &total))) {
+      (void)hipFree(all);
+      break;
+    }
+    n = total;
+    if (nt) k_compact4<<<grid_blocks(nt), 256, 0, st>>>(all, flag, rank, nt, in4);
+    const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
+    if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
+      (void)hipFree(all);
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    if (n) k_bbox4<<<std::min(grid_blocks(n), 2048), 256, 0, st>>>(in4, n, bb);
+    int32_t got[8];
+    if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+      (void)hipFree(all);
+      set_error(std::string("slio map rebuild: bbox: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    (void)hipFree(all);
+    if (got[6]) {
+      set_error("slio map rebuild: non-finite map coordinate");
+      rc = SLIO_EINVAL;
+      break;
+    }
+    if (n)
+      for (int a = 0; a < 3; ++a) {
+        mn[a] = fkey_inv(got[a]);
+        mx[a] = fkey_inv(got[3 + a]);
+      }
+    m.free_index();
+    m.nadd = 0;
+    rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild");
+    m.version++;
+    m.dirty = false;
+  } while (0);
+  for (void* q : {(void*)in4, (void*)flag, (void*)rank, (void*)bb})
+    if (q) (void)hipFree(q);
+  return rc;
+}
+
+}  // namespace slio
+
+extern "C" {
+
 int slio_map_upload(slio_handle h, const float* x, const float* y, const float* z, int64_t n) {
   SLIO_CHECK_H(h);
   if (n < 0 || (n > 0 && (!x || !y || !z)) || n >= (int64_t)0xFFFFFFFFll) {
@@ -2574,7 +3339,9 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
   }
   auto m = std::make_shared<MapDev>();
   m->device = h->c.prm.device;
-  m->n = n;
+  m->cell0 = h->c.prm.grid_cell;
+  m->max_cells = h->c.prm.max_grid_cells;
+  m->next_id = (uint32_t)n;
   hipStream_t st = h->c.stream;
   // bounding box on the host (the snapshot is host-resident anyway)
   float mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
@@ -2594,212 +3361,28 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
     mn[a] = lo;
     mx[a] = hi;
   }
-  GridGeom g;
-  float hcell = h->c.prm.grid_cell;
-  // kGridPad empty cells around the map's bounding box: scan points just
-  // outside it (ground returns below a flat map's lowest point, range noise)
-  // still get a query cell inside the grid, so they take the 3x3x3 fast path
-  // instead of the growing-cube fallback
-  constexpr int kGridPad = 2;
-  for (;;) {
-    g.ox = mn[0] - kGridPad * hcell;
-    g.oy = mn[1] - kGridPad * hcell;
-    g.oz = mn[2] - kGridPad * hcell;
-    g.h = hcell;
-    g.inv_h = 1.0f / hcell;
-    g.dx = cell_coord(mx[0], g.ox, g.inv_h) + 1 + kGridPad;
-    g.dy = cell_coord(mx[1], g.oy, g.inv_h) + 1 + kGridPad;
-    g.dz = cell_coord(mx[2], g.oz, g.inv_h) + 1 + kGridPad;
-    const int64_t nc = (int64_t)g.dx * g.dy * g.dz;
-    if (nc <= h->c.prm.max_grid_cells && nc < (int64_t)0xFFFFFFF0ll) break;
-    hcell *= 1.25f;  // grow cells until the dense table fits the budget
-  }
-  // largest |coordinate| a cell face can have: |origin| + dims * h per axis
-  const float mag = std::max(std::fabs(g.ox) + (float)g.dx * g.h,
-                             std::max(std::fabs(g.oy) + (float)g.dy * g.h,
-                                      std::fabs(g.oz) + (float)g.dz * g.h));
-  g.tol = mag * 3.814697265625e-06f + 1.0e-5f;  // 2^-18 relative: >= 64 ulps
-  m->g = g;
-  m->ncells = (int64_t)g.dx * g.dy * g.dz;
-
-  SLIO_HIP(hipMalloc(&m->start, sizeof(uint32_t) * (m->ncells + 1)));
-  if (n > 0) SLIO_HIP(hipMalloc(&m->pts, sizeof(float4) * n));
-  if (n == 0) {
-    SLIO_HIP(hipMemsetAsync(m->start, 0, sizeof(uint32_t) * (m->ncells + 1), st));
-    SLIO_HIP(hipStreamSynchronize(st));
-    h->c.map = m;
-    return SLIO_OK;
-  }
   float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr;
-  uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *cnt = nullptr;
-  void* tmp = nullptr;
+  float4* in4 = nullptr;
   int rc = SLIO_OK;
-  auto fail = [&](const char* what, hipError_t e) {
-    set_error(std::string("slio_map_upload: ") + what + ": " + hipGetErrorString(e));
-    rc = SLIO_EDEVICE;
-  };
-  do {
+  if (n > 0) {
     hipError_t e;
     if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n)) ||
-        (e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
-        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&cnt, 4 * (m->ncells + 1)))) {
-      fail("hipMalloc", e);
+        (e = hipMalloc(&in4, 16 * n))) {
+      set_error(std::string("slio_map_upload: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
-      break;
+    } else if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, st)) ||
+               (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, st)) ||
+               (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, st))) {
+      set_error(std::string("slio_map_upload: H2D: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+    } else {
+      k_pack_ids<<<grid_blocks(n), 256, 0, st>>>(dx_, dy_, dz_, n, 0u, in4);
     }
-    if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, st)) ||
-        (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, st)) ||
-        (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, st))) {
-      fail("H2D", e);
-      break;
-    }
-    const int nb = (int)((n + 255) / 256);
-    k_cell_keys<<<nb, 256, 0, st>>>(dx_, dy_, dz_, n, g, k0, v0);
-    int end_bit = 1;
-    while (end_bit < 32 && ((int64_t)1 << end_bit) < m->ncells) ++end_bit;
-    size_t tb = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, end_bit, st))) {
-      fail("sort size", e);
-      break;
-    }
-    size_t tb2 = 0;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, cnt, m->start, (int)(m->ncells + 1), st))) {
-      fail("scan size", e);
-      break;
-    }
-    tb = std::max(tb, tb2);
-    if ((e = hipMalloc(&tmp, tb))) {
-      fail("hipMalloc tmp", e);
-      rc = SLIO_ENOMEM;
-      break;
-    }
-    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, end_bit, st))) {
-      fail("sort", e);
-      break;
-    }
-    if ((e = hipMemsetAsync(cnt, 0, 4 * (m->ncells + 1), st))) {
-      fail("memset", e);
-      break;
-    }
-    k_cell_hist<<<nb, 256, 0, st>>>(k1, n, cnt);
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, m->start, (int)(m->ncells + 1), st))) {
-      fail("scan", e);
-      break;
-    }
-    k_gather_sorted<<<nb, 256, 0, st>>>(dx_, dy_, dz_, v1, n, m->pts);
-    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
-      fail("build kernels", e);
-      break;
-    }
-    // coarse level: cells of edge 4h on the same origin, points re-sorted by
-    // coarse cell (stable: fine positions ascend inside a cell), tight boxes
-    {
-      GridGeom cg = g;
-      cg.h = 4.0f * g.h;
-      cg.inv_h = 1.0f / cg.h;
-      cg.dx = (g.dx + 3) / 4;
-      cg.dy = (g.dy + 3) / 4;
-      cg.dz = (g.dz + 3) / 4;
-      m->cg = cg;
-      m->nccells = (int64_t)cg.dx * cg.dy * cg.dz;
-      int cbits = 1;
-      while (cbits < 32 && ((int64_t)1 << cbits) < m->nccells) ++cbits;
-      size_t t1 = 0, t2 = 0;
-      if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, cbits, st)) ||
-          (e = hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cnt, m->cstart, (int)(m->nccells + 1), st))) {
-        fail("coarse sizes", e);
-        break;
-      }
-      if (std::max(t1, t2) > tb) {
-        (void)hipFree(tmp);
-        tmp = nullptr;
-        tb = std::max(t1, t2);
-        if ((e = hipMalloc(&tmp, tb))) {
-          fail("hipMalloc tmp", e);
-          rc = SLIO_ENOMEM;
-          break;
-        }
-      }
-      if ((e = hipMalloc(&m->cpts, sizeof(float4) * n)) ||
-          (e = hipMalloc(&m->cstart, sizeof(uint32_t) * (m->nccells + 1))) ||
-          (e = hipMalloc(&m->clo, sizeof(float4) * m->nccells)) ||
-          (e = hipMalloc(&m->chi, sizeof(float4) * m->nccells))) {
-        fail("hipMalloc coarse", e);
-        rc = SLIO_ENOMEM;
-        break;
-      }
-      k_coarse_keys<<<nb, 256, 0, st>>>(m->pts, n, cg, k0, v0);
-      if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, cbits, st)) ||
-          (e = hipMemsetAsync(cnt, 0, 4 * (m->nccells + 1), st))) {
-        fail("coarse sort", e);
-        break;
-      }
-      k_cell_hist<<<nb, 256, 0, st>>>(k1, n, cnt);
-      if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, m->cstart, (int)(m->nccells + 1), st))) {
-        fail("coarse scan", e);
-        break;
-      }
-      k_coarse_gather<<<nb, 256, 0, st>>>(m->pts, v1, n, m->cpts);
-      k_coarse_boxes<<<(int)((m->nccells + 255) / 256), 256, 0, st>>>(m->cpts, m->cstart, m->nccells,
-                                                                      m->clo, m->chi);
-      if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
-        fail("coarse kernels", e);
-        break;
-      }
-    }
-    // block rows (speed only): skipped when disabled, when their positions
-    // would overflow 32 bits or when the device memory is not there
-    const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
-    if ((nb9 && nb9[0] && nb9[0] != '0') || 9 * n >= (int64_t)0xFFFFFFF0ll) break;
-    const int ncb = (int)((m->ncells + 255) / 256);
-    if ((e = hipMalloc(&m->bstart, sizeof(uint32_t) * (m->ncells + 1)))) {
-      (void)hipGetLastError();
-      m->bstart = nullptr;
-      break;
-    }
-    k_blk_count<<<ncb, 256, 0, st>>>(m->start, g, m->ncells, cnt);
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, m->bstart, (int)(m->ncells + 1), st))) {
-      fail("block-row scan", e);
-      break;
-    }
-    uint32_t total = 0;  // <= 9 n < 2^32 (checked above): the scan cannot wrap
-    if ((e = hipMemcpyAsync(&total, m->bstart + m->ncells, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                            st)) ||
-        (e = hipStreamSynchronize(st))) {
-      fail("block-row total", e);
-      break;
-    }
-    if (hipMalloc(&m->blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
-      (void)hipGetLastError();
-      m->blk = nullptr;
-      (void)hipFree(m->bstart);
-      m->bstart = nullptr;
-      break;
-    }
-    m->nblk = (int64_t)total;
-    k_blk_fill<<<ncb, 256, 0, st>>>(m->pts, m->start, m->bstart, g, m->ncells, m->blk);
-    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
-      fail("block-row kernels", e);
-      break;
-    }
-  } while (0);
-  (void)hipFree(dx_);
-  (void)hipFree(dy_);
-  (void)hipFree(dz_);
-  (void)hipFree(k0);
-  (void)hipFree(k1);
-  (void)hipFree(v0);
-  (void)hipFree(v1);
-  (void)hipFree(cnt);
-  (void)hipFree(tmp);
-  if (rc) return rc;
-#ifdef SLIO_BOUNDS_CHECK
-  {
-    const int64_t nc = m->ncells;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_npts), &n, sizeof(n));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_ncells), &nc, sizeof(nc));
   }
-#endif
+  if (!rc) rc = build_index(*m, in4, n, mn, mx, st, "slio_map_upload");
+  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)in4})
+    if (q) (void)hipFree(q);
+  if (rc) return rc;
   h->c.map = m;
   h->c.searched = false;
   return SLIO_OK;
@@ -2822,6 +3405,7 @@ int slio_map_info(slio_handle h, int32_t dims[3], float* cell, int64_t* n) {
     set_error("slio_map_info: no map");
     return SLIO_ESTATE;
   }
+  if (int rc = map_refresh(h->c)) return rc;
   if (dims) {
     dims[0] = h->c.map->g.dx;
     dims[1] = h->c.map->g.dy;
@@ -2829,6 +3413,261 @@ int slio_map_info(slio_handle h, int32_t dims[3], float* cell, int64_t* n) {
   }
   if (cell) *cell = h->c.map->g.h;
   if (n) *n = h->c.map->n;
+  return SLIO_OK;
+}
+
+int slio_map_add_points(slio_handle h, const float* x, const float* y, const float* z, int64_t n,
+                        int downsample, float downsample_size, int64_t* counter) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!c.map) {
+    set_error("slio_map_add_points: no map");
+    return SLIO_ESTATE;
+  }
+  if (n < 0 || (n > 0 && (!x || !y || !z)) || (downsample && !(downsample_size > 0.0f))) {
+    set_error("slio_map_add_points: bad arguments");
+    return SLIO_EINVAL;
+  }
+  for (int64_t i = 0; i < n; ++i)
+    if (!std::isfinite(x[i]) || !std::isfinite(y[i]) || !std::isfinite(z[i])) {
+      set_error("slio_map_add_points: non-finite coordinate");
+      return SLIO_EINVAL;
+    }
+  int64_t cnt = 0;
+  if (n > 0) {
+    float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr;
+    float4* in4 = nullptr;
+    int rc = SLIO_OK;
+    hipError_t e;
+    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n)) ||
+        (e = hipMalloc(&in4, 16 * n))) {
+      set_error(std::string("slio_map_add_points: hipMalloc: ") + hipGetErrorString(e));
+      rc = SLIO_ENOMEM;
+    } else if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
+               (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
+               (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, c.stream))) {
+      set_error(std::string("slio_map_add_points: H2D: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+    } else {
+      k_pack_ids<<<grid_blocks(n), 256, 0, c.stream>>>(dx_, dy_, dz_, n, 0u, in4);
+      rc = map_add(c, in4, n, downsample != 0, downsample_size, &cnt);
+      if (!rc) (void)hipStreamSynchronize(c.stream);
+    }
+    for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)in4})
+      if (q) (void)hipFree(q);
+    if (rc) return rc;
+  }
+  if (counter) *counter = cnt;
+  return SLIO_OK;
+}
+
+int slio_map_delete_boxes(slio_handle h, const float* boxes, int64_t nboxes, int64_t* deleted) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!c.map) {
+    set_error("slio_map_delete_boxes: no map");
+    return SLIO_ESTATE;
+  }
+  if (nboxes < 0 || (nboxes > 0 && !boxes)) {
+    set_error("slio_map_delete_boxes: bad arguments");
+    return SLIO_EINVAL;
+  }
+  MapDev& m = *c.map;
+  unsigned long long* dc = nullptr;
+  SLIO_HIP(hipMalloc(&dc, 8));
+  SLIO_HIP(hipMemsetAsync(dc, 0, 8, c.stream));
+  for (int64_t b0 = 0; b0 < nboxes; b0 += 8) {
+    Boxes8 bx{};
+    bx.n = (int)std::min<int64_t>(8, nboxes - b0);
+    for (int k = 0; k < bx.n; ++k)
+      for (int j = 0; j < 6; ++j) bx.b[k][j] = boxes[6 * (b0 + k) + j];
+    if (m.n) k_map_delete<<<grid_blocks(m.n), 256, 0, c.stream>>>(m.pts, m.keep, m.n, bx, dc);
+    if (m.nadd) k_map_delete<<<grid_blocks(m.nadd), 256, 0, c.stream>>>(m.add4, m.akeep, m.nadd, bx, dc);
+  }
+  unsigned long long k = 0;
+  hipError_t e = hipMemcpyAsync(&k, dc, 8, hipMemcpyDeviceToHost, c.stream);
+  if (!e) e = hipStreamSynchronize(c.stream);
+  (void)hipFree(dc);
+  if (e) {
+    set_error(std::string("slio_map_delete_boxes: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  if (k) m.dirty = true;
+  if (deleted) *deleted = (int64_t)k;
+  return SLIO_OK;
+}
+
+int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_map_min, int ekf_inited,
+                         int64_t counts[3]) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!x || !(filter_size_map_min > 0.0)) {
+    set_error("slio_map_incremental: bad arguments");
+    return SLIO_EINVAL;
+  }
+  if (!c.map || !c.searched || c.search_version != c.map->version) {
+    set_error("slio_map_incremental: no search pass on the current map (Nearest_Points)");
+    return SLIO_ESTATE;
+  }
+  if (c.prm.nranks != 1) {
+    set_error("slio_map_incremental: needs the whole scan (nranks == 1)");
+    return SLIO_EINVAL;
+  }
+  const int64_t n = c.n;
+  WorldMat W;
+  {
+    // Eigen Quaternion::toRotationMatrix (Sophus SO3::matrix)
+    auto mat = [](const double* q, double* R) {
+      const double w = q[0], qx = q[1], qy = q[2], qz = q[3];
+      const double tx = 2.0 * qx, ty = 2.0 * qy, tz = 2.0 * qz;
+      const double twx = tx * w, twy = ty * w, twz = tz * w;
+      const double txx = tx * qx, txy = ty * qx, txz = tz * qx;
+      const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+      R[0] = 1.0 - (tyy + tzz);
+      R[1] = txy - twz;
+      R[2] = txz + twy;
+      R[3] = txy + twz;
+      R[4] = 1.0 - (txx + tzz);
+      R[5] = tyz - twx;
+      R[6] = txz - twy;
+      R[7] = tyz + twx;
+      R[8] = 1.0 - (txx + tyy);
+    };
+    mat(x->rot, W.R);
+    mat(x->rli, W.RL);
+    for (int k = 0; k < 3; ++k) {
+      W.pos[k] = x->pos[k];
+      W.tli[k] = x->tli[k];
+    }
+  }
+  int64_t out[3] = {0, 0, 0};
+  if (n > 0) {
+    float4 *w4 = nullptr, *l1 = nullptr, *l2 = nullptr;
+    uint32_t *fa = nullptr, *fn = nullptr, *ra = nullptr, *rn = nullptr;
+    int rc = SLIO_OK;
+    do {
+      hipError_t e;
+      if ((e = hipMalloc(&w4, 16 * n)) || (e = hipMalloc(&l1, 16 * n)) || (e = hipMalloc(&l2, 16 * n)) ||
+          (e = hipMalloc(&fa, 4 * n)) || (e = hipMalloc(&fn, 4 * n)) || (e = hipMalloc(&ra, 4 * n)) ||
+          (e = hipMalloc(&rn, 4 * n))) {
+        set_error(std::string("slio_map_incremental: hipMalloc: ") + hipGetErrorString(e));
+        rc = SLIO_ENOMEM;
+        break;
+      }
+      const int nb = grid_blocks(n);
+      k_map_classify<<<nb, 256, 0, c.stream>>>(c.bx, c.by, c.bz, n, W, c.nbr_pos, c.map->pts,
+                                               filter_size_map_min, ekf_inited, w4, fa, fn);
+      uint32_t na = 0, nn = 0;
+      if ((rc = scan_flags(fa, ra, n, c.stream, &na)) || (rc = scan_flags(fn, rn, n, c.stream, &nn))) break;
+      k_compact4<<<nb, 256, 0, c.stream>>>(w4, fa, ra, n, l1);
+      k_compact4<<<nb, 256, 0, c.stream>>>(w4, fn, rn, n, l2);
+      out[0] = na;
+      out[1] = nn;
+      int64_t cnt = 0, cnt2 = 0;
+      if ((rc = map_add(c, l1, na, true, (float)filter_size_map_min, &cnt))) break;
+      if ((rc = map_add(c, l2, nn, false, (float)filter_size_map_min, &cnt2))) break;
+      out[2] = cnt;
+      SLIO_HIP(hipStreamSynchronize(c.stream));
+    } while (0);
+    for (void* q : {(void*)w4, (void*)l1, (void*)l2, (void*)fa, (void*)fn, (void*)ra, (void*)rn})
+      if (q) (void)hipFree(q);
+    if (rc) return rc;
+  }
+  if (counts)
+    for (int k = 0; k < 3; ++k) counts[k] = out[k];
+  return SLIO_OK;
+}
+
+int slio_map_download(slio_handle h, float* x, float* y, float* z, uint32_t* ids, int64_t cap, int64_t* n) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!c.map) {
+    set_error("slio_map_download: no map");
+    return SLIO_ESTATE;
+  }
+  if (int rc = map_refresh(c)) return rc;
+  const MapDev& m = *c.map;
+  if (n) *n = m.n;
+  if (cap < m.n || (m.n > 0 && (!x || !y || !z || !ids))) {
+    set_error("slio_map_download: buffer too small");
+    return SLIO_ECAPACITY;
+  }
+  std::vector<float4> buf((size_t)m.n);
+  if (m.n) SLIO_HIP(hipMemcpy(buf.data(), m.pts, 16 * m.n, hipMemcpyDeviceToHost));
+  std::vector<std::pair<uint32_t, uint32_t>> order((size_t)m.n);
+  for (int64_t i = 0; i < m.n; ++i) {
+    uint32_t id;
+    std::memcpy(&id, &buf[i].w, 4);
+    order[i] = {id, (uint32_t)i};
+  }
+  std::sort(order.begin(), order.end());
+  for (int64_t k = 0; k < m.n; ++k) {
+    const float4& p = buf[order[k].second];
+    x[k] = p.x;
+    y[k] = p.y;
+    z[k] = p.z;
+    ids[k] = order[k].first;
+  }
+  return SLIO_OK;
+}
+
+int slio_fov_segment(const double pos_lid[3], float box_min[3], float box_max[3], int* initialized,
+                     double cube_len, float det_range, float boxes_out[18], int* nboxes) {
+  if (!pos_lid || !box_min || !box_max || !initialized || !boxes_out || !nboxes) {
+    set_error("slio_fov_segment: bad arguments");
+    return SLIO_EINVAL;
+  }
+  // lasermap_fov_segment (laserMapping.cpp:309-365), MOV_THRESHOLD 1.5 (:40)
+  const float kMov = 1.5f;
+  *nboxes = 0;
+  if (!*initialized) {
+    for (int i = 0; i < 3; ++i) {
+      box_min[i] = (float)(pos_lid[i] - cube_len / 2.0);
+      box_max[i] = (float)(pos_lid[i] + cube_len / 2.0);
+    }
+    *initialized = 1;
+    return SLIO_OK;
+  }
+  float dist[3][2];
+  bool need_move = false;
+  for (int i = 0; i < 3; ++i) {
+    dist[i][0] = (float)std::fabs(pos_lid[i] - box_min[i]);
+    dist[i][1] = (float)std::fabs(pos_lid[i] - box_max[i]);
+    if (dist[i][0] <= kMov * det_range || dist[i][1] <= kMov * det_range) need_move = true;
+  }
+  if (!need_move) return SLIO_OK;
+  float nmin[3], nmax[3];
+  for (int i = 0; i < 3; ++i) {
+    nmin[i] = box_min[i];
+    nmax[i] = box_max[i];
+  }
+  const float mov = (float)std::max((cube_len - 2.0 * kMov * det_range) * 0.5 * 0.9,
+                                    double(det_range * (kMov - 1)));
+  int k = 0;
+  for (int i = 0; i < 3; ++i) {
+    float tmin[3] = {box_min[0], box_min[1], box_min[2]}, tmax[3] = {box_max[0], box_max[1], box_max[2]};
+    if (dist[i][0] <= kMov * det_range) {
+      nmax[i] -= mov;
+      nmin[i] -= mov;
+      tmin[i] = box_max[i] - mov;
+    } else if (dist[i][1] <= kMov * det_range) {
+      nmax[i] += mov;
+      nmin[i] += mov;
+      tmax[i] = box_min[i] + mov;
+    } else {
+      continue;
+    }
+    for (int j = 0; j < 3; ++j) {
+      boxes_out[6 * k + j] = tmin[j];
+      boxes_out[6 * k + 3 + j] = tmax[j];
+    }
+    ++k;
+  }
+  for (int i = 0; i < 3; ++i) {
+    box_min[i] = nmin[i];
+    box_max[i] = nmax[i];
+  }
+  *nboxes = k;
   return SLIO_OK;
 }
 
@@ -2849,6 +3688,7 @@ int slio_scan_upload(slio_handle h, const float* x, const float* y, const float*
     hipError_t e;
     if ((e = hipMalloc(&c.bx, 4 * cap)) || (e = hipMalloc(&c.by, 4 * cap)) ||
         (e = hipMalloc(&c.bz, 4 * cap)) || (e = hipMalloc(&c.nbr_idx, 4 * 5 * cap)) ||
+        (e = hipMalloc(&c.nbr_pos, 4 * 5 * cap)) ||
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {

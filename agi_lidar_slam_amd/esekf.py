@@ -108,11 +108,49 @@ class KdTreeMap(_Handle):
         x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
         L.check(self.lib.slio_map_upload(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0]),
                 "KdTreeMap.Build")
-        self.points = pts
+        self.points = pts   # the Build snapshot (ids 0..n-1); flatten() gives the live map
         self.generation += 1
 
     def size(self) -> int:
-        return int(self.points.shape[0])
+        """KD_TREE::size (valid points; the device map after any changes)."""
+        n = C.c_int64()
+        L.check(self.lib.slio_map_info(self.h, None, None, C.byref(n)), "map_info")
+        return int(n.value)
+
+    def set_downsample_param(self, downsample_size: float) -> None:
+        """KD_TREE::set_downsample_param (ikd_Tree.h:275), used by Add_Points."""
+        self.downsample_size = float(downsample_size)
+
+    def Add_Points(self, points: np.ndarray, downsample_on: bool) -> int:
+        """KD_TREE::Add_Points (ikd_Tree.cpp:419-512) on the device map."""
+        pts = np.ascontiguousarray(np.asarray(points, dtype=np.float32).reshape(-1, 3))
+        x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
+        cnt = C.c_int64()
+        L.check(self.lib.slio_map_add_points(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0],
+                                             int(downsample_on), getattr(self, "downsample_size", 0.2),
+                                             C.byref(cnt)), "Add_Points")
+        return int(cnt.value)
+
+    def Delete_Point_Boxes(self, boxes: np.ndarray) -> int:
+        """KD_TREE::Delete_Point_Boxes (ikd_Tree.cpp:559-579); boxes (k, 6) =
+        vertex_min xyz, vertex_max xyz."""
+        b = np.ascontiguousarray(np.asarray(boxes, dtype=np.float32).reshape(-1, 6))
+        k = C.c_int64()
+        L.check(self.lib.slio_map_delete_boxes(self.h, L.fptr(b.reshape(-1)), b.shape[0], C.byref(k)),
+                "Delete_Point_Boxes")
+        return int(k.value)
+
+    def flatten(self):
+        """(points (n, 3) f32, ids (n,) u32) of the valid map in ascending id."""
+        n = C.c_int64()
+        self.lib.slio_map_download(self.h, None, None, None, None, 0, C.byref(n))
+        m = n.value
+        x, y, z = (np.zeros(m, np.float32) for _ in range(3))
+        ids = np.zeros(m, np.uint32)
+        L.check(self.lib.slio_map_download(self.h, L.fptr(x), L.fptr(y), L.fptr(z),
+                                           ids.ctypes.data_as(C.POINTER(C.c_uint32)), m, C.byref(n)),
+                "flatten")
+        return np.stack([x, y, z], 1), ids
 
     def grid_info(self):
         dims = (C.c_int32 * 3)()
@@ -210,6 +248,20 @@ class Esekf(_Handle):
         ekfom_data.valid = m.value >= 1
         if Nearest_Points is not None:
             Nearest_Points.update(self.nearest_points())
+
+    def map_incremental(self, ikdtree: "KdTreeMap", filter_size_map_min: float = 0.5,
+                        flg_EKF_inited: bool = True) -> np.ndarray:
+        """map_incremental (laserMapping.cpp:382-433) on the device: the scan of
+        the last update, at the current state, against its Nearest_Points.
+        Returns (|PointToAdd|, |PointNoNeedDownsample|, Add_Points counter)."""
+        if self._map_src is not ikdtree or self._map_gen != ikdtree.generation:
+            raise ValueError("map_incremental: the last update ran on another map")
+        counts = np.zeros(3, np.int64)
+        xc = self.x_.to_c()
+        L.check(self.lib.slio_map_incremental(self.h, C.byref(xc), float(filter_size_map_min),
+                                              int(bool(flg_EKF_inited)), L.i64ptr(counts)),
+                "map_incremental")
+        return counts
 
     def nearest_points(self) -> dict:
         b, e = C.c_int64(), C.c_int64()

@@ -232,6 +232,16 @@ def make_frame(scene: Scene, seed: int, n_scan: int, pattern: str = "avia",
         gt_pos[:2] += SENSOR_STREET
     elif sensor != "origin":
         raise ValueError(f"sensor must be 'street' or 'origin', not {sensor!r}")
+    body = _render(scene, gt_rot, gt_pos, n_scan, pattern, max_range, voxel, rng)
+    init_rot = quat_mul(gt_rot, quat_from_rotvec(rng.uniform(-1, 1, 3) * np.deg2rad(0.5)))
+    init_pos = gt_pos + rng.uniform(-0.1, 0.1, 3)
+    return Frame(body=np.ascontiguousarray(body), gt_rot=gt_rot, gt_pos=gt_pos,
+                 init_rot=init_rot, init_pos=init_pos)
+
+
+def _render(scene: Scene, gt_rot: np.ndarray, gt_pos: np.ndarray, n_scan: int, pattern: str,
+            max_range: float, voxel: float, rng) -> np.ndarray:
+    """n_scan LiDAR-frame returns of the scene seen from the IMU pose (gt_rot, gt_pos)."""
     R = quat_matrix(gt_rot)
     org = R @ AVIA_T_LI + gt_pos
     dir_fn = _avia_dirs if pattern == "avia" else _vlp16_dirs
@@ -261,10 +271,27 @@ def make_frame(scene: Scene, seed: int, n_scan: int, pattern: str = "avia",
     if pw is None:
         raise ValueError(f"could not collect {n_scan} voxel-unique returns")
     body = ((pw - gt_pos) @ R - AVIA_T_LI).astype(np.float32)  # R_LI = I
-    init_rot = quat_mul(gt_rot, quat_from_rotvec(rng.uniform(-1, 1, 3) * np.deg2rad(0.5)))
-    init_pos = gt_pos + rng.uniform(-0.1, 0.1, 3)
-    return Frame(body=np.ascontiguousarray(body), gt_rot=gt_rot, gt_pos=gt_pos,
-                 init_rot=init_rot, init_pos=init_pos)
+    return body
+
+
+def make_trajectory(seed: int, n_map: int, n_frames: int, n_scan: int, step: float = 0.5,
+                    pattern: str = "avia", voxel: float | None = None) -> list:
+    """Frames of a vehicle driving along the street y = BLOCK/2 (+x), `step`
+    metres per scan, with a small yaw / roll wobble; init_* = ground truth (a
+    mapping sequence carries its own state)."""
+    if voxel is None:
+        voxel = 0.2 if pattern == "avia" else 0.0
+    scene = make_scene(seed, n_map)
+    rng = np.random.default_rng(seed + 11)
+    out = []
+    for k in range(n_frames):
+        gt_rot = quat_mul(quat_from_rotvec(np.array([0, 0, 0.05 * np.sin(0.3 * k)])),
+                          quat_from_rotvec(rng.uniform(-0.01, 0.01, 3)))
+        gt_pos = np.array([SENSOR_STREET[0] - 3.0 + step * k, SENSOR_STREET[1] + 0.3 * np.sin(0.2 * k), 1.6])
+        body = _render(scene, gt_rot, gt_pos, n_scan, pattern, 300.0, voxel, rng)
+        out.append(Frame(body=body, gt_rot=gt_rot, gt_pos=gt_pos, init_rot=gt_rot.copy(),
+                         init_pos=gt_pos.copy()))
+    return out
 
 
 def make_problem(n_map: int, n_scan: int, seed: int = 20261015, pattern: str = "avia",

@@ -133,6 +133,51 @@ int slio_map_share(slio_handle h, slio_handle src);
 /* Grid diagnostics: dims[3], cell edge, number of map points. */
 int slio_map_info(slio_handle h, int32_t dims[3], float* cell, int64_t* n);
 
+/* ---- map maintenance (the live laserMapping map, replaces the ikd-Tree
+ *      calls of laserMapping.cpp:364, 430-431 and map_incremental :382-433) */
+/* Map point ids: slio_map_upload gives 0..n-1; each add call gives the new
+ * points that survive it the next ids, in list order.  Nearest_Points
+ * indices (slio_get_neighbors) are these ids.  Changes are applied to the
+ * device map at once (deletions) or queued (additions) and the search index
+ * is rebuilt on the device before the next search pass -- no host copy of
+ * the map, no re-upload.  A map shared by several handles changes for all of
+ * them; do not change it while another handle's update is in flight. */
+/* KD_TREE::Add_Points (ikd_Tree.cpp:419-512).  downsample = 1: for every
+ * point (in order) the points already in its voxel box [floor(p/ds)*ds,
+ * +ds) and the point itself keep only the one nearest the box centre
+ * (ties: the stored point with the lower id wins only when strictly
+ * nearer); *counter = Add_Points' return value.  downsample = 0: every
+ * point is added. */
+int slio_map_add_points(slio_handle h, const float* x, const float* y,
+                        const float* z, int64_t n, int downsample,
+                        float downsample_size, int64_t* counter);
+/* KD_TREE::Delete_Point_Boxes (ikd_Tree.cpp:559-579): removes the points in
+ * the half-open boxes [min, max) (boxes: nboxes x {min x, y, z, max x, y,
+ * z}); *deleted = number of points removed. */
+int slio_map_delete_boxes(slio_handle h, const float* boxes, int64_t nboxes,
+                          int64_t* deleted);
+/* map_incremental (laserMapping.cpp:382-433) on the device: the handle's
+ * scan (feats_down_body) to world at state x with pointBodyToWorld's
+ * rotation matrices (:276-287), classified against the Nearest_Points of
+ * the handle's last search pass (which must have run on the current map),
+ * then Add_Points(PointToAdd, downsample, filter_size_map_min) and
+ * Add_Points(PointNoNeedDownsample, no downsample).  counts = {|PointToAdd|,
+ * |PointNoNeedDownsample|, Add_Points' counter}.  nranks must be 1. */
+int slio_map_incremental(slio_handle h, const slio_state* x,
+                         double filter_size_map_min, int ekf_inited,
+                         int64_t counts[3]);
+/* The valid map points in ascending id (KD_TREE::flatten /
+ * featsFromMap): cap is the buffers' length; *n = number of points
+ * (ECAPACITY if cap is smaller). */
+int slio_map_download(slio_handle h, float* x, float* y, float* z,
+                      uint32_t* ids, int64_t cap, int64_t* n);
+/* lasermap_fov_segment (laserMapping.cpp:309-365), host only: moves the
+ * local map box [box_min, box_max] (in/out) with the LiDAR position and
+ * returns up to 3 boxes to delete (for slio_map_delete_boxes). */
+int slio_fov_segment(const double pos_lid[3], float box_min[3], float box_max[3],
+                     int* initialized, double cube_len, float det_range,
+                     float boxes_out[18], int* nboxes);
+
 /* ---- scan (feats_down_body, laserMapping.cpp:737-739) -------------------- */
 /* Upload the whole scan (host SoA float32, body frame).  With nranks > 1
  * every rank uploads the full scan and processes its own point shard. */

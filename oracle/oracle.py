@@ -23,7 +23,8 @@ _lib = None
 
 
 def build() -> str:
-    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "Makefile")]
+    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "map_oracle.cpp",
+                                            "Makefile")]
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
     return LIB
@@ -45,8 +46,27 @@ def load() -> C.CDLL:
         lib.orc_ikf_update.argtypes = [C.c_void_p, _FP, _FP, _FP, C.c_int64, _DP, _DP, C.c_double,
                                        C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
                                        C.c_int, _IP, _FP, _U8P, _I64P]
+        _bind_map(lib)
         _lib = lib
     return _lib
+
+
+def _bind_map(lib):
+    lib.orc_map_new.restype = C.c_void_p
+    lib.orc_map_new.argtypes = [_FP, _FP, _FP, C.c_int64, C.c_float]
+    lib.orc_map_free.argtypes = [C.c_void_p]
+    lib.orc_map_size.restype = C.c_int64
+    lib.orc_map_size.argtypes = [C.c_void_p]
+    lib.orc_map_dump.restype = C.c_int64
+    lib.orc_map_dump.argtypes = [C.c_void_p, _FP, _FP, _FP, C.POINTER(C.c_uint32)]
+    lib.orc_map_add.restype = C.c_int64
+    lib.orc_map_add.argtypes = [C.c_void_p, _FP, _FP, _FP, C.c_int64, C.c_int, C.c_float]
+    lib.orc_map_delete_boxes.restype = C.c_int64
+    lib.orc_map_delete_boxes.argtypes = [C.c_void_p, _FP, C.c_int64]
+    lib.orc_body_to_world_mat.argtypes = [_DP, _FP, _FP, _FP, C.c_int64, _FP, _FP, _FP]
+    lib.orc_map_incremental.argtypes = [C.c_void_p, _DP, _FP, _FP, _FP, C.c_int64, _IP, C.c_double,
+                                        C.c_int, C.c_float, _I64P]
+    lib.orc_fov_segment.argtypes = [_DP, _FP, _FP, C.POINTER(C.c_int), C.c_double, C.c_float, _FP]
 
 
 def _f(a):
@@ -144,6 +164,81 @@ def ikf_update(tree: Tree, body, state26, P, R=0.001, maximum_iter=4, extrinsic=
                                sel.ctypes.data_as(_U8P), st.ctypes.data_as(_I64P))
     assert rc == 0, rc
     return s, Pm, st, idx, sqd, sel
+
+
+# ---------------------------------------------------------------- map maintenance
+class Map:
+    """Set-semantics restatement of the ikd-Tree map as laserMapping changes it
+    (map_oracle.cpp): Build, Add_Points, Delete_Point_Boxes, map_incremental.
+    Points carry ids (0..n-1 for the build, then new survivors in list order)."""
+
+    def __init__(self, pts: np.ndarray, hash_edge: float = 0.5):
+        self.lib = load()
+        p = _f(pts).reshape(-1, 3)
+        x, y, z = (_f(p[:, k]) for k in range(3))
+        self.h = self.lib.orc_map_new(x.ctypes.data_as(_FP), y.ctypes.data_as(_FP), z.ctypes.data_as(_FP),
+                                      p.shape[0], hash_edge)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.orc_map_free(self.h)
+            self.h = None
+
+    def size(self) -> int:
+        return int(self.lib.orc_map_size(self.h))
+
+    def dump(self):
+        """(points (n, 3) f32, ids (n,) u32) in ascending id."""
+        n = self.size()
+        x, y, z = (np.zeros(n, np.float32) for _ in range(3))
+        ids = np.zeros(n, np.uint32)
+        self.lib.orc_map_dump(self.h, x.ctypes.data_as(_FP), y.ctypes.data_as(_FP), z.ctypes.data_as(_FP),
+                              ids.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return np.stack([x, y, z], 1), ids
+
+    def add_points(self, pts: np.ndarray, downsample: bool, ds: float = 0.5) -> int:
+        p = _f(pts).reshape(-1, 3)
+        x, y, z = (_f(p[:, k]) for k in range(3))
+        return int(self.lib.orc_map_add(self.h, x.ctypes.data_as(_FP), y.ctypes.data_as(_FP),
+                                        z.ctypes.data_as(_FP), p.shape[0], int(downsample), ds))
+
+    def delete_boxes(self, boxes: np.ndarray) -> int:
+        b = _f(boxes).reshape(-1, 6)
+        return int(self.lib.orc_map_delete_boxes(self.h, b.ctypes.data_as(_FP), b.shape[0]))
+
+    def incremental(self, state26, body, nbr_ids, filter_size_map_min=0.5, ekf_inited=True, ds=0.5):
+        s = np.ascontiguousarray(state26, dtype=np.float64)
+        bx, by, bz = (_f(body[:, j]) for j in range(3))
+        ids = np.ascontiguousarray(nbr_ids, dtype=np.int32)
+        counts = np.zeros(3, np.int64)
+        rc = self.lib.orc_map_incremental(self.h, s.ctypes.data_as(_DP), bx.ctypes.data_as(_FP),
+                                          by.ctypes.data_as(_FP), bz.ctypes.data_as(_FP), body.shape[0],
+                                          ids.ctypes.data_as(_IP), filter_size_map_min, int(ekf_inited), ds,
+                                          counts.ctypes.data_as(_I64P))
+        assert rc == 0, "map_incremental: neighbour id not in the map"
+        return counts
+
+
+def body_to_world_mat(state26, body):
+    """pointBodyToWorld (laserMapping.cpp:276-287): rotation matrices, not quaternions."""
+    s = np.ascontiguousarray(state26, dtype=np.float64)
+    bx, by, bz = (_f(body[:, j]) for j in range(3))
+    n = body.shape[0]
+    w = [np.zeros(n, np.float32) for _ in range(3)]
+    load().orc_body_to_world_mat(s.ctypes.data_as(_DP), bx.ctypes.data_as(_FP), by.ctypes.data_as(_FP),
+                                 bz.ctypes.data_as(_FP), n, *(a.ctypes.data_as(_FP) for a in w))
+    return np.stack(w, 1)
+
+
+def fov_segment(pos_lid, box_min, box_max, initialized, cube_len=1000.0, det_range=300.0):
+    """lasermap_fov_segment; box_min/box_max float32 (3,) updated in place; returns
+    (initialized, boxes (k, 6))."""
+    p = np.ascontiguousarray(pos_lid, dtype=np.float64)
+    ini = C.c_int(int(initialized))
+    out = np.zeros(18, np.float32)
+    k = load().orc_fov_segment(p.ctypes.data_as(_DP), box_min.ctypes.data_as(_FP), box_max.ctypes.data_as(_FP),
+                               C.byref(ini), cube_len, det_range, out.ctypes.data_as(_FP))
+    return bool(ini.value), out[:6 * k].reshape(-1, 6)
 
 
 # ---------------------------------------------------------------- LIO-SAM front-end

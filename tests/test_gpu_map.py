@@ -1,0 +1,194 @@
+"""GPU parity of the map maintenance mirror and the
+multi-scan laserMapping sequence (§8a-1).
+
+The device map changes exactly as the oracle's set-semantics restatement of
+ikd-Tree says (oracle/map_oracle.cpp): Add_Points with and without
+downsampling (ikd_Tree.cpp:419-512), Delete_Point_Boxes (:559-579),
+map_incremental (laserMapping.cpp:382-433).  Maps are compared as (id,
+x, y, z) lists, bit for bit.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_gpu_parity import L, mk, rot_err, state_of, upload_map  # noqa: E402,F401
+
+pytestmark = pytest.mark.gpu
+
+
+def dump(L, h):
+    lib = L.load()
+    n = C.c_int64()
+    lib.slio_map_download(h, None, None, None, None, 0, C.byref(n))
+    x, y, z = (np.zeros(n.value, np.float32) for _ in range(3))
+    ids = np.zeros(n.value, np.uint32)
+    L.check(lib.slio_map_download(h, L.fptr(x), L.fptr(y), L.fptr(z), ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                  n.value, C.byref(n)), "download")
+    return np.stack([x, y, z], 1), ids
+
+
+def add(L, h, pts, ds_on, ds=0.5):
+    pts = np.ascontiguousarray(pts, np.float32)
+    x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
+    cnt = C.c_int64()
+    L.check(L.load().slio_map_add_points(h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0], int(ds_on), ds,
+                                         C.byref(cnt)), "add")
+    return cnt.value
+
+
+def delete(L, h, boxes):
+    b = np.ascontiguousarray(boxes, np.float32).reshape(-1)
+    k = C.c_int64()
+    L.check(L.load().slio_map_delete_boxes(h, L.fptr(b), b.size // 6, C.byref(k)), "delete")
+    return k.value
+
+
+def assert_same_map(L, h, om):
+    gp, gi = dump(L, h)
+    op, oi = om.dump()
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gp, op)
+
+
+@pytest.mark.parametrize("cell", [1.25, 0.37])
+def test_add_delete_vs_oracle(L, oracle_mod, cell):
+    """Add_Points with downsampling (voxel groups of 1..5 new points against
+    0..4 stored points, exact duplicates for same_point), without it, box
+    deletions (also of points still waiting to be indexed), a search in
+    between: the device map equals the oracle's after every call."""
+    rng = np.random.default_rng(3)
+    base = rng.uniform(-20, 20, (20000, 3)).astype(np.float32)
+    base[:, 2] *= 0.2
+    h = mk(L, n_max=1000, cell=cell)
+    om = oracle_mod.Map(base)
+    try:
+        upload_map(L, h, base)
+        assert_same_map(L, h, om)
+        for rep in range(4):
+            new = np.concatenate([
+                rng.uniform(-22, 22, (3000, 3)),
+                base[rng.choice(base.shape[0], 500)] + rng.normal(0, 0.05, (500, 3)),
+                np.repeat(rng.uniform(-20, 20, (200, 3)), 3, axis=0),          # same voxel, same point
+                base[rng.choice(base.shape[0], 100)],                          # exact duplicates of stored
+            ]).astype(np.float32)
+            new = new[rng.permutation(new.shape[0])]
+            assert add(L, h, new, True) == om.add_points(new, True, 0.5)
+            assert_same_map(L, h, om)
+            extra = rng.uniform(-25, 25, (700, 3)).astype(np.float32)
+            assert add(L, h, extra, False) == om.add_points(extra, False, 0.5) == 0
+            boxes = np.array([[-30, -30, -30, -10, 30, 30], [5.0, 5.0, -1.0, 9.0, 9.5, 1.0]], np.float32)
+            boxes[:, :3] += rep
+            assert delete(L, h, boxes) == om.delete_boxes(boxes)   # also hits the unindexed additions
+            assert_same_map(L, h, om)
+            # a search pass on the changed map (index rebuilt on the device): exact kNN
+            q = rng.uniform(-15, 15, (1000, 3)).astype(np.float32)
+            from test_gpu_parity import IDENT, iterate, results, upload_scan
+            upload_scan(L, h, q)
+            iterate(L, h, IDENT, True)
+            idx, sqd, *_ = results(L, h, q.shape[0])
+            op, oi = om.dump()
+            ridx, rsqd = oracle_mod.Tree(op).knn(q, 5)
+            np.testing.assert_array_equal(idx, oi[ridx].astype(np.int32))
+            np.testing.assert_array_equal(sqd, rsqd)
+    finally:
+        L.load().slio_destroy(h)
+
+
+def test_fov_segment_matches_oracle(L, oracle_mod):
+    """lasermap_fov_segment: the C-ABI host function and the oracle move the
+    local map box identically and emit the same boxes along a trajectory."""
+    lib = L.load()
+    gmin, gmax = np.zeros(3, np.float32), np.zeros(3, np.float32)
+    omin, omax = np.zeros(3, np.float32), np.zeros(3, np.float32)
+    gini, oini = C.c_int(0), False
+    rng = np.random.default_rng(7)
+    pos = np.zeros(3)
+    nmoves = 0
+    for k in range(200):
+        pos = pos + rng.uniform(-2, 8, 3) * np.array([1, 1, 0.1])
+        out = np.zeros(18, np.float32)
+        nb = C.c_int()
+        L.check(lib.slio_fov_segment(L.dptr(pos), L.fptr(gmin), L.fptr(gmax), C.byref(gini), 200.0, 30.0,
+                                     L.fptr(out), C.byref(nb)), "fov")
+        oini, ob = oracle_mod.fov_segment(pos, omin, omax, oini, cube_len=200.0, det_range=30.0)
+        np.testing.assert_array_equal(gmin, omin)
+        np.testing.assert_array_equal(gmax, omax)
+        np.testing.assert_array_equal(out[:6 * nb.value].reshape(-1, 6), ob)
+        nmoves += nb.value > 0
+    assert nmoves > 5
+
+
+def test_map_incremental_sequence(L, oracle_mod):
+    """The laserMapping sequence (§8a-1 + §8f-1): 10 scans along a street, the
+    state carried from scan to scan (prior = last state moved by the true
+    motion, P reset to 1e-2 I: standing in for the IMU propagation and its
+    process noise); per scan lasermap_fov_segment +
+    Delete_Point_Boxes (small cube_len so the local map moves), the device
+    IKF update (4 iterations, reference control flow), map_incremental.  The
+    oracle runs its own IKF on its own copy of the map: states agree within
+    north_star tolerance; given the device's state and Nearest_Points, the
+    oracle's map_incremental leaves a map identical to the device's, every
+    scan."""
+    from agi_lidar_slam_amd import synth
+    from agi_lidar_slam_amd.esekf import StateIkfom
+    from agi_lidar_slam_amd.mapping import LaserMapping
+    seed = 20261015
+    frames = synth.make_trajectory(seed, 200000, 11, 20000, step=0.6)
+    lm = LaserMapping(filter_size_map_min=0.5, cube_len=124.0, det_range=40.0, maximum_iter=4,
+                      max_points=20000)
+    om = None
+    omin, omax = np.zeros(3, np.float32), np.zeros(3, np.float32)
+    oini = False
+    x = StateIkfom(pos=frames[0].gt_pos.copy(), rot=frames[0].gt_rot.copy(),
+                   offset_T_L_I=synth.AVIA_T_LI.copy())
+    lm.kf.change_x(x)
+    lm.kf.change_P(np.eye(24) * 1e-2)
+    total_del = total_add = 0
+    for k, fr in enumerate(frames):
+        x = lm.kf.get_x()
+        if k > 0:
+            # the IMU propagation's role: the prior moves by the ground-truth
+            # motion since the last scan (a street is a corridor: the ground
+            # and side walls do not observe motion along it)
+            x.pos = x.pos + (fr.gt_pos - frames[k - 1].gt_pos)
+            lm.kf.change_x(x)
+            lm.kf.change_P(np.eye(24) * 1e-2)   # and its process noise
+        st = x.to_array()
+        P0 = lm.kf.get_P().copy()
+        did = lm.process(fr.body, lidar_beg_time=0.1 * k)
+        # oracle: the same steps
+        pos_lid = synth_pos_lid(st)
+        oini, boxes = oracle_mod.fov_segment(pos_lid, omin, omax, oini, cube_len=124.0, det_range=40.0)
+        np.testing.assert_array_equal(boxes, lm.last["fov_boxes"])
+        if k == 0:
+            assert not did
+            om = oracle_mod.Map(oracle_mod.body_to_world_mat(st, fr.body))
+            assert_same_map(L, lm.ikdtree.h, om)
+            continue
+        assert lm.last["deleted"] == om.delete_boxes(boxes)
+        total_del += lm.last["deleted"]
+        op, oi = om.dump()
+        T = oracle_mod.Tree(op)
+        s_ref, *_ = oracle_mod.ikf_update(T, fr.body, st, P0, maximum_iter=4, mode=0, reference_gain=0)
+        xg = lm.kf.get_x().to_array()
+        assert np.abs(xg[0:3] - s_ref[0:3]).max() < 1e-4
+        assert rot_err(xg[3:7], s_ref[3:7]) < 1e-5
+        # the scan converged near the ground truth
+        assert np.abs(xg[0:3] - fr.gt_pos).max() < 0.15
+        # map_incremental with the device's state and Nearest_Points
+        ids = lm.Nearest_Points["index"]
+        counts = om.incremental(xg, fr.body, ids, 0.5, True, 0.5)
+        np.testing.assert_array_equal(counts, lm.last["map_incremental"])
+        total_add += int(counts[0] + counts[1])
+        assert_same_map(L, lm.ikdtree.h, om)
+    assert total_del > 0 and total_add > 0
+
+
+def synth_pos_lid(st):
+    # pos + rot * T_LI with the rotation matrix (laserMapping.cpp:729-730)
+    from agi_lidar_slam_amd.mapping import _mv, quat_matrix
+    return st[0:3] + _mv(quat_matrix(st[3:7]), st[11:14][:, None])[:, 0]
