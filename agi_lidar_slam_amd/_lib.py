@@ -162,6 +162,8 @@ SIGNATURES = {
     "slio_map_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
     "slio_map_share": (C.c_int, [_P, _P]),
     "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),
+    "slio_scan_upload_voxel": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_float, _I64P]),
+    "slio_scan_download": (C.c_int, [_P, _FP, _FP, _FP]),
     "slio_map_add_points": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_int, C.c_float, _I64P]),
     "slio_map_delete_boxes": (C.c_int, [_P, _FP, C.c_int64, _I64P]),
     "slio_map_incremental": (C.c_int, [_P, C.POINTER(SlioState), C.c_double, C.c_int, _I64P]),

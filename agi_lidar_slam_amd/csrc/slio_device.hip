@@ -2872,6 +2872,25 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
   return rc;
 }
 
+static int ensure_scan_buffers(Ctx& c) {
+  if (!c.bx) {
+    const int64_t cap = c.prm.max_points;
+    const int64_t capc = num_chunks(cap) + 1;
+    hipError_t e;
+    if ((e = hipMalloc(&c.bx, 4 * cap)) || (e = hipMalloc(&c.by, 4 * cap)) ||
+        (e = hipMalloc(&c.bz, 4 * cap)) || (e = hipMalloc(&c.nbr_idx, 4 * 5 * cap)) ||
+        (e = hipMalloc(&c.nbr_pos, 4 * 5 * cap)) ||
+        (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
+        (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
+        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {
+      free_scan(&c);
+      set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));
+      return SLIO_ENOMEM;
+    }
+  }
+  return SLIO_OK;
+}
+
 // ---------------------------------------------------------------- map maintenance
 // Device mirror of the map changes laserMapping makes every scan
 // (map_incremental laserMapping.cpp:382-433, KD_TREE::Add_Points
@@ -3093,6 +3112,96 @@ __global__ void k_compact4(const float4* __restrict__ in, const uint32_t* __rest
                            const uint32_t* __restrict__ rank, int64_t n, float4* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && flag[i]) out[rank[i]] = in[i];
+}
+
+// ---------------------------------------------------------------- scan VoxelGrid
+// downSizeFilterSurf (laserMapping.cpp:683-686, 737-739): pcl::VoxelGrid
+// (PCL 1.10 voxel_grid.hpp applyFilter + CentroidPoint) on the device.
+__global__ void k_vg_bbox(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                          int64_t n, int32_t* __restrict__ out) {
+  int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  int cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float c[3] = {x[i], y[i], z[i]};
+    if (!(isfinite(c[0]) && isfinite(c[1]) && isfinite(c[2]))) continue;  // getMinMax3D skips them
+    ++cnt;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const int32_t k = fkey(c[a]);
+      lo[a] = min(lo[a], k);
+      hi[a] = max(hi[a], k);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int d = 32; d > 0; d >>= 1) {
+      lo[a] = min(lo[a], __shfl_xor(lo[a], d, 64));
+      hi[a] = max(hi[a], __shfl_xor(hi[a], d, 64));
+    }
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(out + a, lo[a]);
+      atomicMax(out + 3 + a, hi[a]);
+    }
+    atomicAdd(out + 6, cnt);
+  }
+}
+
+struct VgGeom {
+  float inv[3];
+  int minb[3];
+  int mul[3];
+};
+
+// voxel index idx = ijk0 + ijk1 * div0 + ijk2 * div0 * div1, ijk =
+// int(floor(p * inv) - float(min_b)); non-finite points sort last (dropped)
+__global__ void k_vg_keys(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                          int64_t n, VgGeom G, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float c[3] = {x[i], y[i], z[i]};
+  uint32_t key = 0xFFFFFFFFu;
+  if (isfinite(c[0]) && isfinite(c[1]) && isfinite(c[2])) {
+    int ijk[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ijk[a] = (int)(floorf(c[a] * G.inv[a]) - (float)G.minb[a]);
+    key = (uint32_t)(ijk[0] * G.mul[0] + ijk[1] * G.mul[1] + ijk[2] * G.mul[2]);
+  }
+  keys[i] = key;
+  vals[i] = (uint32_t)i;
+}
+
+__global__ void k_vg_heads(const uint32_t* __restrict__ keys, int64_t n, uint32_t* __restrict__ head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  head[i] = keys[i] != 0xFFFFFFFFu && (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+// one thread per voxel: the centroid, summed in float in the sorted order
+// (ascending point index inside a voxel), divided by the count (CentroidPoint
+// AccumulatorXYZ: xyz += p; get: xyz / n)
+__global__ void k_vg_centroids(const float* __restrict__ x, const float* __restrict__ y,
+                               const float* __restrict__ z, const uint32_t* __restrict__ keys,
+                               const uint32_t* __restrict__ order, const uint32_t* __restrict__ head,
+                               const uint32_t* __restrict__ rank, int64_t n, float* __restrict__ ox,
+                               float* __restrict__ oy, float* __restrict__ oz) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= n || !head[i0]) return;
+  float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+  int64_t j = i0;
+  for (; j < n && keys[j] == keys[i0]; ++j) {
+    const uint32_t o = order[j];
+    sx = sx + x[o];
+    sy = sy + y[o];
+    sz = sz + z[o];
+  }
+  const float cnt = (float)(j - i0);
+  const uint32_t r = rank[i0];
+  ox[r] = sx / cnt;
+  oy[r] = sy / cnt;
+  oz[r] = sz / cnt;
 }
 
 // exclusive scan of n flags into rank; returns the total
@@ -3671,6 +3780,140 @@ int slio_fov_segment(const double pos_lid[3], float box_min[3], float box_max[3]
   return SLIO_OK;
 }
 
+int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const float* z, int64_t n,
+                           float leaf, int64_t* n_down) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (n < 0 || (n > 0 && (!x || !y || !z)) || !(leaf > 0.0f) || n >= (int64_t)0xFFFFFFFFll) {
+    set_error("slio_scan_upload_voxel: bad arguments");
+    return SLIO_EINVAL;
+  }
+  hipStream_t st = c.stream;
+  float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr;
+  uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *hd = nullptr, *rk = nullptr;
+  int32_t* bb = nullptr;
+  void* tmp = nullptr;
+  int rc = SLIO_OK;
+  int64_t m = 0;
+  bool passthrough = false;
+  do {
+    if (n == 0) break;
+    hipError_t e;
+    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n)) ||
+        (e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
+        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&hd, 4 * n)) || (e = hipMalloc(&rk, 4 * n)) ||
+        (e = hipMalloc(&bb, 32))) {
+      set_error(std::string("slio_scan_upload_voxel: hipMalloc: ") + hipGetErrorString(e));
+      rc = SLIO_ENOMEM;
+      break;
+    }
+    const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
+    int32_t got[8];
+    if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
+      set_error(std::string("slio_scan_upload_voxel: H2D: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    k_vg_bbox<<<std::min(grid_blocks(n), 1024), 256, 0, st>>>(dx_, dy_, dz_, n, bb);
+    if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+      set_error(std::string("slio_scan_upload_voxel: bbox: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    if (got[6] == 0) break;  // no finite point: empty scan
+    // PCL's geometry (voxel_grid.hpp applyFilter), float arithmetic
+    VgGeom G;
+    float mn[3], mx[3];
+    int64_t dd[3];
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fkey_inv(got[a]);
+      mx[a] = fkey_inv(got[3 + a]);
+      G.inv[a] = 1.0f / leaf;
+      dd[a] = (int64_t)((mx[a] - mn[a]) * G.inv[a]) + 1;
+    }
+    if (dd[0] * dd[1] * dd[2] > (int64_t)INT32_MAX) {
+      passthrough = true;  // PCL: leaf too small for the cloud, output = input
+      break;
+    }
+    int div[3];
+    for (int a = 0; a < 3; ++a) {
+      G.minb[a] = (int)std::floor(mn[a] * G.inv[a]);
+      div[a] = (int)std::floor(mx[a] * G.inv[a]) - G.minb[a] + 1;
+    }
+    G.mul[0] = 1;
+    G.mul[1] = div[0];
+    G.mul[2] = div[0] * div[1];
+    const int nb = grid_blocks(n);
+    k_vg_keys<<<nb, 256, 0, st>>>(dx_, dy_, dz_, n, G, k0, v0);
+    size_t tb = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
+        (e = hipMalloc(&tmp, tb)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
+      set_error(std::string("slio_scan_upload_voxel: sort: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    k_vg_heads<<<nb, 256, 0, st>>>(k1, n, hd);
+    uint32_t total = 0;
+    if ((rc = scan_flags(hd, rk, n, st, &total))) break;
+    m = total;
+    if (m > c.prm.max_points) {
+      set_error("slio_scan_upload_voxel: downsampled scan exceeds max_points");
+      rc = SLIO_ECAPACITY;
+      break;
+    }
+    if ((rc = ensure_scan_buffers(c))) break;
+    k_vg_centroids<<<nb, 256, 0, st>>>(dx_, dy_, dz_, k1, v1, hd, rk, n, c.bx, c.by, c.bz);
+    if ((e = hipGetLastError())) {
+      set_error(std::string("slio_scan_upload_voxel: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+  } while (0);
+  if (!rc && passthrough) {
+    if (n > c.prm.max_points) {
+      set_error("slio_scan_upload_voxel: scan exceeds max_points");
+      rc = SLIO_ECAPACITY;
+    } else if (!(rc = ensure_scan_buffers(c))) {
+      // non-finite points stay (PCL copies the input as is)
+      (void)hipMemcpyAsync(c.bx, dx_, 4 * n, hipMemcpyDeviceToDevice, st);
+      (void)hipMemcpyAsync(c.by, dy_, 4 * n, hipMemcpyDeviceToDevice, st);
+      (void)hipMemcpyAsync(c.bz, dz_, 4 * n, hipMemcpyDeviceToDevice, st);
+      m = n;
+    }
+  }
+  if (!rc) {
+    if (m > 0 && c.bx) (void)hipMemsetAsync(c.sel, 0, m, st);
+    (void)hipStreamSynchronize(st);
+    c.n = m;
+    c.searched = false;
+    if (n_down) *n_down = m;
+  }
+  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)hd,
+                  (void*)rk, (void*)bb, tmp})
+    if (q) (void)hipFree(q);
+  return rc;
+}
+
+int slio_scan_download(slio_handle h, float* x, float* y, float* z) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (c.n > 0 && (!x || !y || !z)) {
+    set_error("slio_scan_download: bad arguments");
+    return SLIO_EINVAL;
+  }
+  if (c.n > 0) {
+    SLIO_HIP(hipStreamSynchronize(c.stream));
+    SLIO_HIP(hipMemcpy(x, c.bx, 4 * c.n, hipMemcpyDeviceToHost));
+    SLIO_HIP(hipMemcpy(y, c.by, 4 * c.n, hipMemcpyDeviceToHost));
+    SLIO_HIP(hipMemcpy(z, c.bz, 4 * c.n, hipMemcpyDeviceToHost));
+  }
+  return SLIO_OK;
+}
+
 int slio_scan_upload(slio_handle h, const float* x, const float* y, const float* z, int64_t n) {
   SLIO_CHECK_H(h);
   Ctx& c = h->c;
@@ -3682,21 +3925,7 @@ int slio_scan_upload(slio_handle h, const float* x, const float* y, const float*
     set_error("slio_scan_upload: scan exceeds max_points");
     return SLIO_ECAPACITY;
   }
-  if (!c.bx) {
-    const int64_t cap = c.prm.max_points;
-    const int64_t capc = num_chunks(cap) + 1;
-    hipError_t e;
-    if ((e = hipMalloc(&c.bx, 4 * cap)) || (e = hipMalloc(&c.by, 4 * cap)) ||
-        (e = hipMalloc(&c.bz, 4 * cap)) || (e = hipMalloc(&c.nbr_idx, 4 * 5 * cap)) ||
-        (e = hipMalloc(&c.nbr_pos, 4 * 5 * cap)) ||
-        (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
-        (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
-        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {
-      free_scan(&c);
-      set_error(std::string("slio_scan_upload: hipMalloc: ") + hipGetErrorString(e));
-      return SLIO_ENOMEM;
-    }
-  }
+  if (int rc = ensure_scan_buffers(c)) return rc;
   c.n = n;
   if (n > 0) {
     SLIO_HIP(hipMemcpyAsync(c.bx, x, 4 * n, hipMemcpyHostToDevice, c.stream));

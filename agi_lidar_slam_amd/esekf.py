@@ -198,16 +198,42 @@ class Esekf(_Handle):
         self.P_ = np.array(P, dtype=np.float64).reshape(24, 24)
 
     # --- plumbing
-    def _bind(self, feats_down_body: np.ndarray, ikdtree: KdTreeMap) -> int:
+    def downsample_scan(self, feats_undistort: np.ndarray, filter_size_surf: float) -> int:
+        """downSizeFilterSurf.filter (laserMapping.cpp:737-739) on the device:
+        the downsampled scan stays in HBM as this filter's feats_down_body
+        (pass feats_down_body=None to the update to use it).  Returns
+        feats_down_size."""
+        pts = np.ascontiguousarray(np.asarray(feats_undistort, dtype=np.float32)[:, :3])
+        x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
+        n = C.c_int64()
+        L.check(self.lib.slio_scan_upload_voxel(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0],
+                                                float(filter_size_surf), C.byref(n)), "downsample_scan")
+        self._scan_ref = None
+        self._n_scan = int(n.value)
+        return self._n_scan
+
+    def feats_down_body(self) -> np.ndarray:
+        """The handle's current scan (feats_down_body) as an (n, 3) array."""
+        b, e = C.c_int64(), C.c_int64()
+        L.check(self.lib.slio_shard_range(self.h, C.byref(b), C.byref(e)), "shard_range")
+        n = getattr(self, "_n_scan", 0)
+        x, y, z = (np.zeros(n, np.float32) for _ in range(3))
+        L.check(self.lib.slio_scan_download(self.h, L.fptr(x), L.fptr(y), L.fptr(z)), "scan_download")
+        return np.stack([x, y, z], 1)
+
+    def _bind(self, feats_down_body: np.ndarray | None, ikdtree: KdTreeMap) -> int:
         if self._map_src is not ikdtree or self._map_gen != ikdtree.generation:
             L.check(self.lib.slio_map_share(self.h, ikdtree.h), "map_share")
             self._map_src = ikdtree
             self._map_gen = ikdtree.generation
+        if feats_down_body is None:   # the device scan of downsample_scan
+            return getattr(self, "_n_scan", 0)
         pts = np.ascontiguousarray(np.asarray(feats_down_body, dtype=np.float32)[:, :3])
         x, y, z = (np.ascontiguousarray(pts[:, k]) for k in range(3))
         L.check(self.lib.slio_scan_upload(self.h, L.fptr(x), L.fptr(y), L.fptr(z), pts.shape[0]),
                 "scan_upload")
         self._scan_ref = feats_down_body
+        self._n_scan = int(pts.shape[0])
         return pts.shape[0]
 
     def boxplus(self, x: StateIkfom, f: np.ndarray) -> StateIkfom:
@@ -229,6 +255,7 @@ class Esekf(_Handle):
         """One measurement pass (esekfom.hpp:106-227); search iff ekfom_data.converge."""
         if (feats_down_body is not self._scan_ref or self._map_src is not ikdtree
                 or self._map_gen != ikdtree.generation):
+            # (feats_down_body None: the device scan of downsample_scan)
             self._bind(feats_down_body, ikdtree)
         pose = L.SlioPose()
         pose.rot[:] = list(self.x_.rot)

@@ -183,6 +183,21 @@ int slio_fov_segment(const double pos_lid[3], float box_min[3], float box_max[3]
  * every rank uploads the full scan and processes its own point shard. */
 int slio_scan_upload(slio_handle h, const float* x, const float* y,
                      const float* z, int64_t n);
+/* downSizeFilterSurf (laserMapping.cpp:683-686, 737-739) on the device: the
+ * raw scan (feats_undistort, host SoA float32, n points) through
+ * pcl::VoxelGrid with edge `leaf` (PCL 1.10 applyFilter + CentroidPoint:
+ * voxel index over the cloud's bounding box, centroids in ascending voxel
+ * index, float sums / count; non-finite points skipped; a leaf too small for
+ * the cloud copies the input) becomes the handle's scan (feats_down_body),
+ * *n_down points, ready for the passes below.  Inside a voxel the points are
+ * summed in ascending input order (PCL's std::sort leaves that order
+ * implementation-defined; a voxel of >= 3 points can differ from PCL's in
+ * the last bits).  ECAPACITY if more than max_points voxels remain. */
+int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y,
+                           const float* z, int64_t n, float leaf,
+                           int64_t* n_down);
+/* The handle's current scan (feats_down_body) back to the host. */
+int slio_scan_download(slio_handle h, float* x, float* y, float* z);
 /* Point range [begin, end) this handle processes for the uploaded scan. */
 int slio_shard_range(slio_handle h, int64_t* begin, int64_t* end);
 

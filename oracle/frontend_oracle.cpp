@@ -166,6 +166,60 @@ int64_t voxel_grid(const float* xyzi, const std::vector<int64_t>& pos, float lea
   return ns;
 }
 
+// The same VoxelGrid with PCL 1.10's own index sort: std::sort of
+// {idx, cloud_point_index} with operator< on idx only (voxel_grid.hpp,
+// cloud_point_index_idx), i.e. libstdc++ introsort's order inside a voxel.
+int64_t voxel_grid_pcl_order(const float* xyzi, const std::vector<int64_t>& pos, float leaf, float* out) {
+  struct Idx {
+    uint32_t idx, cpi;
+    bool operator<(const Idx& o) const { return idx < o.idx; }
+  };
+  if (pos.empty()) return 0;
+  const float inv = 1.0f / leaf;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t p : pos)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = std::min(mn[a], xyzi[p * 4 + a]);
+      mx[a] = std::max(mx[a], xyzi[p * 4 + a]);
+    }
+  const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+  const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+  const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+  int64_t ns = 0;
+  if (dx * dy * dz > (int64_t)INT32_MAX) {
+    for (int64_t p : pos) std::memcpy(out + (ns++) * 4, xyzi + p * 4, 16);
+    return ns;
+  }
+  int minb[3], divb[3];
+  for (int a = 0; a < 3; ++a) {
+    minb[a] = (int)std::floor(mn[a] * inv);
+    divb[a] = (int)std::floor(mx[a] * inv) - minb[a] + 1;
+  }
+  const int mul[3] = {1, divb[0], divb[0] * divb[1]};
+  std::vector<Idx> iv;
+  iv.reserve(pos.size());
+  for (size_t q = 0; q < pos.size(); ++q) {
+    const float* pp = xyzi + pos[q] * 4;
+    int ijk[3];
+    for (int a = 0; a < 3; ++a) ijk[a] = (int)(std::floor(pp[a] * inv) - (float)minb[a]);
+    iv.push_back(Idx{(uint32_t)(ijk[0] * mul[0] + ijk[1] * mul[1] + ijk[2] * mul[2]), (uint32_t)q});
+  }
+  std::sort(iv.begin(), iv.end());
+  size_t a0 = 0;
+  while (a0 < iv.size()) {
+    size_t a1 = a0 + 1;
+    while (a1 < iv.size() && iv[a1].idx == iv[a0].idx) ++a1;
+    float sm[4] = {0, 0, 0, 0};
+    for (size_t q = a0; q < a1; ++q)
+      for (int c = 0; c < 4; ++c) sm[c] += xyzi[pos[iv[q].cpi] * 4 + c];
+    const float cnt = (float)(a1 - a0);
+    for (int c = 0; c < 4; ++c) out[ns * 4 + c] = sm[c] / cnt;
+    ++ns;
+    a0 = a1;
+  }
+  return ns;
+}
+
 // featureExtraction.cpp:108-177 / featureAssociation.cpp:807-876:
 // calculateSmoothness + markOccludedPoints over (range, column) lists.
 // picked = 1 for entries the reference never initialises (< 5, >= n - 5).
@@ -810,3 +864,30 @@ int orc_lego_features(const orc_lego_params* P, const float* orient, const int32
 }
 
 }  // extern "C"
+
+// downSizeFilterSurf (laserMapping.cpp:683-686, 737-739): pcl::VoxelGrid
+// over a cloud's xyz; non-finite points are skipped (PCL with is_dense
+// false).  pcl_order = 0: ties of the voxel index sort by point index (the
+// device's order); 1: PCL 1.10's std::sort order.  Returns the number of
+// centroids written to ox / oy / oz (capacity n).
+extern "C" int64_t orc_voxel_grid_xyz(const float* x, const float* y, const float* z, int64_t n, float leaf,
+                                      int pcl_order, float* ox, float* oy, float* oz) {
+  std::vector<float> xyzi((size_t)n * 4);
+  std::vector<int64_t> pos;
+  for (int64_t i = 0; i < n; ++i) {
+    xyzi[4 * i] = x[i];
+    xyzi[4 * i + 1] = y[i];
+    xyzi[4 * i + 2] = z[i];
+    xyzi[4 * i + 3] = 0.0f;
+    if (std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i])) pos.push_back(i);
+  }
+  std::vector<float> out(pos.size() * 4 + 4);
+  const int64_t m = pcl_order ? voxel_grid_pcl_order(xyzi.data(), pos, leaf, out.data())
+                              : voxel_grid(xyzi.data(), pos, leaf, out.data());
+  for (int64_t k = 0; k < m; ++k) {
+    ox[k] = out[4 * k];
+    oy[k] = out[4 * k + 1];
+    oz[k] = out[4 * k + 2];
+  }
+  return m;
+}

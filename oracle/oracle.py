@@ -52,6 +52,8 @@ def load() -> C.CDLL:
 
 
 def _bind_map(lib):
+    lib.orc_voxel_grid_xyz.restype = C.c_int64
+    lib.orc_voxel_grid_xyz.argtypes = [_FP, _FP, _FP, C.c_int64, C.c_float, C.c_int, _FP, _FP, _FP]
     lib.orc_map_new.restype = C.c_void_p
     lib.orc_map_new.argtypes = [_FP, _FP, _FP, C.c_int64, C.c_float]
     lib.orc_map_free.argtypes = [C.c_void_p]
@@ -217,6 +219,18 @@ class Map:
                                           counts.ctypes.data_as(_I64P))
         assert rc == 0, "map_incremental: neighbour id not in the map"
         return counts
+
+
+def voxel_grid(pts: np.ndarray, leaf: float, pcl_order: bool = False) -> np.ndarray:
+    """pcl::VoxelGrid centroids of a cloud's xyz (laserMapping downSizeFilterSurf)."""
+    p = _f(pts).reshape(-1, 3)
+    x, y, z = (_f(p[:, k]) for k in range(3))
+    n = p.shape[0]
+    ox, oy, oz = (np.zeros(max(n, 1), np.float32) for _ in range(3))
+    m = load().orc_voxel_grid_xyz(x.ctypes.data_as(_FP), y.ctypes.data_as(_FP), z.ctypes.data_as(_FP), n, leaf,
+                                  int(pcl_order), ox.ctypes.data_as(_FP), oy.ctypes.data_as(_FP),
+                                  oz.ctypes.data_as(_FP))
+    return np.stack([ox[:m], oy[:m], oz[:m]], 1)
 
 
 def body_to_world_mat(state26, body):

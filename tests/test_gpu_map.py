@@ -192,3 +192,65 @@ def synth_pos_lid(st):
     # pos + rot * T_LI with the rotation matrix (laserMapping.cpp:729-730)
     from agi_lidar_slam_amd.mapping import _mv, quat_matrix
     return st[0:3] + _mv(quat_matrix(st[3:7]), st[11:14][:, None])[:, 0]
+
+
+@pytest.mark.parametrize("leaf", [0.5, 0.2, 1e-5])
+def test_voxel_grid_vs_oracle(L, oracle_mod, leaf):
+    """downSizeFilterSurf on the device vs the oracle's
+    pcl::VoxelGrid restatement: bit-exact with the same in-voxel order
+    (ascending point index); against PCL 1.10's own std::sort order the voxel
+    list is identical and only voxels of >= 3 points may differ, in the last
+    bits.  leaf 1e-5: the cloud is too large for the voxel index, PCL (and
+    the device) pass the input through.  Non-finite points are dropped."""
+    from agi_lidar_slam_amd import synth
+    from agi_lidar_slam_amd.esekf import Esekf
+    _, fr = synth.make_problem(200000, 20000, pattern="avia")
+    rng = np.random.default_rng(1)
+    raw = np.concatenate([fr.body, fr.body[rng.choice(fr.body.shape[0], 8000)] + rng.normal(0, 0.05, (8000, 3))])
+    raw = raw[rng.permutation(raw.shape[0])].astype(np.float32)
+    raw[::997] = np.nan
+    kf = Esekf(max_points=raw.shape[0])
+    try:
+        n = kf.downsample_scan(raw, leaf)
+        got = kf.feats_down_body()
+        assert got.shape == (n, 3)
+        if leaf < 1e-3:
+            np.testing.assert_array_equal(got, raw)
+            return
+        ref = oracle_mod.voxel_grid(raw, leaf)
+        np.testing.assert_array_equal(got, ref)
+        pcl = oracle_mod.voxel_grid(raw, leaf, pcl_order=True)
+        assert pcl.shape == ref.shape
+        diff = (pcl != ref).any(axis=1)
+        np.testing.assert_allclose(pcl, ref, rtol=4e-7, atol=1e-6)
+        print(f"leaf {leaf}: {n} voxels; centroids differing from PCL's sort order in the last bits: "
+              f"{int(diff.sum())}")
+    finally:
+        kf.close()
+
+
+def test_voxel_scan_feeds_update(L, oracle_mod):
+    """The device-downsampled scan goes straight into the IKF update (no host
+    round trip) and gives the same result as uploading the oracle's
+    downsampled scan."""
+    from agi_lidar_slam_amd import synth
+    from agi_lidar_slam_amd.esekf import Esekf, KdTreeMap, StateIkfom
+    mp, fr = synth.make_problem(200000, 20000, pattern="avia")
+    st = state_of(fr)
+    kd = KdTreeMap(grid_cell=1.25)
+    kd.Build(mp)
+    out = []
+    for dev in (True, False):
+        kf = Esekf(max_points=20000)
+        kf.change_x(StateIkfom.from_array(st))
+        kf.change_P(np.eye(24) * 1e-2)
+        if dev:
+            kf.downsample_scan(fr.body, 0.5)
+            body = None
+        else:
+            body = oracle_mod.voxel_grid(fr.body, 0.5)
+        kf.update_iterated_dyn_share_modified(0.001, body, kd, None, 4, False)
+        out.append(kf.get_x().to_array())
+        kf.close()
+    np.testing.assert_array_equal(out[0], out[1])
+    kd.close()
