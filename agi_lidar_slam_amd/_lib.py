@@ -153,6 +153,15 @@ _U8P = C.POINTER(C.c_uint8)
 _U16P = C.POINTER(C.c_uint16)
 
 # name -> (restype, argtypes); every symbol include/*.h declares
+class SlioImuSample(C.Structure):
+    _fields_ = [("t", C.c_double), ("acc", C.c_double * 3), ("gyr", C.c_double * 3)]
+
+
+class SlioImuPose(C.Structure):
+    _fields_ = [("offset_time", C.c_double), ("acc", C.c_double * 3), ("gyr", C.c_double * 3),
+                ("vel", C.c_double * 3), ("pos", C.c_double * 3), ("rot", C.c_double * 9)]
+
+
 SIGNATURES = {
     "slio_params_default": (C.c_int, [C.POINTER(SlioParams)]),
     "slio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioParams)]),
@@ -162,6 +171,14 @@ SIGNATURES = {
     "slio_map_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
     "slio_map_share": (C.c_int, [_P, _P]),
     "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),
+    "slio_ikf_predict": (C.c_int, [C.POINTER(SlioState), _DP, C.c_double, _DP, _DP, _DP]),
+    "slio_imu_forward": (C.c_int, [C.POINTER(SlioImuSample), C.c_int, C.c_double, C.c_double, _DP, C.c_double,
+                                   _DP, _DP, _DP, _DP, _DP, _DP, C.POINTER(SlioState), _DP,
+                                   C.POINTER(SlioImuPose), C.c_int, _IP]),
+    "slio_undistort": (C.c_int, [_P, _FP, _FP, _FP, _FP, C.c_int64, C.POINTER(SlioImuPose), C.c_int,
+                                 C.POINTER(SlioState), _FP, _FP, _FP, _FP]),
+    "slio_scan_upload_undistort_voxel": (C.c_int, [_P, _FP, _FP, _FP, _FP, C.c_int64, C.POINTER(SlioImuPose),
+                                                   C.c_int, C.POINTER(SlioState), C.c_float, _I64P]),
     "slio_scan_upload_voxel": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_float, _I64P]),
     "slio_scan_download": (C.c_int, [_P, _FP, _FP, _FP]),
     "slio_map_add_points": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_int, C.c_float, _I64P]),

@@ -3780,16 +3780,12 @@ int slio_fov_segment(const double pos_lid[3], float box_min[3], float box_max[3]
   return SLIO_OK;
 }
 
-int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const float* z, int64_t n,
-                           float leaf, int64_t* n_down) {
-  SLIO_CHECK_H(h);
-  Ctx& c = h->c;
-  if (n < 0 || (n > 0 && (!x || !y || !z)) || !(leaf > 0.0f) || n >= (int64_t)0xFFFFFFFFll) {
-    set_error("slio_scan_upload_voxel: bad arguments");
-    return SLIO_EINVAL;
-  }
+}  // extern "C"
+
+// downSizeFilterSurf of n device points (dx_, dy_, dz_) into the handle's scan
+static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float* dz_, int64_t n, float leaf,
+                        int64_t* n_down) {
   hipStream_t st = c.stream;
-  float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr;
   uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *hd = nullptr, *rk = nullptr;
   int32_t* bb = nullptr;
   void* tmp = nullptr;
@@ -3799,8 +3795,7 @@ int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const 
   do {
     if (n == 0) break;
     hipError_t e;
-    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n)) ||
-        (e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
+    if ((e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
         (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&hd, 4 * n)) || (e = hipMalloc(&rk, 4 * n)) ||
         (e = hipMalloc(&bb, 32))) {
       set_error(std::string("slio_scan_upload_voxel: hipMalloc: ") + hipGetErrorString(e));
@@ -3809,10 +3804,7 @@ int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const 
     }
     const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
     int32_t got[8];
-    if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, st)) ||
-        (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, st)) ||
-        (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, st)) ||
-        (e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
+    if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
       set_error(std::string("slio_scan_upload_voxel: H2D: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
@@ -3892,8 +3884,233 @@ int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const 
     c.searched = false;
     if (n_down) *n_down = m;
   }
-  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)hd,
-                  (void*)rk, (void*)bb, tmp})
+  for (void* q : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)hd, (void*)rk, (void*)bb, tmp})
+    if (q) (void)hipFree(q);
+  return rc;
+}
+
+// ---------------------------------------------------------------- scan undistortion
+struct UndistEnd {
+  double R[9], RL[9], TL[3], pos[3];
+};
+
+__global__ void k_time_keys(const float* __restrict__ t, int64_t n, uint32_t* __restrict__ keys,
+                            uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = (uint32_t)fkey(t[i]) ^ 0x80000000u;  // float order as unsigned
+  vals[i] = (uint32_t)i;
+}
+
+// UndistortPcl step 5 (IMU_Processing.hpp:351-401): point i of the time
+// order takes the IMU segment (head k, tail k + 1) with the largest k <=
+// npose - 2 whose offset is below its time -- the segment the reference's
+// backward double loop assigns it -- and is moved to the scan end:
+//   R_i = R_head Exp(gyr_tail dt),  T_ei = pos + vel dt + 0.5 acc dt dt - pos_end,
+//   P' = R_LI^T (R_end^T (R_i (R_LI P + T_LI) + T_ei) - T_LI)
+__global__ void k_undistort(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                            const float* __restrict__ t, const uint32_t* __restrict__ order, int64_t n,
+                            const slio_imu_pose* __restrict__ poses, int np, UndistEnd E, float* __restrict__ ox,
+                            float* __restrict__ oy, float* __restrict__ oz, float* __restrict__ ot) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t o = order[i];
+  const float px = x[o], py = y[o], pz = z[o], pt = t[o];
+  ot[i] = pt;
+  const double tt = (double)pt / double(1000);
+  int lo = -1;
+  if (np >= 2) {
+    int a = 0, b = np - 2;  // largest k in [0, np-2] with offset[k] < tt
+    while (a <= b) {
+      const int m = (a + b) >> 1;
+      if (poses[m].offset_time < tt) {
+        lo = m;
+        a = m + 1;
+      } else {
+        b = m - 1;
+      }
+    }
+  }
+  if (lo < 0) {
+    ox[i] = px;
+    oy[i] = py;
+    oz[i] = pz;
+    return;
+  }
+  // The reference's backward loop leaves its point iterator on the first
+  // point once that point is done ("if (it_pcl == begin) break"), so every
+  // earlier segment whose offset is below that point's time compensates it
+  // again (IMU_Processing.hpp:365-399): mirrored for i == 0.
+  float cx = px, cy = py, cz = pz;
+  const int k_end = (i == 0) ? 0 : lo;
+  for (int k = lo; k >= k_end; --k) {
+    const slio_imu_pose& hd = poses[k];
+    const slio_imu_pose& tl = poses[k + 1];
+    if (!(tt > hd.offset_time)) break;
+    const double dt = tt - hd.offset_time;
+    const double w[3] = {tl.gyr[0] * dt, tl.gyr[1] * dt, tl.gyr[2] * dt};
+    double Ex[9];
+    qmatrix(so3_exp(w), Ex);
+    double Ri[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+        Ri[3 * r + cc] = (hd.rot[3 * r] * Ex[cc] + hd.rot[3 * r + 1] * Ex[3 + cc]) + hd.rot[3 * r + 2] * Ex[6 + cc];
+    const double P[3] = {(double)cx, (double)cy, (double)cz};
+    double Tei[3], a[3], b[3], cv[3], d[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      Tei[q] = ((hd.pos[q] + hd.vel[q] * dt) + ((0.5 * tl.acc[q]) * dt) * dt) - E.pos[q];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      a[r] = ((E.RL[3 * r] * P[0] + E.RL[3 * r + 1] * P[1]) + E.RL[3 * r + 2] * P[2]) + E.TL[r];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) b[r] = ((Ri[3 * r] * a[0] + Ri[3 * r + 1] * a[1]) + Ri[3 * r + 2] * a[2]) + Tei[r];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) cv[r] = ((E.R[r] * b[0] + E.R[3 + r] * b[1]) + E.R[6 + r] * b[2]) - E.TL[r];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) d[r] = (E.RL[r] * cv[0] + E.RL[3 + r] * cv[1]) + E.RL[6 + r] * cv[2];
+    cx = (float)d[0];
+    cy = (float)d[1];
+    cz = (float)d[2];
+  }
+  ox[i] = cx;
+  oy[i] = cy;
+  oz[i] = cz;
+}
+
+// undistorted scan in time order into device arrays ux, uy, uz, ut (n each)
+static int undistort_device(Ctx& c, const float* x, const float* y, const float* z, const float* t, int64_t n,
+                            const slio_imu_pose* poses, int np, const slio_state* xe, float* ux, float* uy, float* uz,
+                            float* ut) {
+  hipStream_t st = c.stream;
+  UndistEnd E;
+  qmatrix(Quat{xe->rot[0], xe->rot[1], xe->rot[2], xe->rot[3]}, E.R);
+  qmatrix(Quat{xe->rli[0], xe->rli[1], xe->rli[2], xe->rli[3]}, E.RL);
+  for (int k = 0; k < 3; ++k) {
+    E.TL[k] = xe->tli[k];
+    E.pos[k] = xe->pos[k];
+  }
+  float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr, *dt_ = nullptr;
+  uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr;
+  slio_imu_pose* dp = nullptr;
+  void* tmp = nullptr;
+  int rc = SLIO_OK;
+  do {
+    hipError_t e;
+    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n)) ||
+        (e = hipMalloc(&dt_, 4 * n)) || (e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) ||
+        (e = hipMalloc(&v0, 4 * n)) || (e = hipMalloc(&v1, 4 * n)) ||
+        (e = hipMalloc(&dp, sizeof(slio_imu_pose) * std::max(np, 1)))) {
+      set_error(std::string("slio undistort: hipMalloc: ") + hipGetErrorString(e));
+      rc = SLIO_ENOMEM;
+      break;
+    }
+    if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(dt_, t, 4 * n, hipMemcpyHostToDevice, st)) ||
+        (np > 0 && (e = hipMemcpyAsync(dp, poses, sizeof(slio_imu_pose) * np, hipMemcpyHostToDevice, st)))) {
+      set_error(std::string("slio undistort: H2D: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    const int nb = grid_blocks(n);
+    k_time_keys<<<nb, 256, 0, st>>>(dt_, n, k0, v0);
+    size_t tb = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
+        (e = hipMalloc(&tmp, tb)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
+      set_error(std::string("slio undistort: sort: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+    k_undistort<<<nb, 256, 0, st>>>(dx_, dy_, dz_, dt_, v1, n, dp, np, E, ux, uy, uz, ut);
+    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+      set_error(std::string("slio undistort: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
+  } while (0);
+  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)dt_, (void*)k0, (void*)k1, (void*)v0, (void*)v1,
+                  (void*)dp, tmp})
+    if (q) (void)hipFree(q);
+  return rc;
+}
+
+extern "C" {
+
+int slio_undistort(slio_handle h, const float* x, const float* y, const float* z, const float* t_ms, int64_t n,
+                   const slio_imu_pose* poses, int npose, const slio_state* x_end, float* ox, float* oy, float* oz,
+                   float* ot_ms) {
+  SLIO_CHECK_H(h);
+  if (n < 0 || (n > 0 && (!x || !y || !z || !t_ms || !ox || !oy || !oz || !ot_ms)) || npose < 0 ||
+      (npose > 0 && !poses) || !x_end || n >= (int64_t)0xFFFFFFFFll) {
+    set_error("slio_undistort: bad arguments");
+    return SLIO_EINVAL;
+  }
+  if (n == 0) return SLIO_OK;
+  Ctx& c = h->c;
+  float* u = nullptr;
+  SLIO_HIP(hipMalloc(&u, 16 * n));
+  int rc = undistort_device(c, x, y, z, t_ms, n, poses, npose, x_end, u, u + n, u + 2 * n, u + 3 * n);
+  if (!rc) {
+    hipError_t e;
+    if ((e = hipMemcpy(ox, u, 4 * n, hipMemcpyDeviceToHost)) || (e = hipMemcpy(oy, u + n, 4 * n, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(oz, u + 2 * n, 4 * n, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(ot_ms, u + 3 * n, 4 * n, hipMemcpyDeviceToHost))) {
+      set_error(std::string("slio_undistort: D2H: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+    }
+  }
+  (void)hipFree(u);
+  return rc;
+}
+
+int slio_scan_upload_undistort_voxel(slio_handle h, const float* x, const float* y, const float* z,
+                                     const float* t_ms, int64_t n, const slio_imu_pose* poses, int npose,
+                                     const slio_state* x_end, float leaf, int64_t* n_down) {
+  SLIO_CHECK_H(h);
+  if (n < 0 || (n > 0 && (!x || !y || !z || !t_ms)) || npose < 0 || (npose > 0 && !poses) || !x_end ||
+      !(leaf > 0.0f) || n >= (int64_t)0xFFFFFFFFll) {
+    set_error("slio_scan_upload_undistort_voxel: bad arguments");
+    return SLIO_EINVAL;
+  }
+  Ctx& c = h->c;
+  float* u = nullptr;
+  if (n > 0) SLIO_HIP(hipMalloc(&u, 16 * n));
+  int rc = n > 0 ? undistort_device(c, x, y, z, t_ms, n, poses, npose, x_end, u, u + n, u + 2 * n, u + 3 * n)
+                 : SLIO_OK;
+  if (!rc) rc = voxel_device(c, u, u ? u + n : nullptr, u ? u + 2 * n : nullptr, n, leaf, n_down);
+  if (u) (void)hipFree(u);
+  return rc;
+}
+
+int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const float* z, int64_t n,
+                           float leaf, int64_t* n_down) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (n < 0 || (n > 0 && (!x || !y || !z)) || !(leaf > 0.0f) || n >= (int64_t)0xFFFFFFFFll) {
+    set_error("slio_scan_upload_voxel: bad arguments");
+    return SLIO_EINVAL;
+  }
+  float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr;
+  int rc = SLIO_OK;
+  if (n > 0) {
+    hipError_t e;
+    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n))) {
+      set_error(std::string("slio_scan_upload_voxel: hipMalloc: ") + hipGetErrorString(e));
+      rc = SLIO_ENOMEM;
+    } else if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
+               (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
+               (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, c.stream))) {
+      set_error(std::string("slio_scan_upload_voxel: H2D: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+    }
+  }
+  if (!rc) rc = voxel_device(c, dx_, dy_, dz_, n, leaf, n_down);
+  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_})
     if (q) (void)hipFree(q);
   return rc;
 }

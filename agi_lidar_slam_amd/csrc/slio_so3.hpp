@@ -42,6 +42,19 @@ SLIO_HD inline Quat qnormalized(const Quat& q) {
   return Quat{q.w / n, q.x / n, q.y / n, q.z / n};
 }
 
+// SO3 * vector: Eigen QuaternionBase::_transformVector
+//   uv = vec x v; uv += uv; return v + w * uv + vec x uv
+SLIO_HD inline void qrotate(const Quat& q, const double v[3], double o[3]) {
+  double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+  uv[0] = uv[0] + uv[0];
+  uv[1] = uv[1] + uv[1];
+  uv[2] = uv[2] + uv[2];
+  const double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]};
+  o[0] = (v[0] + q.w * uv[0]) + c[0];
+  o[1] = (v[1] + q.w * uv[1]) + c[1];
+  o[2] = (v[2] + q.w * uv[2]) + c[2];
+}
+
 // row-major 3x3
 SLIO_HD inline void qmatrix(const Quat& q, double R[9]) {
   const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;

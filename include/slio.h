@@ -299,6 +299,58 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
                            slio_allreduce_fn reduce, void* reduce_ctx,
                            slio_ikf_stats* stats);
 
+/* ---- IMU forward propagation and scan undistortion (ImuProcess::UndistortPcl,
+ *      src/S-FAST_LIO/src/IMU_Processing.hpp:253-402) ------------------------ */
+/* One IMU sample: stamp (s), linear acceleration, angular velocity. */
+typedef struct slio_imu_sample {
+  double t;
+  double acc[3];
+  double gyr[3];
+} slio_imu_sample;
+/* Pose6D (common_lib.h / set_pose6d): offset from the scan start (s), the
+ * world-frame acceleration and bias-free angular velocity at that sample,
+ * velocity, position, rotation matrix (row-major). */
+typedef struct slio_imu_pose {
+  double offset_time;
+  double acc[3];
+  double gyr[3];
+  double vel[3];
+  double pos[3];
+  double rot[9];
+} slio_imu_pose;
+/* esekf::predict (esekfom.hpp:82-95) with the process model of
+ * use-ikfom.hpp (get_f, df_dx, df_dw): x [+]= f dt, P = F P F^T + G Q G^T. */
+int slio_ikf_predict(slio_state* x, double P[576], double dt, const double Q[144],
+                     const double acc[3], const double gyr[3]);
+/* UndistortPcl steps 1-4 (IMU_Processing.hpp:253-346), host: forward
+ * propagation over imu[0..nimu) (imu[0] = the previous scan's last sample,
+ * last_imu_, then meas.imu), predicting x / P in place; writes the IMUpose
+ * table (*npose <= nimu entries).  acc_s_last / angvel_last /
+ * last_lidar_end_time are the ImuProcess members carried between scans. */
+int slio_imu_forward(const slio_imu_sample* imu, int nimu, double pcl_beg_time,
+                     double pcl_end_time, double* last_lidar_end_time,
+                     double mean_acc_norm, const double cov_gyr[3],
+                     const double cov_acc[3], const double cov_bias_gyr[3],
+                     const double cov_bias_acc[3], double acc_s_last[3],
+                     double angvel_last[3], slio_state* x, double P[576],
+                     slio_imu_pose* poses, int cap, int* npose);
+/* UndistortPcl step 5 (IMU_Processing.hpp:351-401) on the device: the raw
+ * scan (x, y, z float32, t = per-point time offset in ms, the `curvature`
+ * field of preprocess) sorted by time, every point with t / 1000 > the first
+ * pose's offset moved to the scan end state x_end by the IMU pose segment it
+ * falls in.  Results (feats_undistort, time order) to the host arrays. */
+int slio_undistort(slio_handle h, const float* x, const float* y, const float* z,
+                   const float* t_ms, int64_t n, const slio_imu_pose* poses,
+                   int npose, const slio_state* x_end, float* ox, float* oy,
+                   float* oz, float* ot_ms);
+/* The same undistortion, then downSizeFilterSurf (see slio_scan_upload_voxel)
+ * without leaving the device: the result is the handle's scan. */
+int slio_scan_upload_undistort_voxel(slio_handle h, const float* x, const float* y,
+                                     const float* z, const float* t_ms, int64_t n,
+                                     const slio_imu_pose* poses, int npose,
+                                     const slio_state* x_end, float leaf,
+                                     int64_t* n_down);
+
 /* Manifold helpers exported for tests (esekfom.hpp:59-73, 236-258). */
 int slio_state_boxplus(const slio_state* x, const double dx[24], slio_state* out);
 int slio_state_boxminus(const slio_state* x1, const slio_state* x2, double dx[24]);

@@ -23,7 +23,7 @@ _lib = None
 
 
 def build() -> str:
-    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "map_oracle.cpp",
+    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "map_oracle.cpp", "imu_oracle.cpp",
                                             "Makefile")]
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
@@ -52,6 +52,9 @@ def load() -> C.CDLL:
 
 
 def _bind_map(lib):
+    lib.orc_imu_undistort.argtypes = [_DP, C.c_int, C.c_double, C.c_double, _DP, C.c_double, _DP, _DP, _DP,
+                                      _DP, _DP, _FP, _FP, _FP, _FP, C.c_int64, _FP, _FP, _FP, _FP, _DP,
+                                      C.POINTER(C.c_int)]
     lib.orc_voxel_grid_xyz.restype = C.c_int64
     lib.orc_voxel_grid_xyz.argtypes = [_FP, _FP, _FP, C.c_int64, C.c_float, C.c_int, _FP, _FP, _FP]
     lib.orc_map_new.restype = C.c_void_p
@@ -219,6 +222,38 @@ class Map:
                                           counts.ctypes.data_as(_I64P))
         assert rc == 0, "map_incremental: neighbour id not in the map"
         return counts
+
+
+def imu_undistort(imu: np.ndarray, pcl_beg: float, pcl_end: float, last_lidar_end: float, mean_acc_norm: float,
+                  cov12: np.ndarray, acc_s_last: np.ndarray, angvel_last: np.ndarray, state26: np.ndarray,
+                  P: np.ndarray, pts: np.ndarray, t_ms: np.ndarray):
+    """ImuProcess::UndistortPcl restated; imu (k, 7) = t, acc xyz, gyr xyz (the
+    previous scan's last sample first).  Returns a dict with the undistorted
+    points (time order), their times, the predicted state / P, the IMUpose
+    table (k, 22) and the members carried to the next scan."""
+    im = np.ascontiguousarray(imu, dtype=np.float64)
+    st = np.ascontiguousarray(state26, dtype=np.float64).copy()
+    Pm = np.ascontiguousarray(P, dtype=np.float64).copy()
+    asl = np.ascontiguousarray(acc_s_last, dtype=np.float64).copy()
+    avl = np.ascontiguousarray(angvel_last, dtype=np.float64).copy()
+    cov = np.ascontiguousarray(cov12, dtype=np.float64)
+    lle = C.c_double(last_lidar_end)
+    p = _f(pts).reshape(-1, 3)
+    n = p.shape[0]
+    x, y, z = (_f(p[:, k]) for k in range(3))
+    t = _f(t_ms)
+    ox, oy, oz, ot = (np.zeros(max(n, 1), np.float32) for _ in range(4))
+    poses = np.zeros((im.shape[0], 22))
+    npose = C.c_int()
+    load().orc_imu_undistort(im.ctypes.data_as(_DP), im.shape[0], pcl_beg, pcl_end, C.byref(lle), mean_acc_norm,
+                             cov.ctypes.data_as(_DP), asl.ctypes.data_as(_DP), avl.ctypes.data_as(_DP),
+                             st.ctypes.data_as(_DP), Pm.ctypes.data_as(_DP), x.ctypes.data_as(_FP),
+                             y.ctypes.data_as(_FP), z.ctypes.data_as(_FP), t.ctypes.data_as(_FP), n,
+                             ox.ctypes.data_as(_FP), oy.ctypes.data_as(_FP), oz.ctypes.data_as(_FP),
+                             ot.ctypes.data_as(_FP), poses.ctypes.data_as(_DP), C.byref(npose))
+    return {"points": np.stack([ox[:n], oy[:n], oz[:n]], 1), "t_ms": ot[:n], "state": st, "P": Pm,
+            "poses": poses[:npose.value], "acc_s_last": asl, "angvel_last": avl,
+            "last_lidar_end_time": lle.value}
 
 
 def voxel_grid(pts: np.ndarray, leaf: float, pcl_order: bool = False) -> np.ndarray:

@@ -12,6 +12,8 @@ while [ $# -gt 0 ]; do
          rc=$?; echo "runtime rc=$rc"; tail -15 gpurun_out/${tag}_runtime.log; [ $rc -eq 0 ] || exit $rc ;;
     map) timeout -k 10 600 python -u -m pytest tests/test_gpu_map.py -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/${tag}_map.log 2>&1
          rc=$?; echo "map rc=$rc"; tail -25 gpurun_out/${tag}_map.log; [ $rc -eq 0 ] || exit $rc ;;
+    imu) timeout -k 10 300 python -u -m pytest tests/test_gpu_imu.py -m gpu -x -v -s --timeout 200 --timeout-method thread > gpurun_out/${tag}_imu.log 2>&1
+         rc=$?; echo "imu rc=$rc"; tail -25 gpurun_out/${tag}_imu.log; [ $rc -eq 0 ] || exit $rc ;;
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
          rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/${tag}_tests.log; [ $rc -eq 0 ] || exit $rc ;;
     stats) shift; timeout -k 10 600 python -u scripts/far_stats.py $1 > gpurun_out/${tag}_stats.log 2>&1
