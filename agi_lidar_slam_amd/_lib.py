@@ -179,6 +179,10 @@ SIGNATURES = {
                                  C.POINTER(SlioState), _FP, _FP, _FP, _FP]),
     "slio_scan_upload_undistort_voxel": (C.c_int, [_P, _FP, _FP, _FP, _FP, C.c_int64, C.POINTER(SlioImuPose),
                                                    C.c_int, C.POINTER(SlioState), C.c_float, _I64P]),
+    "slio_s2m_coeffs": (C.c_int, [_P, C.c_int, _FP, _I64P]),
+    "slio_s2m_get_coeffs": (C.c_int, [_P, _FP, _U8P]),
+    "slio_s2m_normal_equations": (C.c_int, [_P, _P, _FP, _FP, _FP, _I64P]),
+    "slio_s2m_lm_step": (C.c_int, [_FP, _FP, C.c_int64, C.c_int, _FP, _IP, _FP, _IP]),
     "slio_scan_upload_voxel": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_float, _I64P]),
     "slio_scan_download": (C.c_int, [_P, _FP, _FP, _FP]),
     "slio_map_add_points": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64, C.c_int, C.c_float, _I64P]),

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libslio.so")
 
-SOURCES = ["slio_device.hip", "slio_ikf.cpp", "slio_imu.cpp", "slio_lio.hip"]
+SOURCES = ["slio_device.hip", "slio_ikf.cpp", "slio_imu.cpp", "slio_s2m.cpp", "slio_lio.hip"]
 HEADERS = ["slio_common.hpp", "slio_plane.hpp", "slio_so3.hpp"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

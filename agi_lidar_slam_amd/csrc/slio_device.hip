@@ -933,6 +933,7 @@ struct PassCfg {
   int extrinsic;
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
+  int knn_only;            // 1: neighbours only (nbr_*), no fit / rows / products
 };
 
 // ---------------------------------------------------------------- far queries
@@ -1962,6 +1963,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         out.nbr_idx[i * 5 + j] = (int32_t)__float_as_uint(c.w);
         out.nbr_pos[i * 5 + j] = ps;
       }
+      if (cfg.knn_only) sel = false;
       if (sel) {
         float pl[4];
         sel = esti_plane_dev(nb, cfg.plane_thr, pl);
@@ -1989,6 +1991,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __syncthreads();
   if (tid == 0) STAMP(2);
   // ---------------- phase 3: fixed-order products
+  if (cfg.knn_only) return;
   chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
   if (tid == 0) STAMP(3);
 }
@@ -2165,6 +2168,10 @@ struct Ctx {
   int32_t* nbr_idx = nullptr;
   uint32_t* nbr_pos = nullptr;
   uint64_t search_version = 0;  // map version the last search pass ran on
+  float* wbx = nullptr;  // scan-to-map: the scan in the map frame
+  float* wby = nullptr;
+  float* wbz = nullptr;
+  int s2m_kind = -1;
   float* nbr_sqd = nullptr;
   float4* plane = nullptr;
   uint8_t* sel = nullptr;
@@ -2267,6 +2274,10 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->nbr_idx);
   (void)hipFree(c->nbr_pos);
   c->nbr_pos = nullptr;
+  (void)hipFree(c->wbx);
+  (void)hipFree(c->wby);
+  (void)hipFree(c->wbz);
+  c->wbx = c->wby = c->wbz = nullptr;
   (void)hipFree(c->nbr_sqd);
   (void)hipFree(c->plane);
   (void)hipFree(c->sel);
@@ -2338,7 +2349,7 @@ static int map_refresh(Ctx& c, bool adds_only = false);
 
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
                         int extrinsic_est, const SolveArgs* sa = nullptr,
-                        bool with_super = true) {
+                        bool with_super = true, bool knn_only = false, const ScanDev* sd = nullptr) {
   if (!c.map) {
     set_error("slio pass: no map uploaded");
     return SLIO_ESTATE;
@@ -2371,10 +2382,11 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_begin = c0;
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
+  cfg.knn_only = knn_only ? 1 : 0;
   if (int rc = map_refresh(c); rc) return rc;
   PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane, c.sel, c.resid,
             c.chunk_part, c.count + 4};
-  ScanDev s{c.bx, c.by, c.bz, c.n};
+  ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
   if (c.prof && (c.pending[0].size() + c.pending[1].size()) > 256) prof_drain(c);
@@ -3888,6 +3900,397 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
     if (q) (void)hipFree(q);
   return rc;
 }
+
+// ---------------------------------------------------------------- LIO-SAM scan-to-map
+// mapOptmization.cpp cornerOptimization (:1303-1432), surfOptimization
+// (:1438-1515) and the rows / normal equations of LMOptimization
+// (:1552-1626) on the device; the 6x6 solve stays on the host
+// (slio_s2m_lm_step).  One handle per feature class: its map is
+// laserCloud{Corner,Surf}FromMapDS, its scan laserCloud{Corner,Surf}LastDS.
+
+// pointAssociateToMap (:359-373) with the float affine of
+// pcl::getTransformation(transformTobeMapped)
+struct Aff12 {
+  float m[12];
+};
+__global__ void k_s2m_transform(const float* __restrict__ bx, const float* __restrict__ by,
+                                const float* __restrict__ bz, int64_t n, Aff12 T, float* __restrict__ wx,
+                                float* __restrict__ wy, float* __restrict__ wz) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = bx[i], y = by[i], z = bz[i];
+  wx[i] = ((T.m[0] * x + T.m[1] * y) + T.m[2] * z) + T.m[3];
+  wy[i] = ((T.m[4] * x + T.m[5] * y) + T.m[6] * z) + T.m[7];
+  wz[i] = ((T.m[8] * x + T.m[9] * y) + T.m[10] * z) + T.m[11];
+}
+
+// OpenCV's hypot (lapack.cpp): scaled, in the element type
+__device__ __forceinline__ float cv_hypot(float a, float b) {
+  a = fabsf(a);
+  b = fabsf(b);
+  if (a > b) {
+    b /= a;
+    return a * sqrtf(1 + b * b);
+  }
+  if (b > 0) {
+    a /= b;
+    return b * sqrtf(1 + a * a);
+  }
+  return 0;
+}
+
+// cv::eigen of a symmetric 3x3 float matrix: OpenCV hal::Jacobi
+// (JacobiImpl_, lapack.cpp) -- eigenvalues W descending, eigenvectors the
+// rows of V.  Fully unrolled over compile-time indices (n = 3).
+__device__ __forceinline__ void cv_jacobi3(float A[9], float W[3], float V[9]) {
+  const float eps = 1.1920928955078125e-07f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+  int indR[3], indC[3];
+  W[0] = A[0];
+  W[1] = A[4];
+  W[2] = A[8];
+  // k = 0: row max over cols 1..2; k = 1: col 2 and column max over rows 0
+  indR[0] = (fabsf(A[1]) < fabsf(A[2])) ? 2 : 1;
+  indR[1] = 2;
+  indC[1] = 0;
+  indC[2] = (fabsf(A[2]) < fabsf(A[5])) ? 1 : 0;
+  for (int iters = 0; iters < 3 * 3 * 30; ++iters) {
+    int k = 0;
+    float mv = fabsf(A[indR[0]]);
+    {
+      const float val = fabsf(A[3 + indR[1]]);
+      if (mv < val) mv = val, k = 1;
+    }
+    int l = indR[k];
+    for (int i = 1; i < 3; ++i) {
+      const float val = fabsf(A[3 * indC[i] + i]);
+      if (mv < val) mv = val, k = indC[i], l = i;
+    }
+    const float p = A[3 * k + l];
+    if (fabsf(p) <= eps) break;
+    float y = (float)((W[l] - W[k]) * 0.5);
+    float t = fabsf(y) + cv_hypot(p, y);
+    float sn = cv_hypot(p, t);
+    const float c = t / sn;
+    sn = p / sn;
+    t = (p / t) * p;
+    if (y < 0) sn = -sn, t = -t;
+    A[3 * k + l] = 0;
+    W[k] -= t;
+    W[l] += t;
+    float a0, b0;
+#define SLIO_ROT(v0, v1) a0 = v0, b0 = v1, v0 = a0 * c - b0 * sn, v1 = a0 * sn + b0 * c
+    for (int i = 0; i < k; ++i) SLIO_ROT(A[3 * i + k], A[3 * i + l]);
+    for (int i = k + 1; i < l; ++i) SLIO_ROT(A[3 * k + i], A[3 * i + l]);
+    for (int i = l + 1; i < 3; ++i) SLIO_ROT(A[3 * k + i], A[3 * l + i]);
+    for (int i = 0; i < 3; ++i) SLIO_ROT(V[3 * k + i], V[3 * l + i]);
+#undef SLIO_ROT
+    for (int j = 0; j < 2; ++j) {
+      const int idx = j == 0 ? k : l;
+      if (idx < 2) {
+        int m = idx + 1;
+        float mvv = fabsf(A[3 * idx + m]);
+        for (int i = idx + 2; i < 3; ++i) {
+          const float val = fabsf(A[3 * idx + i]);
+          if (mvv < val) mvv = val, m = i;
+        }
+        indR[idx] = m;
+      }
+      if (idx > 0) {
+        int m = 0;
+        float mvv = fabsf(A[idx]);
+        for (int i = 1; i < idx; ++i) {
+          const float val = fabsf(A[3 * i + idx]);
+          if (mvv < val) mvv = val, m = i;
+        }
+        indC[idx] = m;
+      }
+    }
+  }
+  for (int k = 0; k < 2; ++k) {
+    int m = k;
+    for (int i = k + 1; i < 3; ++i)
+      if (W[m] < W[i]) m = i;
+    if (k != m) {
+      const float tw = W[m];
+      W[m] = W[k];
+      W[k] = tw;
+      for (int i = 0; i < 3; ++i) {
+        const float tv = V[3 * m + i];
+        V[3 * m + i] = V[3 * k + i];
+        V[3 * k + i] = tv;
+      }
+    }
+  }
+}
+
+// coefficients (coeff.x, y, z, intensity) and selection of every scan point
+template <int KIND>  // 0: corner (point-to-line), 1: surf (point-to-plane)
+__global__ void k_s2m_coeff(const float* __restrict__ wx, const float* __restrict__ wy,
+                            const float* __restrict__ wz, int64_t n, const uint32_t* __restrict__ nbr_pos,
+                            const float* __restrict__ nbr_sqd, const float4* __restrict__ pts,
+                            float4* __restrict__ coeff, uint8_t* __restrict__ sel) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t ok = 0;
+  float4 cf = make_float4(0, 0, 0, 0);
+  const float x0 = wx[i], y0 = wy[i], z0 = wz[i];
+  if (nbr_sqd[i * 5 + 4] < 1.0f) {  // (< 1.0 is false for +inf: fewer than 5 map points)
+    float nb[5][3];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const float4 p = pts[nbr_pos[i * 5 + j]];
+      nb[j][0] = p.x;
+      nb[j][1] = p.y;
+      nb[j][2] = p.z;
+    }
+    if (KIND == 0) {
+      float cx = 0, cy = 0, cz = 0;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        cx += nb[j][0];
+        cy += nb[j][1];
+        cz += nb[j][2];
+      }
+      cx /= 5;
+      cy /= 5;
+      cz /= 5;
+      float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const float ax = nb[j][0] - cx, ay = nb[j][1] - cy, az = nb[j][2] - cz;
+        a11 += ax * ax;
+        a12 += ax * ay;
+        a13 += ax * az;
+        a22 += ay * ay;
+        a23 += ay * az;
+        a33 += az * az;
+      }
+      a11 /= 5;
+      a12 /= 5;
+      a13 /= 5;
+      a22 /= 5;
+      a23 /= 5;
+      a33 /= 5;
+      float A[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33}, W[3], V[9];
+      cv_jacobi3(A, W, V);
+      if (W[0] > 3 * W[1]) {
+        const float x1 = cx + 0.1 * V[0], y1 = cy + 0.1 * V[1], z1 = cz + 0.1 * V[2];
+        const float x2 = cx - 0.1 * V[0], y2 = cy - 0.1 * V[1], z2 = cz - 0.1 * V[2];
+        const float u = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+        const float v = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+        const float w = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+        const float a012 = sqrtf(u * u + v * v + w * w);
+        const float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+        const float la = ((y1 - y2) * u + (z1 - z2) * v) / a012 / l12;
+        const float lb = -((x1 - x2) * u - (z1 - z2) * w) / a012 / l12;
+        const float lc = -((x1 - x2) * v + (y1 - y2) * w) / a012 / l12;
+        const float ld2 = a012 / l12;
+        const float s = 1 - 0.9 * fabsf(ld2);
+        cf = make_float4(s * la, s * lb, s * lc, s * ld2);
+        ok = s > 0.1;
+      }
+    } else {
+      float sol[3];
+      qr_solve_m1_dev(nb, sol);
+      float pa = sol[0], pb = sol[1], pc = sol[2], pd = 1;
+      const float ps = sqrtf(pa * pa + pb * pb + pc * pc);
+      pa /= ps;
+      pb /= ps;
+      pc /= ps;
+      pd /= ps;
+      bool valid = true;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (fabsf(pa * nb[j][0] + pb * nb[j][1] + pc * nb[j][2] + pd) > 0.2) valid = false;
+      if (valid) {
+        const float pd2 = pa * x0 + pb * y0 + pc * z0 + pd;
+        const float s = 1 - 0.9 * fabsf(pd2) / sqrtf(sqrtf(x0 * x0 + y0 * y0 + z0 * z0));
+        cf = make_float4(s * pa, s * pb, s * pc, s * pd2);
+        ok = s > 0.1;
+      }
+    }
+  }
+  coeff[i] = cf;
+  sel[i] = ok;
+}
+
+// LMOptimization rows (:1583-1626, lidar <-> camera axis swap included) of the
+// selected points and their A^T A (21) / A^T B (6) / count, summed in double:
+// each workgroup its 256 points in a fixed tree, one partial per workgroup
+struct S2mTrig {
+  float srx, crx, sry, cry, srz, crz;
+};
+constexpr int kS2mSums = 28;
+__global__ __launch_bounds__(256) void k_s2m_rows(const float* __restrict__ bx, const float* __restrict__ by,
+                                                  const float* __restrict__ bz, const float4* __restrict__ coeff,
+                                                  const uint8_t* __restrict__ sel, int64_t n, S2mTrig T,
+                                                  double* __restrict__ partial) {
+  __shared__ double red[256];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double v[kS2mSums];
+#pragma unroll
+  for (int k = 0; k < kS2mSums; ++k) v[k] = 0.0;
+  if (i < n && sel[i]) {
+    const float4 cs = coeff[i];
+    const float px = by[i], py = bz[i], pz = bx[i];   // lidar -> camera
+    const float cx = cs.y, cy = cs.z, cz = cs.x, ci = cs.w;
+    const float srx = T.srx, crx = T.crx, sry = T.sry, cry = T.cry, srz = T.srz, crz = T.crz;
+    const float arx = (crx * sry * srz * px + crx * crz * sry * py - srx * sry * pz) * cx +
+                      (-srx * srz * px - crz * srx * py - crx * pz) * cy +
+                      (crx * cry * srz * px + crx * cry * crz * py - cry * srx * pz) * cz;
+    const float ary = ((cry * srx * srz - crz * sry) * px + (sry * srz + cry * crz * srx) * py + crx * cry * pz) * cx +
+                      ((-cry * crz - srx * sry * srz) * px + (cry * srz - crz * srx * sry) * py - crx * sry * pz) * cz;
+    const float arz = ((crz * srx * sry - cry * srz) * px + (-cry * crz - srx * sry * srz) * py) * cx +
+                      (crx * crz * px - crx * srz * py) * cy +
+                      ((sry * srz + cry * crz * srx) * px + (crz * sry - cry * srx * srz) * py) * cz;
+    const float a[6] = {arz, arx, ary, cz, cx, cy};
+    const float b = -ci;
+    int q = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = r; c < 6; ++c) v[q++] = (double)a[r] * (double)a[c];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) v[21 + r] = (double)a[r] * (double)b;
+    v[27] = 1.0;
+  }
+  for (int k = 0; k < kS2mSums; ++k) {
+    red[threadIdx.x] = v[k];
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if (threadIdx.x < st) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + st];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[(int64_t)blockIdx.x * kS2mSums + k] = red[0];
+    __syncthreads();
+  }
+}
+
+// pcl::getTransformation (pcl/common/impl/eigen.hpp) in float, the trig
+// correctly rounded (evaluated in double)
+static Aff12 s2m_affine(const float tf[6]) {
+  const float x = tf[3], y = tf[4], z = tf[5], roll = tf[0], pitch = tf[1], yaw = tf[2];
+  auto fc = [](float a) { return (float)std::cos((double)a); };
+  auto fs = [](float a) { return (float)std::sin((double)a); };
+  const float A = fc(yaw), B = fs(yaw), C = fc(pitch), D = fs(pitch), E = fc(roll), F = fs(roll), DE = D * E,
+              DF = D * F;
+  Aff12 t;
+  t.m[0] = A * C, t.m[1] = A * DF - B * E, t.m[2] = B * F + A * DE, t.m[3] = x;
+  t.m[4] = B * C, t.m[5] = A * E + B * DF, t.m[6] = B * DE - A * F, t.m[7] = y;
+  t.m[8] = -D, t.m[9] = C * F, t.m[10] = C * E, t.m[11] = z;
+  return t;
+}
+
+extern "C" {
+
+int slio_s2m_coeffs(slio_handle h, int kind, const float transform[6], int64_t* nsel) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if ((kind != 0 && kind != 1) || !transform) {
+    set_error("slio_s2m_coeffs: bad arguments");
+    return SLIO_EINVAL;
+  }
+  if (!c.map || !c.bx) {
+    set_error("slio_s2m_coeffs: map and scan needed");
+    return SLIO_ESTATE;
+  }
+  if (c.prm.nranks != 1) {
+    set_error("slio_s2m_coeffs: single-rank handles only");
+    return SLIO_EINVAL;
+  }
+  const int64_t n = c.n;
+  if (!c.wbx) {
+    const int64_t cap = c.prm.max_points;
+    hipError_t e;
+    if ((e = hipMalloc(&c.wbx, 4 * cap)) || (e = hipMalloc(&c.wby, 4 * cap)) || (e = hipMalloc(&c.wbz, 4 * cap))) {
+      set_error(std::string("slio_s2m_coeffs: hipMalloc: ") + hipGetErrorString(e));
+      return SLIO_ENOMEM;
+    }
+  }
+  if (n > 0) {
+    k_s2m_transform<<<grid_blocks(n), 256, 0, c.stream>>>(c.bx, c.by, c.bz, n, s2m_affine(transform), c.wbx,
+                                                           c.wby, c.wbz);
+    // the 5-NN of the world points: the search pass in kNN-only mode with the
+    // identity pose (body -> world of an identity pose is exact in float)
+    slio_pose idp{};
+    idp.rot[0] = 1.0;
+    idp.rli[0] = 1.0;
+    const PoseDev P = make_pose(&idp);
+    const ScanDev sd{c.wbx, c.wby, c.wbz, n};
+    if (int rc = enqueue_pass(c, &P, nullptr, 1, 0, nullptr, false, true, &sd)) return rc;
+    if (kind == 0)
+      k_s2m_coeff<0><<<grid_blocks(n), 256, 0, c.stream>>>(c.wbx, c.wby, c.wbz, n, c.nbr_pos, c.nbr_sqd,
+                                                            c.map->pts, c.plane, c.sel);
+    else
+      k_s2m_coeff<1><<<grid_blocks(n), 256, 0, c.stream>>>(c.wbx, c.wby, c.wbz, n, c.nbr_pos, c.nbr_sqd,
+                                                            c.map->pts, c.plane, c.sel);
+    SLIO_HIP(hipGetLastError());
+  }
+  c.s2m_kind = kind;
+  if (nsel) {
+    std::vector<uint8_t> sl((size_t)n);
+    if (n) {
+      SLIO_HIP(hipStreamSynchronize(c.stream));
+      SLIO_HIP(hipMemcpy(sl.data(), c.sel, n, hipMemcpyDeviceToHost));
+    }
+    int64_t k = 0;
+    for (uint8_t v : sl) k += v;
+    *nsel = k;
+  }
+  return SLIO_OK;
+}
+
+int slio_s2m_get_coeffs(slio_handle h, float* coeff, uint8_t* sel) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (c.n > 0) {
+    SLIO_HIP(hipStreamSynchronize(c.stream));
+    if (coeff) SLIO_HIP(hipMemcpy(coeff, c.plane, 16 * c.n, hipMemcpyDeviceToHost));
+    if (sel) SLIO_HIP(hipMemcpy(sel, c.sel, c.n, hipMemcpyDeviceToHost));
+  }
+  return SLIO_OK;
+}
+
+int slio_s2m_normal_equations(slio_handle h_corner, slio_handle h_surf, const float transform[6], float AtA[36],
+                              float AtB[6], int64_t* nsel) {
+  if (!transform || !AtA || !AtB) {
+    set_error("slio_s2m_normal_equations: bad arguments");
+    return SLIO_EINVAL;
+  }
+  // the camera-frame trig of LMOptimization (:1564-1569), float sin / cos
+  S2mTrig T;
+  auto fc = [](float a) { return (float)std::cos((double)a); };
+  auto fs = [](float a) { return (float)std::sin((double)a); };
+  T.srx = fs(transform[1]), T.crx = fc(transform[1]);
+  T.sry = fs(transform[2]), T.cry = fc(transform[2]);
+  T.srz = fs(transform[0]), T.crz = fc(transform[0]);
+  double acc[kS2mSums] = {0};
+  // corners first, then surfs (combineOptimizationCoeffs :1517-1543)
+  for (slio_handle h : {h_corner, h_surf}) {
+    if (!h) continue;
+    Ctx& c = h->c;
+    const int64_t n = c.n;
+    if (n == 0) continue;
+    const int nb = (int)((n + 255) / 256);
+    k_s2m_rows<<<nb, 256, 0, c.stream>>>(c.bx, c.by, c.bz, c.plane, c.sel, n, T, c.chunk_part);
+    std::vector<double> part((size_t)nb * kS2mSums);
+    SLIO_HIP(hipGetLastError());
+    SLIO_HIP(hipStreamSynchronize(c.stream));
+    SLIO_HIP(hipMemcpy(part.data(), c.chunk_part, 8 * part.size(), hipMemcpyDeviceToHost));
+    for (int b = 0; b < nb; ++b)
+      for (int k = 0; k < kS2mSums; ++k) acc[k] = acc[k] + part[(size_t)b * kS2mSums + k];
+  }
+  int q = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int cc = r; cc < 6; ++cc, ++q) AtA[6 * r + cc] = AtA[6 * cc + r] = (float)acc[q];
+  for (int r = 0; r < 6; ++r) AtB[r] = (float)acc[21 + r];
+  if (nsel) *nsel = (int64_t)llround(acc[27]);
+  return SLIO_OK;
+}
+
+}  // extern "C"
 
 // ---------------------------------------------------------------- scan undistortion
 struct UndistEnd {

@@ -39,8 +39,8 @@ __device__ __forceinline__ void cond_swap_cols(float (&a)[3][5], float (&nu)[3],
 
 // nb[j] = (x, y, z) of neighbour j in ascending-distance order.
 // Returns true and fills abcd when the plane is accepted.
-__device__ __forceinline__ bool esti_plane_dev(const float (&nb)[5][3],
-                                               float threshold, float (&abcd)[4]) {
+// A x = -1 for the 5x3 A of the neighbours (ColPivHouseholderQR solve)
+__device__ __forceinline__ void qr_solve_m1_dev(const float (&nb)[5][3], float (&sol)[3]) {
   constexpr float kEps = 1.1920928955078125e-07f;    // FLT_EPSILON
   constexpr float kTiny = 1.17549435082228750797e-38f; // FLT_MIN
   float a[3][5];
@@ -162,7 +162,7 @@ __device__ __forceinline__ bool esti_plane_dev(const float (&nb)[5][3],
     perm[k] = pt;
   }
 
-  float sol[3] = {0.0f, 0.0f, 0.0f};
+  sol[0] = sol[1] = sol[2] = 0.0f;
   if (nzp > 0) {
     float c[5] = {-1.0f, -1.0f, -1.0f, -1.0f, -1.0f};
     // c = Q^T c : H_0 first
@@ -199,6 +199,12 @@ __device__ __forceinline__ bool esti_plane_dev(const float (&nb)[5][3],
     }
   }
 
+}
+
+__device__ __forceinline__ bool esti_plane_dev(const float (&nb)[5][3],
+                                               float threshold, float (&abcd)[4]) {
+  float sol[3];
+  qr_solve_m1_dev(nb, sol);
   const float n = sqrtf((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
   abcd[0] = sol[0] / n;
   abcd[1] = sol[1] / n;

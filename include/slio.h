@@ -351,6 +351,33 @@ int slio_scan_upload_undistort_voxel(slio_handle h, const float* x, const float*
                                      const slio_state* x_end, float leaf,
                                      int64_t* n_down);
 
+/* ---- LIO-SAM scan-to-map (src/LIO-SAM/src/mapOptmization.cpp) -------------
+ * One handle per feature class: map = laserCloud{Corner,Surf}FromMapDS
+ * (slio_map_upload), scan = laserCloud{Corner,Surf}LastDS (slio_scan_upload). */
+/* cornerOptimization (kind 0, :1303-1432) / surfOptimization (kind 1,
+ * :1438-1515) at transformTobeMapped = {roll, pitch, yaw, x, y, z}:
+ * pointAssociateToMap, exact 5-NN in the handle's map, point-to-line (3x3
+ * covariance, cv::eigen restated as OpenCV's Jacobi) or point-to-plane
+ * (ColPivHouseholderQR) coefficients; kept on the device.  *nsel = number of
+ * selected points (laserCloudOri{Corner,Surf}Flag). */
+int slio_s2m_coeffs(slio_handle h, int kind, const float transform[6], int64_t* nsel);
+/* The handle's coefficients (n x {x, y, z, intensity}) and flags to host. */
+int slio_s2m_get_coeffs(slio_handle h, float* coeff, uint8_t* sel);
+/* LMOptimization rows (:1578-1626; corners, then surfs) and the normal
+ * equations A^T A (6x6) / A^T B (6) of the selected points, fp64 sums in a
+ * fixed order rounded to float; *nsel = laserCloudSelNum.  Either handle may
+ * be NULL. */
+int slio_s2m_normal_equations(slio_handle h_corner, slio_handle h_surf,
+                              const float transform[6], float AtA[36], float AtB[6],
+                              int64_t* nsel);
+/* LMOptimization's host step (:1627-1700): X = solve(AtA, AtB) (QR); on
+ * iteration 0 the degeneracy projection matP (eigenvalues < 100) is formed,
+ * later iterations reuse it; transform += X; *converged = deltaR < 0.05 deg
+ * and deltaT < 0.05 cm.  Returns 1 (nothing done) with fewer than 50
+ * correspondences, as the reference's `return false`. */
+int slio_s2m_lm_step(const float AtA[36], const float AtB[6], int64_t nsel, int iter_count,
+                     float transform[6], int* is_degenerate, float matP[36], int* converged);
+
 /* Manifold helpers exported for tests (esekfom.hpp:59-73, 236-258). */
 int slio_state_boxplus(const slio_state* x, const double dx[24], slio_state* out);
 int slio_state_boxminus(const slio_state* x1, const slio_state* x2, double dx[24]);

@@ -23,7 +23,7 @@ _lib = None
 
 
 def build() -> str:
-    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "map_oracle.cpp", "imu_oracle.cpp",
+    srcs = [os.path.join(HERE, f) for f in ("slio_oracle.cpp", "frontend_oracle.cpp", "map_oracle.cpp", "imu_oracle.cpp", "lio_s2m_oracle.cpp",
                                             "Makefile")]
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
@@ -52,6 +52,10 @@ def load() -> C.CDLL:
 
 
 def _bind_map(lib):
+    lib.orc_s2m_transform.argtypes = [_FP, _FP, _FP, _FP, C.c_int64, _FP, _FP, _FP]
+    lib.orc_s2m_coeffs.argtypes = [C.c_int, _FP, _FP, _FP, C.c_int64, _FP, _IP, _FP, _FP, _U8P]
+    lib.orc_s2m_normal_equations.argtypes = [_FP, C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_U8P), _I64P,
+                                             C.c_int, _FP, _FP, _I64P]
     lib.orc_imu_undistort.argtypes = [_DP, C.c_int, C.c_double, C.c_double, _DP, C.c_double, _DP, _DP, _DP,
                                       _DP, _DP, _FP, _FP, _FP, _FP, C.c_int64, _FP, _FP, _FP, _FP, _DP,
                                       C.POINTER(C.c_int)]
@@ -254,6 +258,61 @@ def imu_undistort(imu: np.ndarray, pcl_beg: float, pcl_end: float, last_lidar_en
     return {"points": np.stack([ox[:n], oy[:n], oz[:n]], 1), "t_ms": ot[:n], "state": st, "P": Pm,
             "poses": poses[:npose.value], "acc_s_last": asl, "angvel_last": avl,
             "last_lidar_end_time": lle.value}
+
+
+def s2m_transform(tf, body):
+    """pointAssociateToMap at transformTobeMapped (LIO-SAM mapOptmization.cpp:359-373)."""
+    t = _f(tf)
+    b = _f(body).reshape(-1, 3)
+    x, y, z = (_f(b[:, k]) for k in range(3))
+    n = b.shape[0]
+    w = [np.zeros(n, np.float32) for _ in range(3)]
+    load().orc_s2m_transform(t.ctypes.data_as(_FP), x.ctypes.data_as(_FP), y.ctypes.data_as(_FP),
+                             z.ctypes.data_as(_FP), n, *(a.ctypes.data_as(_FP) for a in w))
+    return np.stack(w, 1)
+
+
+def s2m_coeffs(kind, world, map_xyz, idx, sqd):
+    """corner (0) / surf (1) coefficients (n, 4) and selection flags."""
+    w = _f(world).reshape(-1, 3)
+    wx, wy, wz = (_f(w[:, k]) for k in range(3))
+    m = _f(map_xyz).reshape(-1)
+    ii = np.ascontiguousarray(idx, dtype=np.int32)
+    ss = _f(sqd)
+    n = w.shape[0]
+    coeff = np.zeros((n, 4), np.float32)
+    sel = np.zeros(n, np.uint8)
+    load().orc_s2m_coeffs(kind, wx.ctypes.data_as(_FP), wy.ctypes.data_as(_FP), wz.ctypes.data_as(_FP), n,
+                          m.ctypes.data_as(_FP), ii.ctypes.data_as(_IP), ss.ctypes.data_as(_FP),
+                          coeff.ctypes.data_as(_FP), sel.ctypes.data_as(_U8P))
+    return coeff, sel
+
+
+def s2m_normal_equations(tf, clouds):
+    """clouds: [(body (n,3), coeff (n,4), sel (n,))...], corners first."""
+    t = _f(tf)
+    keep = []
+    bodies = (_FP * (3 * len(clouds)))()
+    coeffs = (_FP * len(clouds))()
+    sels = (_U8P * len(clouds))()
+    ns = np.zeros(len(clouds), np.int64)
+    for q, (b, c, s) in enumerate(clouds):
+        bb = _f(b).reshape(-1, 3)
+        xyz = [_f(bb[:, k]) for k in range(3)]
+        cc = _f(c)
+        ss = np.ascontiguousarray(s, dtype=np.uint8)
+        keep += xyz + [cc, ss]
+        for k in range(3):
+            bodies[3 * q + k] = xyz[k].ctypes.data_as(_FP)
+        coeffs[q] = cc.ctypes.data_as(_FP)
+        sels[q] = ss.ctypes.data_as(_U8P)
+        ns[q] = bb.shape[0]
+    AtA = np.zeros(36, np.float32)
+    AtB = np.zeros(6, np.float32)
+    nsel = C.c_int64()
+    load().orc_s2m_normal_equations(t.ctypes.data_as(_FP), bodies, coeffs, sels, ns.ctypes.data_as(_I64P),
+                                    len(clouds), AtA.ctypes.data_as(_FP), AtB.ctypes.data_as(_FP), C.byref(nsel))
+    return AtA.reshape(6, 6), AtB, nsel.value
 
 
 def voxel_grid(pts: np.ndarray, leaf: float, pcl_order: bool = False) -> np.ndarray:

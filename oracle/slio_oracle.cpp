@@ -217,7 +217,7 @@ int nearest(const Tree& T, float qx, float qy, float qz, int k, int32_t* idx, fl
 // ------------------------------------------------------------------ plane
 // Eigen ColPivHouseholderQR<Matrix<float,5,3>>::solve(-1) restated with
 // left-to-right sums; then common_lib.h:244-257.
-bool esti_plane(const float nb[5][3], float threshold, float abcd[4]) {
+void qr_solve_m1(const float nb[5][3], float sol[3]) {
   const float eps = 1.1920928955078125e-07f;
   const float tiny = 1.17549435082228750797e-38f;
   float a[3][5];
@@ -300,7 +300,7 @@ bool esti_plane(const float nb[5][3], float threshold, float abcd[4]) {
   }
   int perm[3] = {0, 1, 2};
   for (int k = 0; k < 3; ++k) std::swap(perm[k], perm[trans[k]]);
-  float sol[3] = {0.0f, 0.0f, 0.0f};
+  sol[0] = sol[1] = sol[2] = 0.0f;
   if (nzp > 0) {
     float c[5] = {-1.0f, -1.0f, -1.0f, -1.0f, -1.0f};
     for (int k = 0; k < nzp; ++k) {
@@ -320,6 +320,11 @@ bool esti_plane(const float nb[5][3], float threshold, float abcd[4]) {
     }
     for (int i = 0; i < nzp; ++i) sol[perm[i]] = c[i];
   }
+}
+
+bool esti_plane(const float nb[5][3], float threshold, float abcd[4]) {
+  float sol[3];
+  qr_solve_m1(nb, sol);
   const float n = std::sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
   abcd[0] = sol[0] / n;
   abcd[1] = sol[1] / n;
@@ -663,6 +668,13 @@ int orc_knn(void* t, const float* qx, const float* qy, const float* qz, int64_t 
 #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 256)
   for (int64_t i = 0; i < nq; ++i) nearest(*T, qx[i], qy[i], qz[i], k, idx + i * k, sqd + i * k);
   return 0;
+}
+
+void orc_qr_solve_m1(const float* nb15, float* sol) {
+  float nb[5][3];
+  for (int j = 0; j < 5; ++j)
+    for (int k = 0; k < 3; ++k) nb[j][k] = nb15[3 * j + k];
+  qr_solve_m1(nb, sol);
 }
 
 int orc_esti_plane(const float* nb15, float threshold, float* abcd) {

@@ -4,7 +4,7 @@ mkdir -p agi_lidar_slam_amd/_abl
 S=agi_lidar_slam_amd/csrc
 while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math $2 -I include \
-    $S/slio_device.hip $S/slio_ikf.cpp $S/slio_imu.cpp $S/slio_lio.hip -o agi_lidar_slam_amd/_abl/libslio_$1.so &
+    $S/slio_device.hip $S/slio_ikf.cpp $S/slio_imu.cpp $S/slio_s2m.cpp $S/slio_lio.hip -o agi_lidar_slam_amd/_abl/libslio_$1.so &
   shift 2
 done
 wait

@@ -14,6 +14,8 @@ while [ $# -gt 0 ]; do
          rc=$?; echo "map rc=$rc"; tail -25 gpurun_out/${tag}_map.log; [ $rc -eq 0 ] || exit $rc ;;
     imu) timeout -k 10 300 python -u -m pytest tests/test_gpu_imu.py -m gpu -x -v -s --timeout 200 --timeout-method thread > gpurun_out/${tag}_imu.log 2>&1
          rc=$?; echo "imu rc=$rc"; tail -25 gpurun_out/${tag}_imu.log; [ $rc -eq 0 ] || exit $rc ;;
+    s2m) timeout -k 10 300 python -u -m pytest tests/test_gpu_lio_s2m.py -m gpu -x -v -s --timeout 200 --timeout-method thread > gpurun_out/${tag}_s2m.log 2>&1
+         rc=$?; echo "s2m rc=$rc"; tail -25 gpurun_out/${tag}_s2m.log; [ $rc -eq 0 ] || exit $rc ;;
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
          rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/${tag}_tests.log; [ $rc -eq 0 ] || exit $rc ;;
     stats) shift; timeout -k 10 600 python -u scripts/far_stats.py $1 > gpurun_out/${tag}_stats.log 2>&1
