@@ -157,10 +157,30 @@ struct MapDev {
   bool dirty = false;
   float cell0 = 1.0f;             // requested grid cell and cell budget (slio_params)
   int64_t max_cells = 0;
-  void free_index() {
-    for (void* q : {(void*)pts, (void*)start, (void*)blk, (void*)bstart, (void*)cpts, (void*)cstart,
-                    (void*)clo, (void*)chi, (void*)keep})
-      if (q) (void)hipFree(q);
+  // device allocations kept across index rebuilds (capacity in bytes): a
+  // rebuild per scan must not pay hipMalloc / hipFree of ~GB tables
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Buf b_pts, b_keep, b_cpts, b_start, b_cstart, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6];
+  hipError_t take(Buf& b, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 16);
+    if (bytes <= b.cap) return hipSuccess;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = bytes + bytes / 4;  // headroom: the map grows scan by scan
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e) {
+      (void)hipGetLastError();
+      want = bytes;
+      e = hipMalloc(&b.p, want);
+    }
+    if (!e) b.cap = want;
+    return e;
+  }
+  void free_index() {  // the views only; allocations stay for the next build
     pts = nullptr;
     start = nullptr;
     blk = nullptr;
@@ -173,7 +193,12 @@ struct MapDev {
     n = ncells = nccells = nblk = 0;
   }
   ~MapDev() {
-    free_index();
+    for (Buf* b : {&b_pts, &b_keep, &b_cpts, &b_start, &b_cstart, &b_clo, &b_chi, &b_bstart, &b_blk})
+      if (b->p) (void)hipFree(b->p);
+    for (Buf& b : b_tmp)
+      if (b.p) (void)hipFree(b.p);
+    for (Buf& b : b_ref)
+      if (b.p) (void)hipFree(b.p);
     if (add4) (void)hipFree(add4);
     if (akeep) (void)hipFree(akeep);
   }
@@ -2760,10 +2785,14 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     return e == hipErrorOutOfMemory ? SLIO_ENOMEM : SLIO_EDEVICE;
   };
   hipError_t e;
-  if ((e = hipMalloc(&m.start, sizeof(uint32_t) * (m.ncells + 1))) ||
-      (e = hipMalloc(&m.cstart, sizeof(uint32_t) * (m.nccells + 1))) ||
-      (e = hipMalloc(&m.clo, sizeof(float4) * m.nccells)) || (e = hipMalloc(&m.chi, sizeof(float4) * m.nccells)))
+  if ((e = m.take(m.b_start, sizeof(uint32_t) * (m.ncells + 1))) ||
+      (e = m.take(m.b_cstart, sizeof(uint32_t) * (m.nccells + 1))) ||
+      (e = m.take(m.b_clo, sizeof(float4) * m.nccells)) || (e = m.take(m.b_chi, sizeof(float4) * m.nccells)))
     return fail("hipMalloc", e);
+  m.start = (uint32_t*)m.b_start.p;
+  m.cstart = (uint32_t*)m.b_cstart.p;
+  m.clo = (float4*)m.b_clo.p;
+  m.chi = (float4*)m.b_chi.p;
   if (n == 0) {
     if ((e = hipMemsetAsync(m.start, 0, sizeof(uint32_t) * (m.ncells + 1), st)) ||
         (e = hipMemsetAsync(m.cstart, 0, sizeof(uint32_t) * (m.nccells + 1), st)) ||
@@ -2771,21 +2800,31 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       return fail("empty map", e);
     return SLIO_OK;
   }
-  if ((e = hipMalloc(&m.pts, sizeof(float4) * n)) || (e = hipMalloc(&m.keep, n)) ||
-      (e = hipMalloc(&m.cpts, sizeof(float4) * n)))
+  if ((e = m.take(m.b_pts, sizeof(float4) * n)) || (e = m.take(m.b_keep, n)) ||
+      (e = m.take(m.b_cpts, sizeof(float4) * n)))
     return fail("hipMalloc", e);
+  m.pts = (float4*)m.b_pts.p;
+  m.keep = (uint8_t*)m.b_keep.p;
+  m.cpts = (float4*)m.b_cpts.p;
   uint64_t *k0 = nullptr, *k1 = nullptr;
   uint32_t *v0 = nullptr, *v1 = nullptr, *cnt = nullptr, *c0 = nullptr, *c1 = nullptr;
   void* tmp = nullptr;
   int rc = SLIO_OK;
   const int64_t maxc = std::max(m.ncells, m.nccells) + 1;
   do {
-    if ((e = hipMalloc(&k0, 8 * n)) || (e = hipMalloc(&k1, 8 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
-        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&c0, 4 * n)) || (e = hipMalloc(&c1, 4 * n)) ||
-        (e = hipMalloc(&cnt, 4 * maxc))) {
+    if ((e = m.take(m.b_tmp[0], 8 * n)) || (e = m.take(m.b_tmp[1], 8 * n)) || (e = m.take(m.b_tmp[2], 4 * n)) ||
+        (e = m.take(m.b_tmp[3], 4 * n)) || (e = m.take(m.b_tmp[4], 4 * n)) || (e = m.take(m.b_tmp[5], 4 * n)) ||
+        (e = m.take(m.b_tmp[6], 4 * maxc))) {
       rc = fail("hipMalloc", e);
       break;
     }
+    k0 = (uint64_t*)m.b_tmp[0].p;
+    k1 = (uint64_t*)m.b_tmp[1].p;
+    v0 = (uint32_t*)m.b_tmp[2].p;
+    v1 = (uint32_t*)m.b_tmp[3].p;
+    c0 = (uint32_t*)m.b_tmp[4].p;
+    c1 = (uint32_t*)m.b_tmp[5].p;
+    cnt = (uint32_t*)m.b_tmp[6].p;
     int idbits = 1;
     while (idbits < 32 && ((int64_t)1 << idbits) <= (int64_t)m.next_id) ++idbits;
     int cbits = 1;
@@ -2800,10 +2839,11 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       break;
     }
     t4 = std::max(std::max(t1, t2), t3);
-    if ((e = hipMalloc(&tmp, t4))) {
+    if ((e = m.take(m.b_tmp[7], t4))) {
       rc = fail("hipMalloc tmp", e);
       break;
     }
+    tmp = m.b_tmp[7].p;
     const int nb = grid_blocks(n);
     k_cell_keys64<<<nb, 256, 0, st>>>(in, n, g, idbits, k0, v0);
     if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, k0, k1, v0, v1, (int)n, 0, idbits + cbits, st)) ||
@@ -2842,11 +2882,11 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
     if ((nb9 && nb9[0] && nb9[0] != '0') || 9 * n >= (int64_t)0xFFFFFFF0ll) break;
     const int ncb = grid_blocks(m.ncells);
-    if (hipMalloc(&m.bstart, sizeof(uint32_t) * (m.ncells + 1))) {
+    if (m.take(m.b_bstart, sizeof(uint32_t) * (m.ncells + 1))) {
       (void)hipGetLastError();
-      m.bstart = nullptr;
       break;
     }
+    m.bstart = (uint32_t*)m.b_bstart.p;
     k_blk_count<<<ncb, 256, 0, st>>>(m.start, g, m.ncells, cnt);
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.bstart, (int)(m.ncells + 1), st))) {
       rc = fail("block-row scan", e);
@@ -2858,13 +2898,13 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       rc = fail("block-row total", e);
       break;
     }
-    if (hipMalloc(&m.blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
+    if (m.take(m.b_blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
       (void)hipGetLastError();
       m.blk = nullptr;
-      (void)hipFree(m.bstart);
       m.bstart = nullptr;
       break;
     }
+    m.blk = (float4*)m.b_blk.p;
     m.nblk = (int64_t)total;
     k_blk_fill<<<ncb, 256, 0, st>>>(m.pts, m.start, m.bstart, g, m.ncells, m.blk);
     if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
@@ -2872,8 +2912,6 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       break;
     }
   } while (0);
-  for (void* q : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)c0, (void*)c1, (void*)cnt, tmp})
-    if (q) (void)hipFree(q);
 #ifdef SLIO_BOUNDS_CHECK
   if (!rc) {
     const int64_t nc = m.ncells;
@@ -3221,11 +3259,25 @@ static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream
   *total = 0;
   if (n == 0) return SLIO_OK;
   size_t tb = 0;
-  void* tmp = nullptr;
+  // scan temporaries cached per host thread (no hipMalloc / hipFree per call)
+  static thread_local void* tmp = nullptr;
+  static thread_local size_t tcap = 0;
   hipError_t e;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, rank, (int)n, st)) || (e = hipMalloc(&tmp, tb)) ||
-      (e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, rank, (int)n, st))) {
+  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, rank, (int)n, st))) {
+    set_error(std::string("slio map: scan: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  if (tb > tcap) {
     (void)hipFree(tmp);
+    tmp = nullptr;
+    tcap = 0;
+    if ((e = hipMalloc(&tmp, tb + tb / 2))) {
+      set_error(std::string("slio map: scan: ") + hipGetErrorString(e));
+      return SLIO_ENOMEM;
+    }
+    tcap = tb + tb / 2;
+  }
+  if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, rank, (int)n, st))) {
     set_error(std::string("slio map: scan: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
   }
@@ -3233,7 +3285,6 @@ static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream
   e = hipMemcpyAsync(&last[0], rank + n - 1, 4, hipMemcpyDeviceToHost, st);
   if (!e) e = hipMemcpyAsync(&last[1], flag + n - 1, 4, hipMemcpyDeviceToHost, st);
   if (!e) e = hipStreamSynchronize(st);
-  (void)hipFree(tmp);
   if (e) {
     set_error(std::string("slio map: scan total: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
@@ -3359,92 +3410,54 @@ static int map_refresh(Ctx& c, bool adds_only) {
   MapDev& m = *c.map;
   if (adds_only && m.nadd == 0) return SLIO_OK;
   hipStream_t st = c.stream;
-  SLIO_HIP(hipStreamSynchronize(st));
-  const int64_t n0 = m.n, n1 = m.nadd;
-  float4* in4 = nullptr;
-  uint32_t *flag = nullptr, *rank = nullptr;
-  int32_t* bb = nullptr;
-  int rc = SLIO_OK;
-  int64_t n = 0;
+  const int64_t n0 = m.n, n1 = m.nadd, nt = n0 + n1;
+  hipError_t e;
+  // survivors: stored points (cell order) and additions (id order) compacted
+  // into in4; the sort in build_index orders them by (cell, id) anyway
+  if ((e = m.take(m.b_ref[0], 16 * nt)) || (e = m.take(m.b_ref[1], 4 * nt)) || (e = m.take(m.b_ref[2], 4 * nt)) ||
+      (e = m.take(m.b_ref[3], 32))) {
+    set_error(std::string("slio map rebuild: hipMalloc: ") + hipGetErrorString(e));
+    return SLIO_ENOMEM;
+  }
+  float4* in4 = (float4*)m.b_ref[0].p;
+  uint32_t* flag = (uint32_t*)m.b_ref[1].p;
+  uint32_t* rank = (uint32_t*)m.b_ref[2].p;
+  int32_t* bb = (int32_t*)m.b_ref[3].p;
+  if (n0) k_widen_flags<<<grid_blocks(n0), 256, 0, st>>>(m.keep, n0, flag);
+  if (n1) k_widen_flags<<<grid_blocks(n1), 256, 0, st>>>(m.akeep, n1, flag + n0);
+  uint32_t total = 0;
+  if (int rc = scan_flags(flag, rank, nt, st, &total)) return rc;
+  const int64_t n = total;
+  if (n0) k_compact4<<<grid_blocks(n0), 256, 0, st>>>(m.pts, flag, rank, n0, in4);
+  // (the ranks of the additions continue the stored points': one scan)
+  if (n1) k_compact4<<<grid_blocks(n1), 256, 0, st>>>(m.add4, flag + n0, rank + n0, n1, in4);
+  const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
+  int32_t got[8];
+  if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
+    set_error(std::string("slio map rebuild: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  if (n) k_bbox4<<<std::min(grid_blocks(n), 2048), 256, 0, st>>>(in4, n, bb);
+  if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+    set_error(std::string("slio map rebuild: bbox: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  if (got[6]) {
+    set_error("slio map rebuild: non-finite map coordinate");
+    return SLIO_EINVAL;
+  }
   float mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
-  do {
-    hipError_t e;
-    const int64_t nt = n0 + n1;
-    if ((e = hipMalloc(&in4, 16 * std::max<int64_t>(nt, 1))) || (e = hipMalloc(&flag, 4 * std::max<int64_t>(nt, 1))) ||
-        (e = hipMalloc(&rank, 4 * std::max<int64_t>(nt, 1))) || (e = hipMalloc(&bb, 32))) {
-      set_error(std::string("slio map rebuild: hipMalloc: ") + hipGetErrorString(e));
-      rc = SLIO_ENOMEM;
-      break;
+  if (n)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fkey_inv(got[a]);
+      mx[a] = fkey_inv(got[3 + a]);
     }
-    // survivors: stored points in cell order, then additions in id order
-    // (the sort in build_index orders by (cell, id) anyway)
-    float4* all = nullptr;
-    if ((e = hipMalloc(&all, 16 * std::max<int64_t>(nt, 1)))) {
-      set_error("slio map rebuild: hipMalloc");
-      rc = SLIO_ENOMEM;
-      break;
-    }
-    if ((n0 && ((e = hipMemcpyAsync(all, m.pts, 16 * n0, hipMemcpyDeviceToDevice, st)))) ||
-        (n1 && ((e = hipMemcpyAsync(all + n0, m.add4, 16 * n1, hipMemcpyDeviceToDevice, st))))) {
-      (void)hipFree(all);
-      set_error("slio map rebuild: copy");
-      rc = SLIO_EDEVICE;
-      break;
-    }
-    {
-      // keep flags (u8) -> u32 flags
-      uint8_t* kk = nullptr;
-      if ((e = hipMalloc(&kk, std::max<int64_t>(nt, 1)))) {
-        (void)hipFree(all);
-        rc = SLIO_ENOMEM;
-        break;
-      }
-      if (n0) (void)hipMemcpyAsync(kk, m.keep, n0, hipMemcpyDeviceToDevice, st);
-      if (n1) (void)hipMemcpyAsync(kk + n0, m.akeep, n1, hipMemcpyDeviceToDevice, st);
-      k_widen_flags<<<grid_blocks(nt), 256, 0, st>>>(kk, nt, flag);
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(kk);
-    }
-    uint32_t total = 0;
-    if ((rc = scan_flags(flag, rank, nt, st, &total))) {
-      (void)hipFree(all);
-      break;
-    }
-    n = total;
-    if (nt) k_compact4<<<grid_blocks(nt), 256, 0, st>>>(all, flag, rank, nt, in4);
-    const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
-    if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
-      (void)hipFree(all);
-      rc = SLIO_EDEVICE;
-      break;
-    }
-    if (n) k_bbox4<<<std::min(grid_blocks(n), 2048), 256, 0, st>>>(in4, n, bb);
-    int32_t got[8];
-    if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
-      (void)hipFree(all);
-      set_error(std::string("slio map rebuild: bbox: ") + hipGetErrorString(e));
-      rc = SLIO_EDEVICE;
-      break;
-    }
-    (void)hipFree(all);
-    if (got[6]) {
-      set_error("slio map rebuild: non-finite map coordinate");
-      rc = SLIO_EINVAL;
-      break;
-    }
-    if (n)
-      for (int a = 0; a < 3; ++a) {
-        mn[a] = fkey_inv(got[a]);
-        mx[a] = fkey_inv(got[3 + a]);
-      }
-    m.free_index();
-    m.nadd = 0;
-    rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild");
-    m.version++;
-    m.dirty = false;
-  } while (0);
-  for (void* q : {(void*)in4, (void*)flag, (void*)rank, (void*)bb})
-    if (q) (void)hipFree(q);
+  // in4 is b_ref[0]: build_index reads it while writing the b_* tables
+  m.free_index();
+  m.nadd = 0;
+  const int rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild");
+  m.version++;
+  m.dirty = false;
   return rc;
 }
 
