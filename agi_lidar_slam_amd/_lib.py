@@ -257,6 +257,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("SLIO_LIB_OVERRIDE", path)  # diagnostic builds (scripts/build_abl.sh)
     if not os.path.exists(path):
         raise RuntimeError(
             f"{path} is missing: build it with `python -m agi_lidar_slam_amd.build` "

@@ -959,6 +959,17 @@ struct PassCfg {
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
   int knn_only;            // 1: neighbours only (nbr_*), no fit / rows / products
+  // fused filter step (single-rank device-resident update, later passes):
+  // the last workgroup of each super-chunk sums its row, the last of those
+  // runs the filter step -- no separate super-sum launch
+  int fuse;
+  int iter, maxit;
+  double R;
+  const IkfCtl* src;
+  IkfCtl* hblk;
+  double* super_out;
+  uint32_t* cnt;  // [1] rows done, [8 + s] chunks of super-chunk s done
+  int64_t nchunks;
 };
 
 // ---------------------------------------------------------------- far queries
@@ -1324,18 +1335,31 @@ __device__ __forceinline__ bool chol_solve_wave(SolveLds& L, const double (&b)[1
 // the caller's mapped host block on the first pass of an update, else ctl.
 // hblk (the mapped host block) receives x, P and the flags when the update
 // ends.  All threads of the workgroup call this.
+// LDS home of control-block double e (x, xprop | P | P11i | G | dxn)
+__device__ __forceinline__ double& ctl_slot(SolveLds& L, int e) {
+  constexpr int oP = (int)(offsetof(IkfCtl, P) / sizeof(double));
+  constexpr int oI = (int)(offsetof(IkfCtl, P11i) / sizeof(double));
+  constexpr int oG = (int)(offsetof(IkfCtl, G) / sizeof(double));
+  constexpr int oD = (int)(offsetof(IkfCtl, dxn) / sizeof(double));
+  if (e < oP) return reinterpret_cast<double*>(&L.x)[e];
+  if (e < oI) return L.P[e - oP];
+  if (e < oG) return L.P11i[e - oI];
+  if (e < oD) return L.G[e - oG];
+  return L.dxn[e - oD];
+}
+constexpr int kCtlD = (int)(offsetof(IkfCtl, converge) / sizeof(double));
+
 template <int NT>
 __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, double R, int i,
                                 int maxit, SolveLds& L, const double* sup_src,
-                                uint32_t load_mask) {
+                                uint32_t load_mask, bool staged = false) {
   static_assert(NT >= 256, "solve: at least four wavefronts");
   const int t = threadIdx.x;
   const bool first = src != ctl;
   {
     // one round trip: every load of the super rows and of the control block
-    // (x, x_prop, P, G, P11^-1: a contiguous run of doubles) is issued before
-    // any LDS store; global-address-space pointers keep them off the flat path
-    constexpr int kCtlD = (int)(offsetof(IkfCtl, converge) / sizeof(double));
+    // (unless staged) is issued before any LDS store; global-address-space
+    // pointers keep them off the flat path
     constexpr int kRows = SLIO_NSUPER * SLIO_NPROD;
     constexpr int kC = (kCtlD + NT - 1) / NT, kR = (kRows + NT - 1) / NT;
     static_assert(offsetof(SolveLds, xprop) == offsetof(SolveLds, x) + sizeof(slio_state), "");
@@ -1347,42 +1371,31 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
       const bool on = e < kRows && sup_src && ((load_mask >> (e / SLIO_NPROD)) & 1u);
       rv[u] = on ? ld_sc1(sup_src + e) : 0.0;
     }
+    if (!staged) {
 #pragma unroll
-    for (int u = 0; u < kC; ++u) {
-      const int e = t + u * NT;
-      cv[u] = e < kCtlD ? gc[e] : 0.0;
+      for (int u = 0; u < kC; ++u) {
+        const int e = t + u * NT;
+        cv[u] = e < kCtlD ? gc[e] : 0.0;
+      }
     }
     typedef __attribute__((address_space(1))) int32_t gint;
-    const int32_t fl = t < 8 ? ((const gint*)(const int32_t*)&src->converge)[t] : 0;
+    const int32_t fl = (!staged && t < 8) ? ((const gint*)(const int32_t*)&src->converge)[t] : 0;
 #pragma unroll
     for (int u = 0; u < kR; ++u) {
       const int e = t + u * NT;
       if (e < kRows && sup_src && ((load_mask >> (e / SLIO_NPROD)) & 1u))
         L.sup[e / SLIO_NPROD][e % SLIO_NPROD] = rv[u];
     }
-    // control block doubles -> LDS fields (x, xprop | P | P11i | G)
+    // control block doubles -> LDS fields (x, xprop | P | P11i | G | dxn)
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       const int e = t + u * NT;
       if (e < kCtlD) {
-        constexpr int oP = (int)(offsetof(IkfCtl, P) / sizeof(double));
-        constexpr int oI = (int)(offsetof(IkfCtl, P11i) / sizeof(double));
-        constexpr int oG = (int)(offsetof(IkfCtl, G) / sizeof(double));
-        constexpr int oD = (int)(offsetof(IkfCtl, dxn) / sizeof(double));
-        if (e < oP)
-          reinterpret_cast<double*>(&L.x)[e] = cv[u];
-        else if (e < oI)
-          L.P[e - oP] = cv[u];
-        else if (e < oG)
-          L.P11i[e - oI] = cv[u];
-        else if (e < oD)
-          L.G[e - oG] = cv[u];
-        else
-          L.dxn[e - oD] = cv[u];
-        if (first) reinterpret_cast<double*>(ctl)[e] = cv[u];  // keep the block in HBM
+        if (!staged) ctl_slot(L, e) = cv[u];
+        if (first) reinterpret_cast<double*>(ctl)[e] = staged ? ctl_slot(L, e) : cv[u];  // keep it in HBM
       }
     }
-    if (t < 8) L.fl[t] = fl;
+    if (!staged && t < 8) L.fl[t] = fl;
     if (first && t == 0) ctl->singular = 0;
   }
   __syncthreads();
@@ -1611,7 +1624,7 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
 // the accumulators and halves are then combined in a fixed order.
 template <int NT>
 __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], double (*part)[SLIO_NPROD],
-                                               double* __restrict__ out) {
+                                               double* __restrict__ out, bool sc1 = false) {
   constexpr int kSplit = NT / 128;                 // row halves handled in parallel
   constexpr int kRowsPer = SLIO_CHUNK / kSplit;
   const int t = threadIdx.x;
@@ -1634,8 +1647,85 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
     double s = part[0][t];
 #pragma unroll
     for (int h = 1; h < kSplit; ++h) s = s + part[h][t];
-    out[t] = s;
+    if (sc1)
+      st_sc1(out + t, s);  // read by another workgroup of this launch
+    else
+      out[t] = s;
   }
+}
+
+// LDS of the fused tail (aliases the pass's LDS)
+struct TailLds {
+  double seg[kSuperSeg * SLIO_NPROD];
+  SolveLds L;
+  int flag;
+};
+
+// Fused filter step, after this workgroup's chunk partial is published
+// (write-through, drained): the last workgroup of super-chunk s sums row s in
+// k_super_sums' fixed order (segment g: chunks c0 + g, c0 + g + 8, ...; then
+// the 8 segments), publishes it and arrives on the row counter; the last of
+// the 8 runs the filter step with the other 7 rows (sc1 loads).  Counters are
+// reset by the workgroup that completes them.
+template <int NT>
+__device__ __forceinline__ void fused_tail(const PassCfg& cfg, const double* chunk_part, int64_t chunk,
+                                           TailLds& T) {
+  const int t = threadIdx.x;
+  drain_stores();
+  __syncthreads();
+  const int64_t C = cfg.nchunks;
+  if (t == 0) {
+    int s = 0;
+#pragma unroll
+    for (int k = 1; k < SLIO_NSUPER; ++k)
+      if (super_lo(C, k) <= chunk) s = k;
+    const uint32_t members = (uint32_t)(super_lo(C, s + 1) - super_lo(C, s));
+    T.flag = arrive(cfg.cnt + 8 + s) == members - 1 ? s : -1;
+  }
+  __syncthreads();
+  const int s = T.flag;
+  if (s < 0) return;
+  if (t == 0) reset_counter(cfg.cnt + 8 + s);
+  {
+    constexpr int KP = (kSuperSeg * SLIO_NPROD + NT - 1) / NT;
+    const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
+    double acc[KP];
+    int64_t lim[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const int p = t + k * NT;
+      const int g = p / SLIO_NPROD;
+      lim[k] = p < kSuperSeg * SLIO_NPROD ? (c1 - c0 - g + kSuperSeg - 1) / kSuperSeg : 0;
+      acc[k] = 0.0;
+    }
+    const double* cp = chunk_part + c0 * SLIO_NPROD + t;
+#pragma unroll 4
+    for (int64_t j = 0; j < lim[0]; ++j) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (j < lim[k]) acc[k] = acc[k] + ld_sc1(cp + j * (kSuperSeg * SLIO_NPROD) + k * NT);
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (t + k * NT < kSuperSeg * SLIO_NPROD) T.seg[t + k * NT] = acc[k];
+  }
+  __syncthreads();
+  if (t < SLIO_NPROD) {
+    double v = T.seg[t];
+#pragma unroll
+    for (int q = 1; q < kSuperSeg; ++q) v = v + T.seg[q * SLIO_NPROD + t];
+    T.L.sup[s][t] = v;
+    st_sc1(cfg.super_out + s * SLIO_NPROD + t, v);
+  }
+  drain_stores();
+  __syncthreads();
+  if (t == 0) T.flag = arrive(cfg.cnt + 1) == (uint32_t)(SLIO_NSUPER - 1);
+  __syncthreads();
+  if (!T.flag) return;
+  if (t == 0) reset_counter(cfg.cnt + 1);
+  if (cfg.src == cfg.ctl && cfg.ctl->done) return;
+  ikf_solve_block<NT>(cfg.ctl, cfg.src, cfg.hblk, cfg.R, cfg.iter, cfg.maxit, T.L, cfg.super_out,
+                      ((1u << SLIO_NSUPER) - 1u) & ~(1u << s));
 }
 
 template <int LPQ>
@@ -1688,16 +1778,34 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
   static_assert(SLIO_CHUNK % QPP == 0, "chunk must be a multiple of queries/pass");
   static_assert(NT >= SLIO_CHUNK, "fit phase needs one lane per point");
-  __shared__ double rows[SLIO_CHUNK][kRow];
-  __shared__ double part[NT / 128][SLIO_NPROD];
-  __shared__ uint32_t nb_pos[SLIO_CHUNK][5];
-  __shared__ float nb_d5[SLIO_CHUNK];
-  __shared__ float4 qw[SLIO_CHUNK];
-  // deferred (far) queries of this chunk and the far workers' scratch
-  __shared__ int far_cnt;
-  __shared__ float4 far_q[SLIO_CHUNK];
-  __shared__ uint8_t far_slot[SLIO_CHUNK];
-  __shared__ uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
+  // the pass's LDS; the fused filter step's tail reuses it once the
+  // products are written
+  struct SearchLds {
+    double rows[SLIO_CHUNK][kRow];
+    double part[NT / 128][SLIO_NPROD];
+    uint32_t nb_pos[SLIO_CHUNK][5];
+    float nb_d5[SLIO_CHUNK];
+    float4 qw[SLIO_CHUNK];
+    // deferred (far) queries of this chunk and the far workers' scratch
+    int far_cnt;
+    float4 far_q[SLIO_CHUNK];
+    uint8_t far_slot[SLIO_CHUNK];
+    uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
+  };
+  __shared__ union {
+    SearchLds s;
+    TailLds t;
+  } lds;
+  auto& rows = lds.s.rows;
+  auto& part = lds.s.part;
+  auto& nb_pos = lds.s.nb_pos;
+  auto& nb_d5 = lds.s.nb_d5;
+  auto& qw = lds.s.qw;
+  auto& far_cnt = lds.s.far_cnt;
+  auto& far_q = lds.s.far_q;
+  auto& far_slot = lds.s.far_slot;
+  auto& far_pre = lds.s.far_pre;
+  auto& far_beg = lds.s.far_beg;
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
   const int tid = threadIdx.x;
   const int sub = tid & (LPQ - 1);
@@ -2017,7 +2125,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (tid == 0) STAMP(2);
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
-  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
+  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, DEVPOSE && cfg.fuse);
+  if constexpr (DEVPOSE && NT == 256)
+    if (cfg.fuse) fused_tail<NT>(cfg, out.chunk_part, chunk, lds.t);
   if (tid == 0) STAMP(3);
 }
 
@@ -2089,6 +2199,22 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
   const int s = blockIdx.x;
   const int t = threadIdx.x;
   if (ctl) SSTAMP(0);
+  // the control block, in flight with the row sums' loads (used by the
+  // workgroup that runs the filter step; src is complete: written by the
+  // previous launch or by the host before this launch was enqueued)
+  constexpr int kC = (kCtlD + NT - 1) / NT;
+  double cv[kC];
+  int32_t fl = 0;
+  if (ctl) {
+    const gdouble* gc = (const gdouble*)(const double*)src;
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int e = t + u * NT;
+      cv[u] = e < kCtlD ? gc[e] : 0.0;
+    }
+    typedef __attribute__((address_space(1))) int32_t gint;
+    if (t < 8) fl = ((const gint*)(const int32_t*)&src->converge)[t];
+  }
   // the pass kernel before this one is complete: keep its number of far
   // queries (slio_far_queries), reset the queue's head and tail
   if (s == 0 && t == 0) {
@@ -2123,6 +2249,14 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
 #pragma unroll
         for (int k = 0; k < KP; ++k)
           v[k][j] = j < lim[k] ? base[j * (kSuperSeg * SLIO_NPROD) + k * NT] : 0.0;
+      if (ctl) {
+#pragma unroll
+        for (int u = 0; u < kC; ++u) {
+          const int e = t + u * NT;
+          if (e < kCtlD) ctl_slot(L, e) = cv[u];
+        }
+        if (t < 8) L.fl[t] = fl;
+      }
 #pragma unroll
       for (int j = 0; j < kJ; ++j)
 #pragma unroll
@@ -2166,7 +2300,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
   if (src == ctl && ctl->done) return;  // the first pass of an update always runs
   SSTAMP(3);
   ikf_solve_block<NT>(ctl, src, hblk, R, iter, maxit, L, super_out,
-                      ((1u << SLIO_NSUPER) - 1u) & ~(1u << s));
+                      ((1u << SLIO_NSUPER) - 1u) & ~(1u << s), true);
 }
 
 // ---------------------------------------------------------------- device IKF
@@ -2408,6 +2542,23 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   cfg.knn_only = knn_only ? 1 : 0;
+  // fused filter step: later search passes of a single-rank device-resident
+  // update in fixed mode (a search pass every iteration); 256-thread blocks
+  // (measured slower than the separate launch: 17.2k vs 19.2k IKF it/s at C2
+  // -- the per-super row sums and the solve on single workgroups at the end of
+  // the pass add more than the launch they save; opt-in for experiments)
+  cfg.fuse = (sa && sa->on && devpose && which == 1 && c.prm.lanes_per_query != 1 && !knn_only &&
+              std::getenv("SLIO_FUSE") != nullptr)
+                 ? 1
+                 : 0;
+  cfg.iter = sa ? sa->iter : 0;
+  cfg.maxit = sa ? sa->maxit : 0;
+  cfg.R = sa ? sa->R : 0.0;
+  cfg.src = sa ? sa->src : nullptr;
+  cfg.hblk = sa ? sa->hblk : nullptr;
+  cfg.super_out = c.d_super;
+  cfg.cnt = c.count;
+  cfg.nchunks = num_chunks(c.n);
   if (int rc = map_refresh(c); rc) return rc;
   PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane, c.sel, c.resid,
             c.chunk_part, c.count + 4};
@@ -2469,7 +2620,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
       hipExtLaunchKernelGGL(k_reuse_pass<false>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
                             rcfg, o);
   }
-  if (with_super) enqueue_super(c, ctl, sa);
+  if (with_super && !cfg.fuse) enqueue_super(c, ctl, sa);
   SLIO_HIP(hipGetLastError());
   if (which != 0) {
     c.searched = true;
