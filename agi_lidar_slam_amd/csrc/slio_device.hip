@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
+#include <type_traits>
 #include <memory>
 #include <string>
 #include <vector>
@@ -78,6 +79,12 @@ __device__ unsigned long long g_wstamps[8192][4][4];  // per wave: refine start/
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192)                              \
       g_wstamps[blockIdx.x][threadIdx.x >> 6][k] = (v);                            \
   } while (0)
+__device__ unsigned long long g_rstamps[8192][4];  // thread 0's first wide refinement
+#define RSTAMP(k)                                                                  \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                     \
+      g_rstamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                 \
+  } while (0)
 #define STAMP(slot)                                                                \
   do {                                                                             \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) {                            \
@@ -94,6 +101,9 @@ __device__ unsigned long long g_wstamps[8192][4][4];  // per wave: refine start/
   } while (0)
 #define WSTAMP(k, v) \
   do {               \
+  } while (0)
+#define RSTAMP(k) \
+  do {            \
   } while (0)
 #endif
 
@@ -1728,6 +1738,126 @@ __device__ __forceinline__ void fused_tail(const PassCfg& cfg, const double* chu
                       ((1u << SLIO_NSUPER) - 1u) & ~(1u << s));
 }
 
+// Refinement scan of ALL the runs of `mask` (<= 34: 25 rows + 9 right
+// segments) by the RL lanes of a group as ONE flattened candidate list: lane
+// j fetches the bounds of runs j, j + RL, ... (one round trip for all), the
+// group's prefix table goes to LDS (pre / dl, kTab entries), and the lanes
+// stride over the whole list with U loads in flight (scan_flat's pipeline),
+// a flat position's run found by a 6-step binary search in the table.  The
+// lanes share every run's points, so one dense run no longer sets the
+// group's time (a per-lane subset of the runs did: ~10 us for one query).
+// Every lane of the wavefront calls it (mask = 0: nothing to scan).
+constexpr int kTab = 36;
+template <int RL, int U>
+__device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
+                                               const uint32_t* __restrict__ start, const GridGeom& g,
+                                               const RunCtx& rc, uint64_t mask, int rsub,
+                                               uint32_t* pre, int32_t* dl, Top5& t) {
+  constexpr int W = (34 + RL - 1) / RL;  // runs per lane
+  const int nr = __popcll(mask);
+  RSTAMP(0);
+  int bits[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) bits[w] = -1;
+  {
+    uint64_t m = mask;
+    for (int q = 0; m; ++q) {
+      const int bit = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        if (q == rsub + w * RL) bits[w] = bit;
+    }
+  }
+  uint32_t rs[W], len[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint32_t s0 = 0, e0 = 0;
+    if (bits[w] >= 0) {
+      int yy, zz, xa, xb;
+      run_range(g, rc, bits[w], yy, zz, xa, xb);
+      if (xa <= xb) {
+        const uint32_t rb = ((uint32_t)zz * (uint32_t)g.dy + (uint32_t)yy) * (uint32_t)g.dx;
+        s0 = start[rb + xa];
+        e0 = start[rb + xb + 1];
+      }
+    }
+    rs[w] = s0;
+    len[w] = e0 - s0;
+  }
+  // lengths to the table, then every lane sums them (broadcast reads)
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (rsub + w * RL < kTab) pre[rsub + w * RL] = len[w];
+  wave_fence();
+  RSTAMP(1);
+  uint32_t acc = 0, own[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) own[w] = 0;
+#pragma unroll
+  for (int j = 0; j < 34; ++j) {
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (j == rsub + w * RL) own[w] = acc;
+    if (j < nr) acc += pre[j];
+  }
+  const uint32_t T = acc;
+  wave_fence();
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const int j = rsub + w * RL;
+    if (j < kTab) {
+      pre[j] = j < nr ? own[w] : 0xFFFFFFFFu;
+      dl[j] = (int32_t)(rs[w] - own[w]);
+    }
+  }
+  if (RL * W < kTab)  // entries no lane owns
+    for (int j = RL * W + rsub; j < kTab; j += RL) pre[j] = 0xFFFFFFFFu;
+  wave_fence();
+  RSTAMP(2);
+  uint32_t t0 = rsub;
+  if (t0 >= T) return;
+  auto addr = [&](uint32_t tt) {
+    int lo = 0;
+#pragma unroll
+    for (int st = 32; st; st >>= 1) {
+      const int c = lo + st;
+      const uint32_t pv = c < kTab ? pre[min(c, kTab - 1)] : 0xFFFFFFFFu;
+      lo = pv <= tt ? c : lo;
+    }
+    return tt + (uint32_t)dl[lo];
+  };
+  constexpr uint32_t kStep = U * RL;
+  uint32_t aA[U], aB[U];
+  float4 cA[U], cB[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) aA[u] = addr(min(t0 + u * RL, T - 1));
+#pragma unroll
+  for (int u = 0; u < U; ++u) cA[u] = pts[aA[u]];
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  for (;;) {
+    const uint32_t t1 = t0 + kStep, t2 = t1 + kStep;
+#pragma unroll
+    for (int u = 0; u < U; ++u) aB[u] = addr(min(t1 + u * RL, T - 1));
+#pragma unroll
+    for (int u = 0; u < U; ++u) cB[u] = pts[aB[u]];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    consume<RL, U>(t, cA, aA, t0, T, rc.qx, rc.qy, rc.qz);
+#pragma unroll
+    for (int u = 0; u < U; ++u) aA[u] = addr(min(t2 + u * RL, T - 1));
+#pragma unroll
+    for (int u = 0; u < U; ++u) cA[u] = pts[aA[u]];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    consume<RL, U>(t, cB, aB, t1, T, rc.qx, rc.qy, rc.qz);
+    if (t2 >= T) break;
+    t0 = t2;
+  }
+  RSTAMP(3);
+}
+
 template <int LPQ>
 constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
 
@@ -1780,14 +1910,26 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   static_assert(NT >= SLIO_CHUNK, "fit phase needs one lane per point");
   // the pass's LDS; the fused filter step's tail reuses it once the
   // products are written
+  // refinement records of the chunk (alias the Jacobian rows, which the fit
+  // phase writes only after the refinement)
+  struct RefLds {
+    uint64_t top[SLIO_CHUNK][5];
+    float4 q[SLIO_CHUNK];
+    uint8_t slot[SLIO_CHUNK];
+    uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
+    int32_t tab_dl[NT / 16][kTab];
+  };
   struct SearchLds {
-    double rows[SLIO_CHUNK][kRow];
+    union {
+      double rows[SLIO_CHUNK][kRow];
+      RefLds ref;
+    } rr;
     double part[NT / 128][SLIO_NPROD];
     uint32_t nb_pos[SLIO_CHUNK][5];
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
-    int far_cnt;
+    int far_cnt, ref_cnt;
     float4 far_q[SLIO_CHUNK];
     uint8_t far_slot[SLIO_CHUNK];
     uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
@@ -1796,12 +1938,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     SearchLds s;
     TailLds t;
   } lds;
-  auto& rows = lds.s.rows;
+  auto& rows = lds.s.rr.rows;
+  auto& ref = lds.s.rr.ref;
   auto& part = lds.s.part;
   auto& nb_pos = lds.s.nb_pos;
   auto& nb_d5 = lds.s.nb_d5;
   auto& qw = lds.s.qw;
   auto& far_cnt = lds.s.far_cnt;
+  auto& ref_cnt = lds.s.ref_cnt;
   auto& far_q = lds.s.far_q;
   auto& far_slot = lds.s.far_slot;
   auto& far_pre = lds.s.far_pre;
@@ -1814,7 +1958,10 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   const float4* __restrict__ pts = map.pts;
   const uint32_t* __restrict__ start = map.start;
   if (tid == 0) STAMP(0);
-  if (tid == 0) far_cnt = 0;
+  if (tid == 0) {
+    far_cnt = 0;
+    ref_cnt = 0;
+  }
   __syncthreads();
 
   // ---------------- phase 1: exact 5-NN
@@ -1931,85 +2078,29 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       }
     }
     if (!SPHERE) {
-      // (2) the refinements of this wavefront, re-grouped: up to 8 queries
-      // per round, kRefLanes lanes each, every lane with its own share of the
-      // region's runs (the 2 lanes of a query group alone went through up to
-      // 6 batches of run bounds and ~60 dependent candidate steps, holding the
-      // wavefront that long); the owner merges the region's top 5 into its list
-      constexpr int kRefLanes = 8;
-      const int lane = tid & 63;
-      const int rslot = lane / kRefLanes, rsub = lane % kRefLanes;
-      uint64_t need = __ballot(refine && sub == 0);
-      WSTAMP(0, __builtin_amdgcn_s_memrealtime());
-#ifndef SLIO_REFINE_STAMP
-      WSTAMP(3, __popcll(need));
-#endif
-      while (need) {
-        const uint64_t round = need;
-        int src = -1;
-        uint64_t m = need;
+      // (2) the refinement is deferred to the block-wide pass after the
+      // fast path: the query's merged list and bound go to LDS
+      const uint64_t nrf = __ballot(refine && sub == 0);
+      (void)nrf;
+      WSTAMP(3, __popcll(nrf));
+      if (refine && sub == 0) {
+        const int k = atomicAdd(&ref_cnt, 1);
+        ref.slot[k] = (uint8_t)slot;
+        ref.q[k] = make_float4(qx, qy, qz, lim);
 #pragma unroll
-        for (int k = 0; k < 64 / kRefLanes; ++k) {
-          if (m) {
-            if (k == rslot) src = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1;
-          }
-        }
-        need = m;
-        const int sl = max(src, 0);
-        const RunCtx rq{__shfl(cx, sl, 64), __shfl(cy, sl, 64), __shfl(cz, sl, 64),
-                        __shfl(qx, sl, 64), __shfl(qy, sl, 64), __shfl(qz, sl, 64), 2, 0.0f,
-                        __shfl(lim, sl, 64)};
-        Top5 tr;
-        top5_clear(tr);
-#ifdef SLIO_REFINE_STAMP
-        const bool first_round = round == __ballot(refine && sub == 0);
-        if (first_round) WSTAMP(2, __builtin_amdgcn_s_memrealtime());
-#endif
-        if (src >= 0) {
-          const uint64_t rows = sphere_rows(g, rq, rq.lim);
-          // lane rsub of the slot takes runs rsub, rsub + 8, ... of the region:
-          // at most 8 runs, so ONE batch (one round trip for all run bounds)
-          const uint64_t runs = rows | ((rows & 0x739c0ull) << 32);
-          scan_runs<1, U>(pts, start, g, rq, runs & (0x0101010101010101ull << rsub), 0, tr);
-        }
-#ifdef SLIO_REFINE_STAMP
-        if (first_round) WSTAMP(3, __builtin_amdgcn_s_memrealtime());
-#endif
-        group_merge<kRefLanes>(tr);
-        // owner group of a query refined this round: its slot is its rank
-        const int own = lane & ~(LPQ - 1);
-        const bool mine = refine && ((round >> own) & 1ull) && ((m >> own) & 1ull) == 0;
-        const int rank = __popcll(round & ((1ull << own) - 1ull));
-        const int from = min(rank, 64 / kRefLanes - 1) * kRefLanes;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const uint64_t k = __shfl(tr.k[j], from, 64);
-          if (mine) top5_insert(t, k);
-        }
-        if (mine) {
-          // exact once the 5th distance lies inside the 5x5x5 cube's bound
-          // (always, when the block's own 5th distance did: lim = d5)
-          bool cov2;
-          const float b2 = outside_bound(g, cx, cy, cz, 2, qx, qy, qz, cov2);
-          const float d5n = __uint_as_float((uint32_t)(t.k[4] >> 32));
-          done = cov2 || (t.k[4] != kInfKey && b2 > 0.0f && d5n < (b2 * b2) * 0.99999f);
-        }
+        for (int j = 0; j < 5; ++j) ref.top[k][j] = t.k[j];
       }
-      WSTAMP(1, __builtin_amdgcn_s_memrealtime());
     }
     // (3) not finished on the fine grid: deferred to the far queue (the
     // group's list is merged: its 5th distance, if any, bounds the search)
-    if (!done && sub == 0) {
+    if (!done && !refine && sub == 0) {
       const int k = atomicAdd(&far_cnt, 1);
       far_slot[k] = (uint8_t)slot;
       far_q[k] = make_float4(qx, qy, qz,
                              t.k[4] != kInfKey ? __uint_as_float((uint32_t)(t.k[4] >> 32))
                                                : __int_as_float(0x7f800000));
     }
-#ifndef SLIO_REFINE_STAMP
     WSTAMP(2, __builtin_amdgcn_s_memrealtime());
-#endif
     // Nearest_Points / pointSearchSqDis for this point
     // (map indices are written by the fit phase, which loads the points)
 #pragma unroll
@@ -2028,8 +2119,90 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       qw[slot] = make_float4(qx, qy, qz, 0.0f);
     }
   }
-  if ((tid >> 6) < 4) STAMP(4 + (tid >> 6));  // per-wave end of the kNN phase
+  if ((tid >> 6) < 4) STAMP(4 + (tid >> 6));  // per-wave end of the fast path
   __syncthreads();
+  if (!SPHERE) {
+    // (2) the chunk's refinements, spread over the whole workgroup: RL lanes
+    // per query, every lane with its own share of the region's runs (each of
+    // the <= 34 runs of the 5x5x5 cube minus the block goes to lane
+    // run % RL).  A wavefront's refinements used to run on that wavefront
+    // alone, 8 per round at ~10 us a round (latency-bound candidate chains),
+    // so one wave with 30 refining queries set the kernel's end; now the
+    // chunk's queries share all NT lanes, and when few refine, each gets
+    // more lanes (shorter chains).
+    const int nref = ref_cnt;
+    WSTAMP(0, __builtin_amdgcn_s_memrealtime());
+    auto refine_all = [&](auto rl) {
+      constexpr int RL = decltype(rl)::value;
+      constexpr uint64_t pat = 0x0101010101010101ull;  // RL == 8: runs rsub, rsub + 8, ...
+      const int lane = tid & 63;
+      const int rsub = lane % RL;
+      for (int base = (tid >> 6) * (64 / RL); base < nref; base += NT / RL) {
+        const int k = base + lane / RL;
+        const bool has = k < nref;
+        const float4 q = has ? ref.q[k] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        int rx = 0, ry = 0, rz = 0;
+        Top5 tr;
+        top5_clear(tr);
+        uint64_t runs = 0;
+        if (has) {
+          rx = cell_coord(q.x, g.ox, g.inv_h);
+          ry = cell_coord(q.y, g.oy, g.inv_h);
+          rz = cell_coord(q.z, g.oz, g.inv_h);
+        }
+        const RunCtx rq{rx, ry, rz, q.x, q.y, q.z, 2, 0.0f, q.w};
+        if (has) {
+          const uint64_t rows = sphere_rows(g, rq, rq.lim);
+          runs = rows | ((rows & 0x739c0ull) << 32);
+        }
+        if (RL >= 16) {
+          const int grp16 = (tid >> 6) * (64 / RL) + lane / RL;
+          scan_runs_wide<RL, U>(pts, start, g, rq, runs, rsub, ref.tab_pre[grp16], ref.tab_dl[grp16], tr);
+        } else if (has) {
+          scan_runs<1, U>(pts, start, g, rq, runs & (pat << rsub), 0, tr);
+        }
+        group_merge<RL>(tr);
+        if (has && rsub == 0) {
+#pragma unroll
+          for (int j = 0; j < 5; ++j) top5_insert(tr, ref.top[k][j]);
+          // exact once the 5th distance lies inside the 5x5x5 cube's bound
+          // (always, when the block's own 5th distance did: lim = d5)
+          bool cov2;
+          const float b2 = outside_bound(g, rx, ry, rz, 2, q.x, q.y, q.z, cov2);
+          const float d5n = __uint_as_float((uint32_t)(tr.k[4] >> 32));
+          const bool fin = cov2 || (tr.k[4] != kInfKey && b2 > 0.0f && d5n < (b2 * b2) * 0.99999f);
+          const int slot = ref.slot[k];
+          const int64_t i = chunk * SLIO_CHUNK + slot;
+          if (fin) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+              const uint64_t mk = tr.k[j];
+              out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+                                                       : __uint_as_float((uint32_t)(mk >> 32));
+              nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
+            }
+            nb_d5[slot] = (tr.k[4] != kInfKey) ? d5n : __int_as_float(0x7f800000);
+          } else {
+            const int f = atomicAdd(&far_cnt, 1);
+            far_slot[f] = (uint8_t)slot;
+            far_q[f] = make_float4(q.x, q.y, q.z, tr.k[4] != kInfKey ? d5n : __int_as_float(0x7f800000));
+          }
+        }
+      }
+    };
+    if (nref > 0) {
+      if (nref <= NT / 64)
+        refine_all(std::integral_constant<int, 64>{});
+      else if (nref <= NT / 32)
+        refine_all(std::integral_constant<int, 32>{});
+      else if (nref <= NT / 16)
+        refine_all(std::integral_constant<int, 16>{});
+      else
+        refine_all(std::integral_constant<int, 8>{});
+      __syncthreads();
+    }
+    WSTAMP(1, __builtin_amdgcn_s_memrealtime());
+  }
   if (tid == 0) STAMP(1);
   const int nfar = far_cnt;
   if (nfar > 0) {
@@ -2681,6 +2854,12 @@ int slio_debug_stamps(unsigned long long* out, int nblocks) {
 }
 int slio_debug_wstamps(unsigned long long* out, int nblocks) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(unsigned long long) * 16 * nblocks) ==
+                 hipSuccess
+             ? 0
+             : -3;
+}
+int slio_debug_rstamps(unsigned long long* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 4 * nblocks) ==
                  hipSuccess
              ? 0
              : -3;

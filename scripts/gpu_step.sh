@@ -22,6 +22,8 @@ while [ $# -gt 0 ]; do
          rc=$?; echo "stats rc=$rc"; cat gpurun_out/${tag}_stats.log | grep '^{'; [ $rc -eq 0 ] || exit $rc ;;
     bench) timeout -k 10 600 python bench.py --steps 100 --warmup 5 --no-cpu-baseline > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err
          rc=$?; echo "bench rc=$rc"; cat gpurun_out/${tag}_bench.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/${tag}_bench.err; exit $rc; } ;;
+    stamps) LPQS=2 timeout -k 10 300 python -u scripts/stamps.py > gpurun_out/${tag}_stamps.log 2>&1
+         rc=$?; echo "stamps rc=$rc"; cat gpurun_out/${tag}_stamps.log; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $1"; exit 9 ;;
   esac
   shift

@@ -11,7 +11,7 @@ from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 lib = L.load(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
 lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
-    for nscan in [25000, 100000]:
+    for nscan in [100000]:
         mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
         body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)][:nscan])
         st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI])
@@ -37,10 +37,14 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         ws = (C.c_ulonglong * (16 * nb))()
         lib.slio_debug_wstamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
         assert lib.slio_debug_wstamps(ws, nb) == 0
+        rs = (C.c_ulonglong * (4 * nb))()
+        lib.slio_debug_rstamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+        assert lib.slio_debug_rstamps(rs, nb) == 0
+        rsa = np.frombuffer(rs, dtype=np.uint64).reshape(nb, 4).astype(np.int64)
         os.makedirs("gpurun_out", exist_ok=True)
         np.savez(f"gpurun_out/stamps_{lpq}_{nscan}.npz", stamps=a,
                  hwid=np.frombuffer(hw, dtype=np.uint32).reshape(nb, 2),
-                 wstamps=np.frombuffer(ws, dtype=np.uint64).reshape(nb, 4, 4))
+                 wstamps=np.frombuffer(ws, dtype=np.uint64).reshape(nb, 4, 4), rstamps=rsa)
         t0 = a[:, 0].min()
         us = (a - t0) / 100.0   # 100 MHz -> us
         ph1 = us[:, 1] - us[:, 0]; ph2 = us[:, 2] - us[:, 1]; ph3 = us[:, 3] - us[:, 2]
@@ -52,4 +56,22 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         tot = us[:, 3] - us[:, 0]
         print(f"  block total: p10 {np.quantile(tot, .1):.1f} p50 {np.median(tot):.1f} p90 {np.quantile(tot, .9):.1f} max {tot.max():.1f}; "
               f"end times p50 {np.median(us[:, 3]):.1f} p90 {np.quantile(us[:, 3], .9):.1f}")
+        wsa = np.frombuffer(ws, dtype=np.uint64).reshape(nb, 4, 4).astype(np.int64)
+        nref = wsa[:, :, 3]   # refining queries per wave (WSTAMP(3))
+        rdur = (wsa[:, :, 1] - wsa[:, :, 0]) / 100.0
+        print(f"  refining queries per wave: mean {nref.mean():.2f} p90 {np.quantile(nref, .9):.0f} max {nref.max()}; "
+              f"waves with any {np.mean(nref > 0):.3f}; total {nref.sum()}")
+        print(f"  refine duration per wave: mean {rdur.mean():.2f} p90 {np.quantile(rdur, .9):.2f} max {rdur.max():.2f} us")
+        bref = nref.sum(1)
+        one = np.nonzero((bref >= 1) & (bref <= 4) & (rsa[:, 0] > 0))[0]
+        if one.size:
+            seg = np.diff(rsa[one], axis=1) / 100.0
+            st = (rsa[one, 0] - wsa[one, 0, 0]) / 100.0
+            en = (wsa[one, 0, 1] - rsa[one, 3]) / 100.0
+            print(f"  wide refine (blocks with 1-4 refs, n={one.size}): start->entry {st.mean():.2f}, bounds {seg[:, 0].mean():.2f}, "
+                  f"table {seg[:, 1].mean():.2f}, scan {seg[:, 2].mean():.2f}, merge+write+sync {en.mean():.2f} us")
+        slow = np.argsort(-tot)[:5]
+        for b in slow:
+            print(f"    slow block {b}: total {tot[b]:.1f} knn {ph1[b]:.1f} fit {ph2[b]:.1f} refs/wave {[int(v) for v in nref[b]]} "
+                  f"refine us {[round(float(v), 1) for v in rdur[b]]}")
         lib.slio_destroy(h)
