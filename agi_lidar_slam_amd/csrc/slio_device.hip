@@ -1785,24 +1785,23 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
     rs[w] = s0;
     len[w] = e0 - s0;
   }
-  // lengths to the table, then every lane sums them (broadcast reads)
+  // exclusive prefix over the runs in their order j = rsub + w * RL: the
+  // runs of the earlier columns w, then those of the earlier lanes of this
+  // column (a group scan per column)
+  uint32_t own[W], T = 0;
 #pragma unroll
-  for (int w = 0; w < W; ++w)
-    if (rsub + w * RL < kTab) pre[rsub + w * RL] = len[w];
-  wave_fence();
-  RSTAMP(1);
-  uint32_t acc = 0, own[W];
+  for (int w = 0; w < W; ++w) {
+    uint32_t inc = len[w];
 #pragma unroll
-  for (int w = 0; w < W; ++w) own[w] = 0;
-#pragma unroll
-  for (int j = 0; j < 34; ++j) {
-#pragma unroll
-    for (int w = 0; w < W; ++w)
-      if (j == rsub + w * RL) own[w] = acc;
-    if (j < nr) acc += pre[j];
+    for (int d = 1; d < RL; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, RL);
+      if (rsub >= d) inc += v;
+    }
+    own[w] = T + inc - len[w];
+    T += __shfl(inc, RL - 1, RL);
   }
-  const uint32_t T = acc;
-  wave_fence();
+  RSTAMP(1);
+  static_assert(RL * W >= kTab, "every table entry has an owner lane");
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     const int j = rsub + w * RL;
@@ -1811,10 +1810,9 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
       dl[j] = (int32_t)(rs[w] - own[w]);
     }
   }
-  if (RL * W < kTab)  // entries no lane owns
-    for (int j = RL * W + rsub; j < kTab; j += RL) pre[j] = 0xFFFFFFFFu;
   wave_fence();
   RSTAMP(2);
+  if (rsub >= T) RSTAMP(3);
   uint32_t t0 = rsub;
   if (t0 >= T) return;
   auto addr = [&](uint32_t tt) {
@@ -1916,8 +1914,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     uint64_t top[SLIO_CHUNK][5];
     float4 q[SLIO_CHUNK];
     uint8_t slot[SLIO_CHUNK];
-    uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
-    int32_t tab_dl[NT / 16][kTab];
   };
   struct SearchLds {
     union {
@@ -1930,6 +1926,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
     int far_cnt, ref_cnt;
+    uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
+    int32_t tab_dl[NT / 16][kTab];
     float4 far_q[SLIO_CHUNK];
     uint8_t far_slot[SLIO_CHUNK];
     uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
@@ -1946,6 +1944,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& qw = lds.s.qw;
   auto& far_cnt = lds.s.far_cnt;
   auto& ref_cnt = lds.s.ref_cnt;
+  auto& tab_pre = lds.s.tab_pre;
+  auto& tab_dl = lds.s.tab_dl;
   auto& far_q = lds.s.far_q;
   auto& far_slot = lds.s.far_slot;
   auto& far_pre = lds.s.far_pre;
@@ -2123,18 +2123,17 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   __syncthreads();
   if (!SPHERE) {
     // (2) the chunk's refinements, spread over the whole workgroup: RL lanes
-    // per query, every lane with its own share of the region's runs (each of
-    // the <= 34 runs of the 5x5x5 cube minus the block goes to lane
-    // run % RL).  A wavefront's refinements used to run on that wavefront
-    // alone, 8 per round at ~10 us a round (latency-bound candidate chains),
-    // so one wave with 30 refining queries set the kernel's end; now the
-    // chunk's queries share all NT lanes, and when few refine, each gets
-    // more lanes (shorter chains).
+    // per query (64 when at most 4 refine, else 16) scan the region as one
+    // flattened candidate list (scan_runs_wide); with more than 16, 8 lanes
+    // per query, each with a share of the runs (measured faster there: one
+    // round instead of two).  A wavefront's
+    // refinements used to run on that wavefront alone, 8 per round with a
+    // per-lane share of the runs, ~10 us a round, so one wave with 30
+    // refining queries set the kernel's end.
     const int nref = ref_cnt;
     WSTAMP(0, __builtin_amdgcn_s_memrealtime());
     auto refine_all = [&](auto rl) {
       constexpr int RL = decltype(rl)::value;
-      constexpr uint64_t pat = 0x0101010101010101ull;  // RL == 8: runs rsub, rsub + 8, ...
       const int lane = tid & 63;
       const int rsub = lane % RL;
       for (int base = (tid >> 6) * (64 / RL); base < nref; base += NT / RL) {
@@ -2156,10 +2155,12 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           runs = rows | ((rows & 0x739c0ull) << 32);
         }
         if (RL >= 16) {
-          const int grp16 = (tid >> 6) * (64 / RL) + lane / RL;
-          scan_runs_wide<RL, U>(pts, start, g, rq, runs, rsub, ref.tab_pre[grp16], ref.tab_dl[grp16], tr);
+          const int gi = (tid >> 6) * (64 / RL) + lane / RL;
+          scan_runs_wide<RL, U>(pts, start, g, rq, runs, rsub, tab_pre[gi], tab_dl[gi], tr);
         } else if (has) {
-          scan_runs<1, U>(pts, start, g, rq, runs & (pat << rsub), 0, tr);
+          // many refining queries: each lane scans its own share of the runs
+          // (runs rsub, rsub + 8, ...), one batch of run bounds per lane
+          scan_runs<1, U>(pts, start, g, rq, runs & (0x0101010101010101ull << rsub), 0, tr);
         }
         group_merge<RL>(tr);
         if (has && rsub == 0) {
@@ -2193,8 +2194,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     if (nref > 0) {
       if (nref <= NT / 64)
         refine_all(std::integral_constant<int, 64>{});
-      else if (nref <= NT / 32)
-        refine_all(std::integral_constant<int, 32>{});
       else if (nref <= NT / 16)
         refine_all(std::integral_constant<int, 16>{});
       else
