@@ -1,6 +1,6 @@
 // slio_lio.hip -- LIO-SAM front-end on gfx950.
 //
-// One scan = 7 launches on the handle's stream:
+// One scan = 8 launches on the handle's stream:
 //   memset(cell owners)            reset of rangeMat (imageProjection.cpp:146)
 //   k_lio_claim   per point        projectPointCloud filters (:614-636); the
 //                                  cell goes to the smallest point index
@@ -13,15 +13,20 @@
 //   k_lio_smooth  per point        calculateSmoothness (featureExtraction.cpp
 //                                  :108-131) + markOccludedPoints (:137-177) in
 //                                  pull form (each flag computed by its owner)
-//   k_lio_features block per ring  extractFeatures (:183-296): per sector a
-//                                  bitonic sort, the greedy edge / flat picks on
-//                                  one wavefront (ballot over 64 candidates),
-//                                  surface collection and the per-ring
-//                                  pcl::VoxelGrid (sorted voxel keys + centroids)
+//   k_fe_pick     block per (ring, sector)  extractFeatures (:183-296): the
+//                                  sector's std::sort (block radix sort), then
+//                                  one wavefront per variant: the greedy edge /
+//                                  flat picks (ballot over 64 candidates), once
+//                                  per possible prefix of marks from the
+//                                  previous sector (0..5 points)
+//   k_fe_ring     block per ring   variant chain (exact sequential result),
+//                                  labels, corners, surfaceCloudScan, and
+//                                  pcl::VoxelGrid (radix sort, centroids)
 //   k_lio_concat  block per ring   ring-ordered cloud_corner / cloud_surface
 // Rings are independent in extractFeatures (suppression reaches 5 points, the
-// gap between rings' candidate ranges is 10), sectors within a ring are not,
-// so a ring is one workgroup and its 6 sectors run in order.
+// gap between rings' candidate ranges is 10); sectors within a ring interact
+// only through the marks a sector leaves on the next one's first <= 5 points
+// (see PickVar), so all 6 x 6 (sector, variant) greedy runs go in parallel.
 //
 // Deterministic choices where the reference is implementation-defined match
 // oracle/frontend_oracle.cpp: float trig as correctly
@@ -29,6 +34,7 @@
 // entries the reference never initialises are never picked.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <hipcub/block/block_radix_sort.hpp>
 
 #include <algorithm>
 #include <cfloat>
@@ -573,312 +579,399 @@ struct FeatCfg {
 };
 
 constexpr int kFeatThreads = 1024;
+constexpr int kPickThreads = 384;  // per (ring, sector): one wavefront per variant
 
-// -DSLIO_LIO_STAMP: wall-clock phase stamps of k_lio_features per ring
-#ifdef SLIO_LIO_STAMP
-__device__ unsigned long long g_lstamp[256 * 8];  // [ring][slot]
-#define LSTAMP(k)                                                             \
-  do {                                                                        \
-    if (threadIdx.x == 0 && blockIdx.x < 256) g_lstamp[blockIdx.x * 8 + (k)] = wall_clock64(); \
+// Scratch of the feature stage, per ring r, sector j, variant v.
+// Sectors of a ring interact only through the suppression marks a sector's
+// picks leave on the first <= 5 points of the next one (reach <= 5,
+// featureExtraction.cpp:220-237, 247-262), and those marks are a PREFIX of
+// the next sector (every mark range starts right after its pick, at or before
+// the sector's first point).  So each sector runs its greedy picks once per
+// possible prefix length v = 0..5, all in parallel, and the ring's chain then
+// selects, sector by sector, the variant the previous sectors' real marks
+// call for: exactly the sequential reference's result.
+struct PickVar {
+  int32_t corner[20];  // edge picks in pick order (featureExtraction.cpp:209-218)
+  int32_t flat[4];     // LeGO-LOAM flat picks in pick order
+  int32_t ncorner;     // <= 20
+  int32_t nflat;       // LeGO-LOAM: <= 4
+  int32_t fwd_end;     // last position past ep newly flagged by this sector's picks (-1: none)
+  int32_t pad;
+};
+
+struct FeatWork {
+  int32_t* spos;      // [R][6][sort_cap]: sector positions in std::sort order
+  PickVar* var;       // [R][6][6]
+  int8_t* lab;        // [R][6][6][sort_cap]: labels of positions sp..ep
+};
+
+// sector j of a ring (featureExtraction.cpp:191-192)
+__device__ __forceinline__ void sector_bounds(int start, int end, int j, int& sp, int& ep) {
+  sp = (start * (6 - j) + end * j) / 6;
+  ep = (start * (5 - j) + end * (j + 1)) / 6 - 1;
+}
+
+#ifdef SLIO_FE_STAMP
+// diagnostic build only: k_fe_pick phase stamps per (ring, sector, variant)
+__device__ unsigned long long g_fstamp[256 * 36][6];
+#define FSTAMP(k)                                                                  \
+  do {                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.y < 256)                               \
+      g_fstamp[blockIdx.y * 36 + blockIdx.x * 6 + (threadIdx.x >> 6)][k] =         \
+          __builtin_amdgcn_s_memrealtime();                                        \
   } while (0)
-// accumulate the time since the last LSTAMP_T0 into slot k (k = 6, 7)
-#define LSTAMP_T0() unsigned long long lst0_ = wall_clock64()
-#define LSTAMP_ACC(k)                                                          \
-  do {                                                                         \
-    const unsigned long long n_ = wall_clock64();                              \
-    if (threadIdx.x == 0 && blockIdx.x < 256) g_lstamp[blockIdx.x * 8 + (k)] += n_ - lst0_; \
-    lst0_ = n_;                                                                \
+__device__ unsigned long long g_rstamp[256][8];
+#define RGSTAMP(k)                                                                 \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < 256)                                      \
+      g_rstamp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                  \
   } while (0)
 #else
-#define LSTAMP_T0() \
-  do {              \
-  } while (0)
-#define LSTAMP_ACC(k) \
-  do {                \
-  } while (0)
-#define LSTAMP(k) \
+#define FSTAMP(k) \
   do {            \
+  } while (0)
+#define RGSTAMP(k) \
+  do {             \
   } while (0)
 #endif
 
-// one ring per workgroup
+// ---- k_fe_pick: grid (6, R), 6 wavefronts: sector j of ring r.  The block
+// loads the sector (curvature, columns, flags, reach) and sorts it once:
+// std::sort(sp, ep) by smoothness (featureExtraction.cpp:200) as a stable
+// block radix sort of (value bits, position) in position order, so ties fall
+// to the lower index (the oracle's deterministic choice; values are squares
+// >= +0, whose bits order as the floats; entries the reference never
+// initialises sort as 0).  Then wavefront v runs the greedy edge / flat picks
+// with the sector's v leading points pre-flagged (variant v), on its own
+// flags and labels, with register eligibility (a 64-candidate chunk is
+// loaded once; a pick clears the candidates inside its reach range; the
+// chunk's labels and flags go to LDS before the next chunk reads them).
 // MODE kModeLio: LIO-SAM extractFeatures (featureExtraction.cpp:183-296);
 // kModeLego: LeGO-LOAM extractFeatures (featureAssociation.cpp:883-1007):
 // edges only off the ground (labels 2 for the first 2 = sharp, 1 up to 20),
 // flats only on the ground, at most 4 per sector (the 4th does not suppress).
-template <int MODE>
-__global__ __launch_bounds__(kFeatThreads) void k_fe_features(
+template <int MODE, int ITEMS>
+__global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     const CloudInfo ci, const float* __restrict__ curvature, const uint8_t* __restrict__ picked0,
-    FeatCfg cfg, FeatOut out) {
+    const uint8_t* __restrict__ ground, FeatCfg cfg, FeatWork fw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // dynamic LDS: keys[max(sort_cap, vox_cap)] (sector sort, then voxel sort),
-  // then per ring position: curvature, column, surface list, flag, label
-  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);  // sector segments, then voxel keys
-  uint64_t* skeys = keys + max(6 * cfg.sort_cap, cfg.vox_cap);  // sorted sector segments
-  float4* vp = reinterpret_cast<float4*>(skeys + 6 * cfg.sort_cap);  // vox_cap
-  float* curv = reinterpret_cast<float*>(vp + cfg.vox_cap);
-  int32_t* col = reinterpret_cast<int32_t*>(curv + cfg.ring_cap);
-  int32_t* slist = col + cfg.ring_cap;
-  // flags and labels are written by one lane and read by the others of the
-  // same wavefront: volatile LDS accesses, issued in program order
-  volatile uint8_t* flag = reinterpret_cast<volatile uint8_t*>(slist + cfg.ring_cap);
-  volatile int8_t* lab = reinterpret_cast<volatile int8_t*>(flag + cfg.ring_cap);
-  uint8_t* reach = reinterpret_cast<uint8_t*>(const_cast<int8_t*>(lab) + cfg.ring_cap);
-  uint8_t* gfl = reach + cfg.ring_cap;  // LeGO: segmentedCloudGroundFlag
-  __shared__ int s_nsurf, s_ncorner;
-  __shared__ int corner_pos[kCornerPerRing];
-  __shared__ int flat_pos[kFlatPerRing];
-  __shared__ int s_nflat;
-  __shared__ int scratch[kFeatThreads / 64 + 1];
-  __shared__ float s_min[3], s_max[3];
-  __shared__ int s_overflow, s_minb[3], s_mul[3];
-
-  const int r = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  using BRS = hipcub::BlockRadixSort<uint32_t, kPickThreads, ITEMS, int32_t>;
+  __shared__ typename BRS::TempStorage tmp;
+  const int j = blockIdx.x, r = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, v = t >> 6;
   const int n = *ci.n_ext;
   const int start = ci.start_ring[r], end = ci.end_ring[r];
   const int base = max(start - 5, 0);
-  const int span_end = min(end + 5, n - 1);  // last index touched
-  LSTAMP(0);
-  int ncorner = 0, nflat = 0, nsharp = 0;  // wavefront 0 counters (uniform)
-  for (int q = base + t; q <= span_end; q += kFeatThreads) {
-    curv[q - base] = curvature[q];
-    col[q - base] = ci.col_ind[q];
-    flag[q - base] = picked0[q];
-    lab[q - base] = 0;
-    if (MODE == kModeLego) gfl[q - base] = out.ground[q];
+  const int span_end = min(end + 5, n - 1);
+  int sp, ep;
+  sector_bounds(start, end, j, sp, ep);
+  if (sp >= ep) {  // `if (sp >= ep) continue;`
+    if (lane == 0 && (j > 0 || v == 0)) {
+      PickVar* pv = fw.var + (r * 6 + j) * 6 + v;
+      pv->ncorner = 0;
+      pv->nflat = 0;
+      pv->fwd_end = -1;
+    }
+    return;
+  }
+  FSTAMP(0);
+  const int cap = cfg.sort_cap, pcap = cfg.sort_cap + 16;
+  const int pb = max(sp - 5, base), pe = min(ep + 5, span_end);
+  int32_t* spos = reinterpret_cast<int32_t*>(smem);  // the sector in sort order
+  float* curv = reinterpret_cast<float*>(spos + cap);
+  int32_t* col = reinterpret_cast<int32_t*>(curv + pcap);
+  uint8_t* pk0 = reinterpret_cast<uint8_t*>(col + pcap);  // cloudNeighborPicked on entry
+  uint8_t* brk = pk0 + pcap;    // column step into position q exceeds 10
+  uint8_t* reach = brk + pcap;  // reachL | reachR << 4
+  uint8_t* gfl = reach + pcap;  // LeGO: segmentedCloudGroundFlag
+  // the wavefront's own flags and labels: written by one lane and read by
+  // the others of the wavefront: volatile LDS accesses, in program order
+  volatile uint8_t* flag = reinterpret_cast<volatile uint8_t*>(gfl + pcap) + v * 2 * pcap;
+  volatile int8_t* lab = reinterpret_cast<volatile int8_t*>(flag + pcap);
+  for (int q = pb + t; q <= pe; q += kPickThreads) {
+    curv[q - pb] = curvature[q];
+    col[q - pb] = ci.col_ind[q];
+    pk0[q - pb] = picked0[q];
+    if (MODE == kModeLego) gfl[q - pb] = ground[q];
+  }
+  // the sector's sort
+  const int len = ep - sp;
+  {
+    uint32_t key[ITEMS];
+    int32_t val[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int idx = t * ITEMS + i, k = sp + idx;
+      key[i] = 0xFFFFFFFFu;
+      val[i] = 0x7FFFFFFF;
+      if (idx < len) {
+        key[i] = __float_as_uint((k >= 5 && k < n - 5) ? curvature[k] : 0.0f);
+        val[i] = k;
+      }
+    }
+    BRS(tmp).Sort(key, val);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+      if (t * ITEMS + i < len) spos[t * ITEMS + i] = val[i];
   }
   __syncthreads();
-
-  // suppression reach (featureExtraction.cpp:220-237, 247-262): points ind+l,
-  // l = 1..5 (and -1..-5), are flagged while consecutive columns differ by
-  // <= 10, so a pick flags the contiguous range [ind - reachL, ind + reachR]
-  for (int q = base + t; q <= span_end; q += kFeatThreads) {
+  FSTAMP(1);
+  // suppression reach (:220-237, 247-262): points ind + l, l = 1..5 (and
+  // -1..-5), are flagged while consecutive columns differ by <= 10, so a
+  // pick flags the contiguous range [ind - reachL, ind + reachR]
+  for (int q = max(pb + 1, sp - 4) + t; q <= pe; q += kPickThreads)
+    brk[q - pb] = abs(col[q - pb] - col[q - 1 - pb]) > 10;
+  __syncthreads();
+  for (int q = sp + t; q <= ep; q += kPickThreads) {
+    bool okr = true, okl = true;
     int rr = 0, rl = 0;
-    for (int l = 1; l <= 5 && q + l <= span_end; ++l) {
-      if (abs(col[q + l - base] - col[q + l - 1 - base]) > 10) break;
-      rr = l;
+#pragma unroll
+    for (int l = 1; l <= 5; ++l) {
+      okr = okr && q + l <= span_end && !brk[min(q + l, pe) - pb];
+      okl = okl && q - l >= base && !brk[q - l + 1 - pb];
+      rr += okr;
+      rl += okl;
     }
-    for (int l = 1; l <= 5 && q - l >= base; ++l) {
-      if (abs(col[q - l - base] - col[q - l + 1 - base]) > 10) break;
-      rl = l;
-    }
-    reach[q - base] = (uint8_t)(rl | (rr << 4));
+    reach[q - pb] = (uint8_t)(rl | (rr << 4));
   }
   __syncthreads();
-  LSTAMP(1);
+  if (j == 0 && v > 0) return;  // nothing precedes the first sector
+  FSTAMP(2);
+  const int slot = (r * 6 + j) * 6 + v;
+  PickVar* pv = fw.var + slot;
+  for (int q = pb + lane; q <= pe; q += 64) {
+    flag[q - pb] = pk0[q - pb] | (uint8_t)(q >= sp && q < sp + v);
+    lab[q - pb] = 0;
+  }
+  auto ind_at = [&](int k) -> int { return k == ep ? ep : spos[k - sp]; };
+  // edges: k = ep .. sp, at most 20 (:205-238).  [sp, ep) is sorted by
+  // curvature, so below the first sorted value <= edgeThreshold nothing is
+  // eligible: the scan stops there (k = ep, outside the sort, first).
+  int picks = 0;
+  bool stop = false;
+  for (int top = ep; top >= sp && !stop; top -= 64) {
+    const int k = top - lane;
+    int ind = 0, lo = 0, hi = -1, myrank = 0;
+    bool el = false, tail = false, mine = false;
+    if (k >= sp) {
+      ind = ind_at(k);
+      const int bb = ind - pb;
+      const int rc = reach[bb];
+      lo = ind - (rc & 15);
+      hi = ind + (rc >> 4);
+      const float cv = curv[bb];
+      el = !flag[bb] && cv > cfg.edge_thr && (MODE == kModeLio || !gfl[bb]);
+      tail = k < ep && !(cv > cfg.edge_thr);
+    }
+    const bool last_chunk = __ballot(tail) != 0;
+    uint64_t msk = __ballot(el);
+    while (msk) {
+      const int l = __ffsll((long long)msk) - 1;
+      if (++picks > 20) {
+        stop = true;
+        break;
+      }
+      const int lol = __builtin_amdgcn_readlane(lo, l);
+      const int hil = __builtin_amdgcn_readlane(hi, l);
+      if (lane == l) {
+        mine = true;
+        myrank = picks;
+        pv->corner[picks - 1] = ind;
+      }
+      el = el && lane > l && !(ind >= lol && ind <= hil);
+      msk = __ballot(el);
+    }
+    if (mine) {
+      lab[ind - pb] = (MODE == kModeLego && myrank <= 2) ? 2 : 1;
+      for (int q = lo; q <= hi; ++q) flag[q - pb] = 1;
+    }
+    if (last_chunk) break;
+  }
+  FSTAMP(3);
+  // flats: k = sp .. ep (:239-263).  Ascending curvature: the scan stops
+  // after the first sorted value >= surfThreshold; k = ep is examined last.
+  bool done_sorted = false;
+  int fpicks = 0;
+  bool fstop = false;
+  for (int bot = sp; bot < ep && !done_sorted && !fstop; bot += 64) {
+    const int k = bot + lane;
+    int ind = 0, lo = 0, hi = -1;
+    bool el = false, tail = false, mine = false, supp = false;
+    if (k < ep) {
+      ind = ind_at(k);
+      const int bb = ind - pb;
+      const int rc = reach[bb];
+      lo = ind - (rc & 15);
+      hi = ind + (rc >> 4);
+      const float cv = curv[bb];
+      el = !flag[bb] && cv < cfg.surf_thr && (MODE == kModeLio || gfl[bb]);
+      tail = !(cv < cfg.surf_thr);
+    }
+    done_sorted = __ballot(tail) != 0;
+    uint64_t msk = __ballot(el);
+    while (msk) {
+      const int l = __ffsll((long long)msk) - 1;
+      ++fpicks;
+      if (lane == l) {
+        mine = true;
+        if (MODE == kModeLego) pv->flat[fpicks - 1] = ind;
+      }
+      if (MODE == kModeLego && fpicks >= 4) {
+        fstop = true;
+        break;
+      }
+      supp |= lane == l;
+      const int lol = __builtin_amdgcn_readlane(lo, l);
+      const int hil = __builtin_amdgcn_readlane(hi, l);
+      el = el && lane > l && !(ind >= lol && ind <= hil);
+      msk = __ballot(el);
+    }
+    if (mine) lab[ind - pb] = -1;
+    if (supp)
+      for (int q = lo; q <= hi; ++q) flag[q - pb] = 1;
+  }
+  if (!fstop) {  // k = ep (outside the sorted range)
+    const int bb = ep - pb;
+    if (!flag[bb] && curv[bb] < cfg.surf_thr && (MODE == kModeLio || gfl[bb])) {
+      ++fpicks;
+      const int rc = reach[bb];
+      const int lol = ep - (rc & 15), hil = ep + (rc >> 4);
+      if (lane == 0) {
+        lab[bb] = -1;
+        if (MODE == kModeLego) pv->flat[fpicks - 1] = ep;
+      }
+      if (!(MODE == kModeLego && fpicks >= 4) && lane <= hil - lol) flag[lol + lane - pb] = 1;
+    }
+  }
+  FSTAMP(4);
+  int8_t* lout = fw.lab + (int64_t)slot * cap;
+  for (int q = sp + lane; q <= ep; q += 64) lout[q - sp] = lab[q - pb];
+  // marks this sector leaves past its end (a prefix of the next sector)
+  const int qf = ep + 1 + lane;
+  const bool marked = lane < 5 && qf <= pe && flag[qf - pb] && !pk0[qf - pb];
+  const uint64_t mb = __ballot(marked);
+  if (lane == 0) {
+    pv->ncorner = min(picks, 20);
+    pv->nflat = MODE == kModeLego ? min(fpicks, 4) : 0;
+    pv->fwd_end = mb ? ep + 64 - __clzll((long long)mb) : -1;
+  }
+  FSTAMP(5);
+}
 
-  // ---- std::sort(sp, ep) of all 6 sectors at once (the sorts depend only
-  // on the smoothness values, not on the picks): sector j occupies the
-  // segment [j * sort_cap, (j + 1) * sort_cap) of `keys`, padded with ~0, and
-  // a bitonic network with k <= sort_cap sorts every segment independently.
-  // Keys are unique (value, index) pairs, so ties fall to the lower index.
-  __shared__ int s_sp[6], s_ep[6];
-  if (t < 6) {
-    s_sp[t] = (start * (6 - t) + end * t) / 6;
-    s_ep[t] = (start * (5 - t) + end * (t + 1)) / 6 - 1;
+// ---- k_fe_ring: one workgroup per ring.  Variant selection (sector j gets
+// the prefix v_j the earlier sectors' marks reach), the ring's labels,
+// corners in pick order, surfaceCloudScan (:265-269: sector positions with
+// label <= 0, position order), then pcl::VoxelGrid on it: bounding box, leaf
+// divisions ("integer indices would overflow" -> output = input), the sort
+// of (voxel index, list index) as a stable block radix sort of the voxel
+// index over the list order (a voxel's points keep list order), one thread
+// per voxel run start, centroid summed in list order (CentroidPoint), voxels
+// in ascending index (applyFilter).
+template <int MODE, int ITEMS>
+__global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, FeatCfg cfg,
+                                                          FeatOut out, FeatWork fw) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float4* rp = reinterpret_cast<float4*>(smem);                 // ring_cap: the ring's points
+  float4* vp = rp + cfg.ring_cap;                               // vox_cap: voxel order
+  uint64_t* keys = reinterpret_cast<uint64_t*>(vp + cfg.vox_cap);  // vox_cap
+  int32_t* slist = reinterpret_cast<int32_t*>(keys + cfg.vox_cap);  // ring_cap
+  int8_t* labr = reinterpret_cast<int8_t*>(slist + cfg.ring_cap);   // ring_cap
+  using BRS = hipcub::BlockRadixSort<uint32_t, kFeatThreads, ITEMS, int32_t>;
+  __shared__ typename BRS::TempStorage tmp;
+  __shared__ int s_sp[6], s_ep[6], s_slot[6], s_cb[7], s_fb[7];
+  __shared__ int s_hdr[36][3];  // the ring's variants: ncorner, nflat, fwd_end
+  __shared__ int scratch[kFeatThreads / 64 + 1];
+  __shared__ float s_min[3], s_max[3];
+  __shared__ int s_overflow, s_minb[3], s_mul[3], s_bits;
+  const int r = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int start = ci.start_ring[r], end = ci.end_ring[r];
+  RGSTAMP(0);
+  // the ring's points, loaded once (corners, surface list and voxel grid
+  // read them from LDS)
+  for (int q = start + t; q <= end; q += kFeatThreads) rp[q - start] = ci.xyzi[q];
+  if (t < 36) {
+    int sp, ep;
+    sector_bounds(start, end, t / 6, sp, ep);
+    const PickVar& p = fw.var[r * 36 + t];
+    const bool live = sp < ep && (t / 6 > 0 || t % 6 == 0);
+    s_hdr[t][0] = live ? p.ncorner : 0;
+    s_hdr[t][1] = live ? p.nflat : 0;
+    s_hdr[t][2] = live ? p.fwd_end : -1;
   }
   __syncthreads();
-  const int cap = cfg.sort_cap;
-  for (int q = t; q < 6 * cap; q += kFeatThreads) {
-    const int j = q / cap, o = q - j * cap;
-    const int k = s_sp[j] + o;
-    uint64_t kk = ~0ull;
-    if (s_sp[j] < s_ep[j] && k < s_ep[j]) {
-      const float v = (k >= 5 && k < n - 5) ? curv[k - base] : 0.0f;
-      kk = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)k;
-    }
-    keys[q] = kk;
-  }
-  __syncthreads();
-  LSTAMP_T0();
-  // rank sort inside each segment (an LDS-broadcast compare loop beat the
-  // shuffle bitonic network here: 15 vs 21 us on a 2048-point ring)
-  for (int q = t; q < 6 * cap; q += kFeatThreads) {
-    const int j = q / cap, o = q - j * cap;
-    const int len = s_ep[j] - s_sp[j];
-    if (o >= len) continue;
-    const uint64_t me = keys[q];
-    const uint64_t* ks = keys + j * cap;
-    int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-    int i2 = 0;
-    for (; i2 + 4 <= len; i2 += 4) {
-      r0 += ks[i2] < me;
-      r1 += ks[i2 + 1] < me;
-      r2 += ks[i2 + 2] < me;
-      r3 += ks[i2 + 3] < me;
-    }
-    for (; i2 < len; ++i2) r0 += ks[i2] < me;
-    skeys[j * cap + (r0 + r1) + (r2 + r3)] = me;
-  }
-  __syncthreads();
-  LSTAMP_ACC(6);
-  // ---- greedy picks, sector by sector on wavefront 0 (no block barriers).
-  // A 64-candidate chunk is loaded once; inside it the picks only update
-  // register eligibility (a pick clears the candidates inside its reach
-  // range), and the chunk's labels and flags are written to LDS once the
-  // chunk is done, before the next chunk reads them.
-  if (w == 0) {
-    for (int j = 0; j < 6; j++) {
-      const int sp = s_sp[j], ep = s_ep[j];
+  if (t == 0) {
+    int maxfwd = -1, cb = 0, fb = 0, sharp = 0;
+    for (int j = 0; j < 6; ++j) {
+      int sp, ep;
+      sector_bounds(start, end, j, sp, ep);
+      s_sp[j] = sp;
+      s_ep[j] = ep;
+      s_cb[j] = cb;
+      s_fb[j] = fb;
+      s_slot[j] = -1;
       if (sp >= ep) continue;
-      const uint64_t* sk = skeys + j * cap;
-      auto ind_at = [&](int k) -> int { return k == ep ? ep : (int)(uint32_t)sk[k - sp]; };
-      // edges: k = ep .. sp, at most 20 (:205-238).  [sp, ep) is sorted by
-      // curvature, so below the first sorted value <= edgeThreshold nothing
-      // is eligible: the scan stops there (k = ep, outside the sort, first).
-      int picks = 0;
-      bool stop = false;
-      for (int top = ep; top >= sp && !stop; top -= 64) {
-        const int k = top - lane;
-        int ind = 0, lo = 0, hi = -1, myrank = 0;
-        bool el = false, tail = false, mine = false;
-        if (k >= sp) {
-          ind = ind_at(k);
-          const int bb = ind - base;
-          const int rc = reach[bb];
-          lo = ind - (rc & 15);
-          hi = ind + (rc >> 4);
-          const float cv = curv[bb];
-          el = !flag[bb] && cv > cfg.edge_thr && (MODE == kModeLio || !gfl[bb]);
-          tail = k < ep && !(cv > cfg.edge_thr);
-        }
-        const bool last_chunk = __ballot(tail) != 0;
-        uint64_t msk = __ballot(el);
-        while (msk) {
-          const int l = __ffsll((long long)msk) - 1;
-          if (++picks > 20) {
-            stop = true;
-            break;
-          }
-          const int lol = __builtin_amdgcn_readlane(lo, l);
-          const int hil = __builtin_amdgcn_readlane(hi, l);
-          if (lane == l) {
-            mine = true;
-            myrank = picks;
-            corner_pos[ncorner + picks - 1] = ind;
-            if (MODE == kModeLego) out.corner_sharp[(int64_t)r * kCornerPerRing + ncorner + picks - 1] = picks <= 2;
-          }
-          el = el && lane > l && !(ind >= lol && ind <= hil);
-          msk = __ballot(el);
-        }
-        if (mine) {
-          lab[ind - base] = (MODE == kModeLego && myrank <= 2) ? 2 : 1;
-          for (int q = lo; q <= hi; ++q) flag[q - base] = 1;
-        }
-        if (last_chunk) break;
-      }
-      ncorner += min(picks, 20);
-      nsharp += min(picks, 2);
-      // flats: k = sp .. ep (:239-263).  Ascending curvature: the scan stops
-      // after the first sorted value >= surfThreshold; k = ep is examined last.
-      // LeGO-LOAM: ground points only, at most 4 (the 4th is labelled but does
-      // not suppress, featureAssociation.cpp:947-953).
-      bool done_sorted = false;
-      int fpicks = 0;
-      bool fstop = false;
-      for (int bot = sp; bot < ep && !done_sorted && !fstop; bot += 64) {
-        const int k = bot + lane;
-        int ind = 0, lo = 0, hi = -1;
-        bool el = false, tail = false, mine = false, supp = false;
-        if (k < ep) {
-          ind = ind_at(k);
-          const int bb = ind - base;
-          const int rc = reach[bb];
-          lo = ind - (rc & 15);
-          hi = ind + (rc >> 4);
-          const float cv = curv[bb];
-          el = !flag[bb] && cv < cfg.surf_thr && (MODE == kModeLio || gfl[bb]);
-          tail = !(cv < cfg.surf_thr);
-        }
-        done_sorted = __ballot(tail) != 0;
-        uint64_t msk = __ballot(el);
-        while (msk) {
-          const int l = __ffsll((long long)msk) - 1;
-          ++fpicks;
-          if (lane == l) {
-            mine = true;
-            if (MODE == kModeLego) flat_pos[nflat + fpicks - 1] = ind;
-          }
-          if (MODE == kModeLego && fpicks >= 4) {
-            fstop = true;
-            break;
-          }
-          supp |= lane == l;
-          const int lol = __builtin_amdgcn_readlane(lo, l);
-          const int hil = __builtin_amdgcn_readlane(hi, l);
-          el = el && lane > l && !(ind >= lol && ind <= hil);
-          msk = __ballot(el);
-        }
-        if (mine) lab[ind - base] = -1;
-        if (supp)
-          for (int q = lo; q <= hi; ++q) flag[q - base] = 1;
-      }
-      if (!fstop) {  // k = ep (outside the sorted range)
-        const int bb = ep - base;
-        if (!flag[bb] && curv[bb] < cfg.surf_thr && (MODE == kModeLio || gfl[bb])) {
-          ++fpicks;
-          const int rc = reach[bb];
-          const int lol = ep - (rc & 15), hil = ep + (rc >> 4);
-          if (lane == 0) {
-            lab[bb] = -1;
-            if (MODE == kModeLego) flat_pos[nflat + fpicks - 1] = ep;
-          }
-          if (!(MODE == kModeLego && fpicks >= 4) && lane <= hil - lol) flag[lol + lane - base] = 1;
-        }
-      }
-      if (MODE == kModeLego) nflat += min(fpicks, 4);
+      const int vv = min(max(maxfwd - sp + 1, 0), 5);
+      s_slot[j] = (r * 6 + j) * 6 + vv;
+      maxfwd = max(maxfwd, s_hdr[j * 6 + vv][2]);
+      cb += s_hdr[j * 6 + vv][0];
+      fb += s_hdr[j * 6 + vv][1];
+      sharp += min(s_hdr[j * 6 + vv][0], 2);
     }
-    LSTAMP_ACC(7);
-    if (t == 0) {
-      s_ncorner = ncorner;
-      s_nflat = nflat;
-      if (MODE == kModeLego) out.sharp_count[r] = nsharp;
+    s_cb[6] = cb;
+    s_fb[6] = fb;
+    out.corner_count[r] = cb;
+    if (MODE == kModeLego) {
+      out.sharp_count[r] = sharp;
+      out.flat_count[r] = fb;
     }
   }
   __syncthreads();
-  // surfaceCloudScan (:265-269): sector positions k in [sp, ep] with label
-  // <= 0, in position order -- one block-wide compaction over the ring
+  RGSTAMP(1);
+  auto sector_of = [&](int k) {
+    int s = -1;
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj)
+      if (s_slot[jj] >= 0 && k >= s_sp[jj] && k <= s_ep[jj]) s = jj;
+    return s;
+  };
+  for (int q = start + t; q <= end; q += kFeatThreads) {
+    const int s = sector_of(q);
+    const int8_t l = s >= 0 ? fw.lab[(int64_t)s_slot[s] * cfg.sort_cap + (q - s_sp[s])] : (int8_t)0;
+    labr[q - start] = l;
+    out.label[q] = l;
+  }
+  // corners of this ring (sector order, pick order inside a sector)
+  for (int q = t; q < s_cb[6]; q += kFeatThreads) {
+    int s = 0;
+    while (q >= s_cb[s + 1]) ++s;
+    const int p = fw.var[s_slot[s]].corner[q - s_cb[s]];  // a ring position by construction
+    out.corner_stage[(int64_t)r * kCornerPerRing + q] = rp[(p >= start && p <= end) ? p - start : 0];
+    if (MODE == kModeLego) out.corner_sharp[(int64_t)r * kCornerPerRing + q] = (q - s_cb[s]) < 2;
+  }
+  if (MODE == kModeLego) {
+    for (int q = t; q < s_fb[6]; q += kFeatThreads) {
+      int s = 0;
+      while (q >= s_fb[s + 1]) ++s;
+      const int p = fw.var[s_slot[s]].flat[q - s_fb[s]];
+      out.flat_stage[(int64_t)r * kFlatPerRing + q] = rp[(p >= start && p <= end) ? p - start : 0];
+    }
+  }
+  __syncthreads();
+  RGSTAMP(2);
+  int m;
   {
     const int per = (end - start + 1 + kFeatThreads - 1) / kFeatThreads;
     const int q0 = start + t * per, q1 = min(q0 + per, end + 1);
-    auto in_sector = [&](int k) {
-      bool in = false;
-#pragma unroll
-      for (int jj = 0; jj < 6; ++jj) in |= s_sp[jj] < s_ep[jj] && k >= s_sp[jj] && k <= s_ep[jj];
-      return in;
-    };
     int cnt = 0;
-    for (int k = q0; k < q1; ++k) cnt += in_sector(k) && lab[k - base] <= 0;
+    for (int k = q0; k < q1; ++k) cnt += sector_of(k) >= 0 && labr[k - start] <= 0;
     int excl;
-    const int total = block_exclusive_scan<kFeatThreads>(cnt, scratch, excl);
+    m = block_exclusive_scan<kFeatThreads>(cnt, scratch, excl);
     for (int k = q0; k < q1; ++k)
-      if (in_sector(k) && lab[k - base] <= 0) slist[excl++] = k;
-    if (t == 0) s_nsurf = total;
+      if (sector_of(k) >= 0 && labr[k - start] <= 0) slist[excl++] = k;
   }
   __syncthreads();
-  LSTAMP(2);
-
-  // ---- corners of this ring (pick order)
-  const int nc = s_ncorner;
-  for (int q = t; q < nc; q += kFeatThreads) {
-    const int p = corner_pos[q];  // a ring position by construction
-    out.corner_stage[(int64_t)r * kCornerPerRing + q] = ci.xyzi[(p >= start && p <= end) ? p : start];
-  }
-  for (int q = base + t; q <= span_end; q += kFeatThreads)
-    if (q >= start && q <= end) out.label[q] = lab[q - base];
-  if (t == 0) out.corner_count[r] = nc;
-  if (MODE == kModeLego) {
-    const int nf = s_nflat;
-    for (int q = t; q < nf; q += kFeatThreads) {
-      const int p = flat_pos[q];
-      out.flat_stage[(int64_t)r * kFlatPerRing + q] = ci.xyzi[(p >= start && p <= end) ? p : start];
-    }
-    if (t == 0) out.flat_count[r] = nf;
-  }
-
-  // ---- pcl::VoxelGrid(leaf) on surfaceCloudScan
-  const int m = s_nsurf;
+  RGSTAMP(3);
   float4* dst = out.surf_stage + (start - 4);  // ring's first extracted index
   if (m == 0) {
     if (t == 0) out.surf_count[r] = 0;
@@ -887,7 +980,7 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_features(
   {
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (int q = t; q < m; q += kFeatThreads) {
-      const float4 p = ci.xyzi[slist[q]];
+      const float4 p = rp[slist[q] - start];
       mn[0] = fminf(mn[0], p.x);
       mn[1] = fminf(mn[1], p.y);
       mn[2] = fminf(mn[2], p.z);
@@ -933,39 +1026,48 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_features(
       s_mul[0] = 1;
       s_mul[1] = divb[0];
       s_mul[2] = divb[0] * divb[1];
+      // voxel indices lie below divb0 * divb1 * divb2: the sort needs only
+      // that many low bits
+      const uint32_t top = (uint32_t)((int64_t)divb[0] * divb[1] * divb[2] - 1);
+      s_bits = top ? 32 - __clz((int)top) : 1;
     }
     __syncthreads();
   }
+  RGSTAMP(4);
   if (s_overflow) {  // PCL: "Integer indices would overflow", output = input
-    for (int q = t; q < m; q += kFeatThreads) dst[q] = ci.xyzi[slist[q]];
+    for (int q = t; q < m; q += kFeatThreads) dst[q] = rp[slist[q] - start];
     if (t == 0) out.surf_count[r] = m;
     return;
   }
   const float inv = 1.0f / cfg.leaf;
-  const int P = max(pow2ceil(m), 64);
-  for (int q = t; q < P; q += kFeatThreads) {
-    uint64_t kk = ~0ull;
+  uint32_t key[ITEMS];
+  int32_t val[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int q = t * ITEMS + i;
+    key[i] = 0xFFFFFFFFu >> (32 - s_bits);  // above every voxel index: sorts last
+    val[i] = 0x7FFFFFFF;
     if (q < m) {
-      const float4 p = ci.xyzi[slist[q]];
+      const float4 p = rp[slist[q] - start];
       const int i0 = (int)(floorf(p.x * inv) - (float)s_minb[0]);
       const int i1 = (int)(floorf(p.y * inv) - (float)s_minb[1]);
       const int i2 = (int)(floorf(p.z * inv) - (float)s_minb[2]);
-      const uint32_t idx = (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
-      kk = ((uint64_t)idx << 32) | (uint32_t)q;
+      key[i] = (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
+      val[i] = q;
     }
-    keys[q] = kk;
+  }
+  RGSTAMP(5);
+  BRS(tmp).Sort(key, val, 0, s_bits);
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int q = t * ITEMS + i;
+    if (q < m) {
+      keys[q] = ((uint64_t)key[i] << 32) | (uint32_t)val[i];
+      vp[q] = rp[slist[val[i]] - start];
+    }
   }
   __syncthreads();
-  LSTAMP(3);
-  if (P <= 2 * kFeatThreads)
-    bitonic_sort_shfl<kFeatThreads>(keys, P);
-  else
-    bitonic_sort<kFeatThreads>(keys, P);
-  LSTAMP(4);
-  // stage the points in sorted order in LDS: the per-voxel folds below read LDS
-  for (int q = t; q < m; q += kFeatThreads) vp[q] = ci.xyzi[slist[(uint32_t)keys[q]]];
-  __syncthreads();
-  // voxel runs: a thread per run start, centroid in point order
+  RGSTAMP(6);
   const int per = (m + kFeatThreads - 1) / kFeatThreads;
   const int q0 = t * per, q1 = min(q0 + per, m);
   int starts = 0;
@@ -989,7 +1091,92 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_features(
     dst[o++] = make_float4(s0 / cnt, s1 / cnt, s2 / cnt, s3 / cnt);
   }
   if (t == 0) out.surf_count[r] = nvox;
-  LSTAMP(5);
+  RGSTAMP(7);
+}
+
+// dynamic LDS of the feature kernels
+struct FeatSmem {
+  size_t pick, ring;
+};
+inline FeatSmem feat_smem_sizes(const FeatCfg& fc) {
+  const size_t pcap = (size_t)fc.sort_cap + 16;
+  return FeatSmem{4 * (size_t)fc.sort_cap + (4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
+                  24 * (size_t)fc.vox_cap + 21 * (size_t)fc.ring_cap};
+}
+// items per thread of the block radix sorts (0: capacity not supported)
+inline int sort_items(int sort_cap) {
+  return sort_cap <= kPickThreads ? 1 : sort_cap <= 2 * kPickThreads ? 2 : sort_cap <= 3 * kPickThreads ? 3
+         : sort_cap <= 6 * kPickThreads ? 6 : 0;
+}
+inline int vox_items(int vox_cap) {
+  return vox_cap <= kFeatThreads ? 1 : vox_cap <= 4 * kFeatThreads ? vox_cap / kFeatThreads : 0;
+}
+
+inline hipError_t feat_work_alloc(FeatWork& fw, int R, const FeatCfg& fc) {
+  hipError_t e = hipSuccess;
+  auto A = [&](auto*& p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p), bytes);
+  };
+  A(fw.spos, 4 * (size_t)6 * R * fc.sort_cap);
+  A(fw.var, sizeof(PickVar) * 36 * (size_t)R);
+  A(fw.lab, (size_t)36 * R * fc.sort_cap);
+  return e;
+}
+
+inline void feat_work_free(FeatWork& fw) {
+  void* p[] = {fw.spos, fw.var, fw.lab};
+  for (void* q : p)
+    if (q) (void)hipFree(q);
+  fw = FeatWork{};
+}
+
+template <int MODE>
+inline const void* ring_kernel(int vitems) {
+  return vitems == 1 ? (const void*)k_fe_ring<MODE, 1>
+         : vitems == 2 ? (const void*)k_fe_ring<MODE, 2> : (const void*)k_fe_ring<MODE, 4>;
+}
+
+// kernels whose LDS may exceed the 64 KB default
+template <int MODE>
+inline const void* pick_kernel(int sitems) {
+  return sitems == 1 ? (const void*)k_fe_pick<MODE, 1>
+         : sitems == 2 ? (const void*)k_fe_pick<MODE, 2>
+         : sitems == 3 ? (const void*)k_fe_pick<MODE, 3> : (const void*)k_fe_pick<MODE, 6>;
+}
+
+// kernels whose LDS may exceed the 64 KB default
+template <int MODE>
+inline void feat_set_smem(const FeatSmem& s, int sitems, int vitems) {
+  if (s.pick > 32 * 1024)
+    (void)hipFuncSetAttribute(pick_kernel<MODE>(sitems), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s.pick);
+  if (s.ring > 32 * 1024)
+    (void)hipFuncSetAttribute(ring_kernel<MODE>(vitems), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s.ring);
+}
+
+// extractFeatures + per-ring VoxelGrid: 2 launches; ev brackets them (the
+// front-end bench's feature-stage timing)
+template <int MODE>
+inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, const float* curv,
+                            const uint8_t* picked0, const FeatCfg& fc, const FeatOut& fo,
+                            const FeatWork& fw, std::pair<hipEvent_t, hipEvent_t> ev) {
+  const FeatSmem sm = feat_smem_sizes(fc);
+  const dim3 gs(6, R);
+  const uint32_t ps = (uint32_t)sm.pick;
+  const uint8_t* gr = fo.ground;
+  switch (sort_items(fc.sort_cap)) {
+    case 1: hipExtLaunchKernelGGL((k_fe_pick<MODE, 1>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
+    case 2: hipExtLaunchKernelGGL((k_fe_pick<MODE, 2>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
+    case 3: hipExtLaunchKernelGGL((k_fe_pick<MODE, 3>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
+    default: hipExtLaunchKernelGGL((k_fe_pick<MODE, 6>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
+  }
+  const uint32_t rs = (uint32_t)sm.ring;
+  switch (vox_items(fc.vox_cap)) {
+    case 1: hipExtLaunchKernelGGL(k_fe_ring<MODE, 1>, dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, fc, fo, fw); break;
+    case 2: hipExtLaunchKernelGGL(k_fe_ring<MODE, 2>, dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, fc, fo, fw); break;
+    default: hipExtLaunchKernelGGL(k_fe_ring<MODE, 4>, dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, fc, fo, fw); break;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_lio_concat(int n_scan, const int32_t* start_ring,
@@ -1061,9 +1248,9 @@ struct slio_lio {
   int64_t* counts = nullptr;  // device: n_corner, n_surface
   int64_t* h_counts = nullptr;  // pinned: n_ext, n_corner, n_surface
   FeatCfg fc{};
-  size_t feat_smem = 0;
+  FeatWork fw{};
   bool ran = false;
-  // k_lio_features timing
+  // feature-stage timing
   bool prof = false;
   double prof_ms = 0.0;
   int64_t prof_n = 0;
@@ -1099,6 +1286,7 @@ void lio_free(slio_lio* h) {
                  h->surface, h->counts};
   for (void* p : dev)
     if (p) (void)hipFree(p);
+  feat_work_free(h->fw);
   if (h->h_counts) (void)hipHostFree(h->h_counts);
   if (h->own) (void)hipStreamDestroy(h->own);
 }
@@ -1115,6 +1303,15 @@ void lio_free(slio_lio* h) {
 }  // namespace
 
 extern "C" {
+
+#ifdef SLIO_FE_STAMP
+int slio_dbg_fe_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fstamp), sizeof(g_fstamp)) == hipSuccess ? 0 : -1;
+}
+int slio_dbg_ring_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rstamp), sizeof(g_rstamp)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int slio_lio_params_default(slio_lio_params* p) {
   if (!p) return SLIO_EINVAL;
@@ -1207,24 +1404,22 @@ int slio_lio_create(slio_lio_handle* out, const slio_lio_params* p) {
   h->fc.vox_cap = 64;
   while (h->fc.vox_cap < H) h->fc.vox_cap <<= 1;
   h->fc.ring_cap = H + 16;
-  const int kcap = std::max(6 * h->fc.sort_cap, h->fc.vox_cap);
-  h->feat_smem = 8 * (size_t)(kcap + 6 * h->fc.sort_cap) + 16 * (size_t)h->fc.vox_cap +
-                 (4 + 4 + 4 + 1 + 1 + 1 + 1) * (size_t)h->fc.ring_cap + 16;
-  if (6 * h->fc.sort_cap > 4 * kFeatThreads) {
-    set_error("slio_lio_create: horizon_scan too large for the sector sort");
+  const FeatSmem fsm = feat_smem_sizes(h->fc);
+  if (std::max(fsm.pick, fsm.ring) > 96 * 1024 || !sort_items(h->fc.sort_cap) ||
+      !vox_items(h->fc.vox_cap)) {
+    set_error("slio_lio_create: horizon_scan too large for the feature kernels' LDS layout");
     lio_free(h);
     delete h;
     return SLIO_EINVAL;
   }
-  if (h->feat_smem > 160 * 1024 - 2048) {
-    set_error("slio_lio_create: horizon_scan too large for the per-ring LDS layout");
+  e = feat_work_alloc(h->fw, p->n_scan, h->fc);
+  if (e) {
+    set_error(std::string("slio_lio_create: ") + hipGetErrorString(e));
     lio_free(h);
     delete h;
-    return SLIO_EINVAL;
+    return SLIO_ENOMEM;
   }
-  if (h->feat_smem > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)k_fe_features<kModeLio>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->feat_smem);
+  feat_set_smem<kModeLio>(fsm, sort_items(h->fc.sort_cap), vox_items(h->fc.vox_cap));
   *out = h;
   return SLIO_OK;
 }
@@ -1320,9 +1515,7 @@ int slio_lio_run_async(slio_lio_handle h) {
     }
     h->pending.push_back(ev);
   }
-  hipExtLaunchKernelGGL(k_fe_features<kModeLio>, dim3(R), dim3(kFeatThreads), (uint32_t)h->feat_smem,
-                        h->stream, ev.first, ev.second, 0, ci, (const float*)h->curvature,
-                        (const uint8_t*)h->picked0, h->fc, fo);
+  launch_features<kModeLio>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw, ev);
   k_lio_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
   LIO_HIP(hipGetLastError());
   h->ran = true;
@@ -1434,11 +1627,6 @@ int slio_lio_get_clouds(slio_lio_handle h, float* corner_xyzi, float* surface_xy
 
 }  // extern "C"
 
-#ifdef SLIO_LIO_STAMP
-extern "C" int slio_dbg_lio_stamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstamp), sizeof(g_lstamp)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // ======================================================================
 // LeGO-LOAM.  One scan = 14 launches:
@@ -2088,7 +2276,7 @@ struct slio_lego {
   float4 *c_sharp = nullptr, *c_less_sharp = nullptr, *c_flat = nullptr, *c_less_flat = nullptr;
   int64_t* counts = nullptr;
   FeatCfg fc{};
-  size_t feat_smem = 0;
+  FeatWork fw{};
   bool ran = false;
   bool prof = false;
   double prof_ms = 0.0;
@@ -2126,6 +2314,7 @@ void lego_free(slio_lego* h) {
                  h->c_less_flat, h->counts};
   for (void* p : dev)
     if (p) (void)hipFree(p);
+  feat_work_free(h->fw);
   if (h->own) (void)hipStreamDestroy(h->own);
 }
 
@@ -2256,18 +2445,21 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   h->fc.vox_cap = 64;
   while (h->fc.vox_cap < H) h->fc.vox_cap <<= 1;
   h->fc.ring_cap = H + 16;
-  const int kcap = std::max(6 * h->fc.sort_cap, h->fc.vox_cap);
-  h->feat_smem = 8 * (size_t)(kcap + 6 * h->fc.sort_cap) + 16 * (size_t)h->fc.vox_cap +
-                 (4 + 4 + 4 + 1 + 1 + 1 + 1) * (size_t)h->fc.ring_cap + 16;
-  if (6 * h->fc.sort_cap > 4 * kFeatThreads || h->feat_smem > 160 * 1024 - 4096) {
-    set_error("slio_lego_create: horizon_scan too large for the per-ring LDS layout");
+  const FeatSmem fsm = feat_smem_sizes(h->fc);
+  if (std::max(fsm.pick, fsm.ring) > 96 * 1024 || !sort_items(h->fc.sort_cap) ||
+      !vox_items(h->fc.vox_cap)) {
+    set_error("slio_lego_create: horizon_scan too large for the feature kernels' LDS layout");
     lego_free(h);
     delete h;
     return SLIO_EINVAL;
   }
-  if (h->feat_smem > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)k_fe_features<kModeLego>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->feat_smem);
+  if (feat_work_alloc(h->fw, p->n_scan, h->fc) != hipSuccess) {
+    set_error("slio_lego_create: out of device memory");
+    lego_free(h);
+    delete h;
+    return SLIO_ENOMEM;
+  }
+  feat_set_smem<kModeLego>(fsm, sort_items(h->fc.sort_cap), vox_items(h->fc.vox_cap));
   *out = h;
   return SLIO_OK;
 }
@@ -2413,9 +2605,7 @@ int slio_lego_run_async(slio_lego_handle h) {
     }
     h->pending.push_back(ev);
   }
-  hipExtLaunchKernelGGL(k_fe_features<kModeLego>, dim3(R), dim3(kFeatThreads),
-                        (uint32_t)h->feat_smem, h->stream, ev.first, ev.second, 0, ci,
-                        (const float*)h->curvature, (const uint8_t*)h->picked0, h->fc, fo);
+  launch_features<kModeLego>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw, ev);
   k_lego_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->c_sharp, h->c_less_sharp,
                                           h->c_flat, h->c_less_flat, h->counts);
   LIO_HIP(hipGetLastError());

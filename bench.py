@@ -100,7 +100,7 @@ def bench_c3(args, rank, world, dev, dist):
     value = args.steps * world / el
     avg_s = (ms.value / max(nl.value, 1)) * 1e-3
     n_ext, nc, ns = counts.n_extracted, counts.n_corner, counts.n_surface
-    # k_lio_features compulsory bytes: per extracted point curvature 4 + column 4
+    # feature stage (k_fe_pick .. k_fe_voxel) compulsory bytes: per extracted point curvature 4 + column 4
     # + flag 1 + label 4 + the point 16 (surface / corner gathers), and the
     # corner / surface outputs 16 B each
     alg_bytes = 29 * n_ext + 16 * (nc + ns)
@@ -150,7 +150,7 @@ def bench_c3(args, rank, world, dev, dist):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_lio_features",
+            "kernel": "feature stage: k_fe_pick + k_fe_chain + k_fe_vrank + k_fe_voxel (one timed span)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

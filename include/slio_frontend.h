@@ -75,8 +75,9 @@ int slio_lio_run_async(slio_lio_handle h);
 int slio_lio_run(slio_lio_handle h, slio_lio_counts* counts);
 int slio_lio_get_counts(slio_lio_handle h, slio_lio_counts* counts);
 
-/* Kernel timing: enable != 0 times every k_lio_features launch (the
- * dominant kernel; start/stop hipEvents carried in the dispatch packet) and
+/* Kernel timing: enable != 0 times every feature stage (k_fe_pick start to
+ * k_fe_voxel end, the dominant part; start/stop hipEvents carried in the
+ * dispatch packets) and
  * accumulates device milliseconds; 0 disables.  SLIO_LIO_PROFILE_KEEP keeps
  * the totals (pause / resume).  Read: accumulated ms and launch count
  * (synchronises the stream). */
