@@ -12,7 +12,9 @@
 //   * float sin/cos/atan2 are evaluated in double and rounded to float (the
 //     correctly rounded float value);
 //   * std::sort ties (featureExtraction.cpp:201-202, VoxelGrid's index sort)
-//     are broken by point index;
+//     are broken by point index (orc_lio_features_ex / voxel_grid_pcl_order
+//     also run the reference's own std::sort calls, to count ties and show
+//     whether the order changes anything);
 //   * smoothness entries the reference never initialises (index < 5 or
 //     >= cloudSize - 5; read for ring 0 sector 0, featureExtraction.cpp:196)
 //     are {value 0, ind = own index} with neighbourPicked = 1.
@@ -339,11 +341,16 @@ int64_t orc_lio_project(int n_scan, int horizon, int downsample_rate, float min_
 // PCL VoxelGrid::applyFilter with downsample_all_data_ / CentroidPoint).
 // out: curvature[n], picked0[n] (after markOccludedPoints), label[n] (final),
 //      corner_xyzi / surface_xyzi (capacity n); counts via n_corner/n_surface.
-int orc_lio_features(int n_scan, float edge_threshold, float surf_threshold, float leaf,
-                     const int32_t* start_ring, const int32_t* end_ring, const int32_t* col_ind,
-                     const float* prange, const float* ext_xyzi, int64_t n, float* curvature,
-                     uint8_t* picked0, int32_t* label, float* corner_xyzi, int64_t* n_corner,
-                     float* surface_xyzi, int64_t* n_surface) {
+// std_ties = 0: ties of the sector sort by point index (the device's order);
+// 1: the reference's own call, std::sort over {float value; size_t ind}
+// elements with by_value (value only, featureExtraction.cpp:16-20, 201-202),
+// i.e. libstdc++ introsort's order for equal values.  n_tied (optional):
+// keys that share their value with another key of the same sector sort.
+int orc_lio_features_ex(int n_scan, float edge_threshold, float surf_threshold, float leaf,
+                        const int32_t* start_ring, const int32_t* end_ring, const int32_t* col_ind,
+                        const float* prange, const float* ext_xyzi, int64_t n, float* curvature,
+                        uint8_t* picked0, int32_t* label, float* corner_xyzi, int64_t* n_corner,
+                        float* surface_xyzi, int64_t* n_surface, int std_ties, int64_t* n_tied) {
   std::vector<float> sval;
   std::vector<int> picked;
   smooth_occlude(prange, col_ind, n, curvature, picked, sval);
@@ -374,23 +381,42 @@ int orc_lio_features(int n_scan, float edge_threshold, float surf_threshold, flo
       const int sp = (start_ring[i] * (6 - j) + end_ring[i] * j) / 6;
       const int ep = (start_ring[i] * (5 - j) + end_ring[i] * (j + 1)) / 6 - 1;
       if (sp >= ep) continue;
-      // std::sort(begin + sp, begin + ep, by_value), ties by index
-      order.resize(ep - sp);
-      for (int k = sp; k < ep; ++k) order[k - sp] = k;
-      std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-        if (sval[a] != sval[b]) return sval[a] < sval[b];
-        return sind[a] < sind[b];
-      });
-      std::vector<float> v2(ep - sp);
-      std::vector<int64_t> i2(ep - sp);
-      for (int k = sp; k < ep; ++k) {
-        v2[k - sp] = sval[order[k - sp]];
-        i2[k - sp] = sind[order[k - sp]];
+      if (std_ties) {
+        // the reference's element type and comparator, sorted in place
+        struct smoothness_t {
+          float value;
+          size_t ind;
+        };
+        std::vector<smoothness_t> cs(ep - sp);
+        for (int k = sp; k < ep; ++k) cs[k - sp] = smoothness_t{sval[k], (size_t)sind[k]};
+        std::sort(cs.begin(), cs.end(),
+                  [](const smoothness_t& a, const smoothness_t& b) { return a.value < b.value; });
+        for (int k = sp; k < ep; ++k) {
+          sval[k] = cs[k - sp].value;
+          sind[k] = (int64_t)cs[k - sp].ind;
+        }
+      } else {
+        // std::sort(begin + sp, begin + ep, by_value), ties by index
+        order.resize(ep - sp);
+        for (int k = sp; k < ep; ++k) order[k - sp] = k;
+        std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+          if (sval[a] != sval[b]) return sval[a] < sval[b];
+          return sind[a] < sind[b];
+        });
+        std::vector<float> v2(ep - sp);
+        std::vector<int64_t> i2(ep - sp);
+        for (int k = sp; k < ep; ++k) {
+          v2[k - sp] = sval[order[k - sp]];
+          i2[k - sp] = sind[order[k - sp]];
+        }
+        for (int k = sp; k < ep; ++k) {
+          sval[k] = v2[k - sp];
+          sind[k] = i2[k - sp];
+        }
       }
-      for (int k = sp; k < ep; ++k) {
-        sval[k] = v2[k - sp];
-        sind[k] = i2[k - sp];
-      }
+      if (n_tied)
+        for (int k = sp; k < ep; ++k)
+          *n_tied += (k > sp && sval[k] == sval[k - 1]) || (k + 1 < ep && sval[k] == sval[k + 1]);
       int largestPickedNum = 0;
       for (int k = ep; k >= sp; k--) {
         const int64_t ind = sind[k];
@@ -422,6 +448,16 @@ int orc_lio_features(int n_scan, float edge_threshold, float surf_threshold, flo
   *n_corner = nc;
   *n_surface = ns;
   return 0;
+}
+
+int orc_lio_features(int n_scan, float edge_threshold, float surf_threshold, float leaf,
+                     const int32_t* start_ring, const int32_t* end_ring, const int32_t* col_ind,
+                     const float* prange, const float* ext_xyzi, int64_t n, float* curvature,
+                     uint8_t* picked0, int32_t* label, float* corner_xyzi, int64_t* n_corner,
+                     float* surface_xyzi, int64_t* n_surface) {
+  return orc_lio_features_ex(n_scan, edge_threshold, surf_threshold, leaf, start_ring, end_ring, col_ind,
+                             prange, ext_xyzi, n, curvature, picked0, label, corner_xyzi, n_corner,
+                             surface_xyzi, n_surface, 0, nullptr);
 }
 
 }  // extern "C"

@@ -362,6 +362,8 @@ def _bind_frontend(lib):
     lib.orc_lio_features.restype = C.c_int
     lib.orc_lio_features.argtypes = [C.c_int, C.c_float, C.c_float, C.c_float, _IP, _IP, _IP,
                                      _FP, _FP, C.c_int64, _FP, _U8P, _IP, _FP, _I64P, _FP, _I64P]
+    lib.orc_lio_features_ex.restype = C.c_int
+    lib.orc_lio_features_ex.argtypes = lib.orc_lio_features.argtypes + [C.c_int, _I64P]
     lib._fe_bound = True
 
 
@@ -403,8 +405,11 @@ def lio_project(scan: dict, n_scan: int, horizon: int, deskew_table=None, downsa
 
 
 def lio_features(info: dict, n_scan: int, edge_threshold: float = 1.0, surf_threshold: float = 0.1,
-                 leaf: float = 0.4) -> dict:
-    """featureExtraction.cpp:108-296 on the CPU."""
+                 leaf: float = 0.4, std_sort_ties: bool = False) -> dict:
+    """featureExtraction.cpp:108-296 on the CPU.  std_sort_ties: the sector
+    sorts as the reference's own std::sort(by_value) call (libstdc++ order for
+    equal values) instead of ties by point index; the result's "ties" counts
+    the keys that share their value inside a sector sort."""
     lib = load()
     _bind_frontend(lib)
     n = info["pointRange"].shape[0]
@@ -418,14 +423,15 @@ def lio_features(info: dict, n_scan: int, edge_threshold: float = 1.0, surf_thre
     lb = np.empty(n, np.int32)
     co = np.empty((max(n, 1), 4), np.float32)
     su = np.empty((max(n, 1), 4), np.float32)
-    nc, ns = C.c_int64(), C.c_int64()
-    lib.orc_lio_features(n_scan, edge_threshold, surf_threshold, leaf, st.ctypes.data_as(_IP),
+    nc, ns, nt = C.c_int64(), C.c_int64(), C.c_int64(0)
+    lib.orc_lio_features_ex(n_scan, edge_threshold, surf_threshold, leaf, st.ctypes.data_as(_IP),
                          en.ctypes.data_as(_IP), ci.ctypes.data_as(_IP), pr.ctypes.data_as(_FP),
                          xyzi.ctypes.data_as(_FP), n, cv.ctypes.data_as(_FP),
                          pk.ctypes.data_as(_U8P), lb.ctypes.data_as(_IP), co.ctypes.data_as(_FP),
-                         C.byref(nc), su.ctypes.data_as(_FP), C.byref(ns))
+                         C.byref(nc), su.ctypes.data_as(_FP), C.byref(ns), int(std_sort_ties),
+                         C.byref(nt))
     return dict(cloudCurvature=cv, cloudNeighborPicked=pk, cloudLabel=lb,
-                cloud_corner=co[:nc.value].copy(), cloud_surface=su[:ns.value].copy())
+                cloud_corner=co[:nc.value].copy(), cloud_surface=su[:ns.value].copy(), ties=nt.value)
 
 
 # ---------------------------------------------------------------- LeGO-LOAM front-end

@@ -232,3 +232,23 @@ def test_oracle_empty_and_tiny(oracle_mod):
     np.testing.assert_array_equal(info["endRingIndex"], np.full(8, -6))
     fe = oracle_mod.lio_features(info, 8)
     assert fe["cloud_corner"].shape[0] == 0 and fe["cloud_surface"].shape[0] == 0
+
+
+def test_c3_reference_sort_ties(oracle_mod):
+    """The reference sorts each sector with std::sort(by_value) on the value
+    alone (featureExtraction.cpp:16-20, 201-202), so equal smoothness values
+    come out in libstdc++ introsort's order; the device and the oracle break
+    ties by point index.  On C3 (64 x 2048 Ouster scan) 150 keys share their
+    value with another key of the same sector, and the reference's own
+    std::sort call yields the identical labels, corners and surface cloud."""
+    from agi_lidar_slam_amd import synth
+
+    sc = synth.make_ouster_scan()
+    tb = imu_deskew_table(sc["imu_stamps"], sc["imu_gyro"], sc["time_scan_cur"], sc["time_scan_end"])
+    info = oracle_mod.lio_project(sc, 64, 2048, tb)
+    by_index = oracle_mod.lio_features(info, 64)
+    by_ref = oracle_mod.lio_features(info, 64, std_sort_ties=True)
+    assert by_index["ties"] == by_ref["ties"] > 0
+    np.testing.assert_array_equal(by_index["cloudLabel"], by_ref["cloudLabel"])
+    np.testing.assert_array_equal(by_index["cloud_corner"], by_ref["cloud_corner"])
+    np.testing.assert_array_equal(by_index["cloud_surface"], by_ref["cloud_surface"])
