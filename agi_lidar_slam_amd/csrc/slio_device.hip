@@ -1922,6 +1922,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     } rr;
     double part[NT / 128][SLIO_NPROD];
     uint32_t nb_pos[SLIO_CHUNK][5];
+    float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
@@ -1940,6 +1941,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& ref = lds.s.rr.ref;
   auto& part = lds.s.part;
   auto& nb_pos = lds.s.nb_pos;
+  auto& nb_sqd = lds.s.nb_sqd;
   auto& nb_d5 = lds.s.nb_d5;
   auto& qw = lds.s.qw;
   auto& far_cnt = lds.s.far_cnt;
@@ -2101,13 +2103,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
                                                : __int_as_float(0x7f800000));
     }
     WSTAMP(2, __builtin_amdgcn_s_memrealtime());
-    // Nearest_Points / pointSearchSqDis for this point
-    // (map indices are written by the fit phase, which loads the points)
+    // Nearest_Points / pointSearchSqDis for this point, to LDS: the fit phase
+    // writes them out (no global stores in the kNN phase, whose workgroup
+    // barriers would wait for them)
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       if (j % LPQ == sub && live && done) {
         const uint64_t mk = t.k[j];
-        out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+        nb_sqd[slot][j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                  : __uint_as_float((uint32_t)(mk >> 32));
         nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
       }
@@ -2178,7 +2181,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
               const uint64_t mk = tr.k[j];
-              out.nbr_sqd[i * 5 + j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+              nb_sqd[slot][j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                        : __uint_as_float((uint32_t)(mk >> 32));
               nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
             }
@@ -2221,7 +2224,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
 #pragma unroll
       for (int j = 1; j < 5; ++j) mk = (lane == j) ? tf.k[j] : mk;
       if (lane < 5) {
-        out.nbr_sqd[i * 5 + lane] = (mk == kInfKey) ? __int_as_float(0x7f800000)
+        nb_sqd[slot][lane] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                     : __uint_as_float((uint32_t)(mk >> 32));
         nb_pos[slot][lane] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
       }
@@ -2267,6 +2270,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb[j][2] = c.z;
         out.nbr_idx[i * 5 + j] = (int32_t)__float_as_uint(c.w);
         out.nbr_pos[i * 5 + j] = ps;
+        out.nbr_sqd[i * 5 + j] = nb_sqd[slot][j];
       }
       if (cfg.knn_only) sel = false;
       if (sel) {
