@@ -559,6 +559,20 @@ __device__ __forceinline__ void group_merge(Top5& t) {
   }
 }
 
+// The same merge as a rolled loop over ds_bpermute rounds: for cold code
+// (the refinement path runs in few workgroups, so its instructions are
+// rarely in the instruction cache, and the unrolled DPP merge is ~5 KB).
+__device__ __forceinline__ void group_merge_rolled(Top5& t, int width) {
+#pragma unroll 1
+  for (int m = 1; m < width; m <<= 1) {
+    uint64_t ok[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) ok[j] = __shfl_xor(t.k[j], m);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) top5_insert(t, ok[j]);
+  }
+}
+
 // Conservative lower bound of the distance from coordinate q to the points
 // assigned to grid cell i along one axis (cell edges are known to +-tol).
 __device__ __forceinline__ float axis_gap(float q, int i, float o, float h, float tol) {
@@ -2165,7 +2179,11 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           // (runs rsub, rsub + 8, ...), one batch of run bounds per lane
           scan_runs<1, U>(pts, start, g, rq, runs & (0x0101010101010101ull << rsub), 0, tr);
         }
+#ifdef SLIO_REFINE_DPP_MERGE
         group_merge<RL>(tr);
+#else
+        group_merge_rolled(tr, RL);
+#endif
         if (has && rsub == 0) {
 #pragma unroll
           for (int j = 0; j < 5; ++j) top5_insert(tr, ref.top[k][j]);

@@ -6,7 +6,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
+from agi_lidar_slam_amd import _lib as L, shard, synth  # noqa: E402
 
 lib = L.load(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
 lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
@@ -14,7 +14,9 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
     for nscan in [100000]:
         mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
         body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)][:nscan])
-        st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI])
+        at_gt = os.environ.get("STAMP_POSE", "init") == "gt"
+        st = np.concatenate([fr.gt_pos if at_gt else fr.init_pos, fr.gt_rot if at_gt else fr.init_rot,
+                             [1, 0, 0, 0], synth.AVIA_T_LI])
         pose = L.SlioPose()
         pose.pos[:] = list(st[0:3]); pose.rot[:] = list(st[3:7])
         pose.rli[:] = list(st[7:11]); pose.tli[:] = list(st[11:14])
@@ -27,7 +29,7 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         HTH = np.zeros(78); HTh = np.zeros(12); m = C.c_int64()
         for _ in range(5):
             L.check(lib.slio_iterate(h, C.byref(pose), 1, 0, L.dptr(HTH), L.dptr(HTh), C.byref(m)), "it")
-        nb = (nscan + 127) // 128
+        nb = shard.num_chunks(nscan)
         buf = (C.c_ulonglong * (8 * nb))()
         assert lib.slio_debug_stamps(buf, nb) == 0
         a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
