@@ -165,6 +165,11 @@ struct MapDev {
   uint32_t next_id = 0;
   uint64_t version = 1;           // bumped by every rebuild (positions change)
   bool dirty = false;
+  // block rows of a rebuilt map are built once it has been searched
+  // kBlkAfterPasses times unchanged (a map changed every scan goes without:
+  // they cost ~1 ms per rebuild and save ~5 us per search pass)
+  bool blk_deferred = false;
+  int stable_passes = 0;
   float cell0 = 1.0f;             // requested grid cell and cell budget (slio_params)
   int64_t max_cells = 0;
   // device allocations kept across index rebuilds (capacity in bytes): a
@@ -262,11 +267,26 @@ __global__ void k_cell_keys(const float* __restrict__ x, const float* __restrict
   vals[i] = (uint32_t)i;
 }
 
-__global__ void k_cell_hist(const uint32_t* __restrict__ keys, int64_t n,
-                            uint32_t* __restrict__ counts) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  atomicAdd(&counts[keys[i]], 1u);
+// per-cell counts of SORTED keys (cell = key >> shift): one atomic per run of
+// equal cells inside a wavefront (sorted keys put up to 64 lanes on one
+// counter; per-lane atomics serialised there: 0.64 ms for the coarse level
+// of a 10M map)
+template <typename K>
+__global__ void k_cell_hist_sorted(const K* __restrict__ keys, int64_t n, int shift,
+                                   uint32_t* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  const uint32_t c = live ? (uint32_t)(keys[i] >> shift) : 0xFFFFFFFFu;
+  const int lane = threadIdx.x & 63;
+  const uint32_t prev = __shfl_up(c, 1, 64);
+  const bool head = live && (lane == 0 || prev != c);
+  const uint64_t heads = __ballot(head);
+  const uint64_t livem = __ballot(live);
+  if (head) {
+    const uint64_t above = lane == 63 ? 0ull : heads & ~((2ull << lane) - 1ull);
+    const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll((long long)livem);
+    atomicAdd(&counts[c], (uint32_t)(end - lane));
+  }
 }
 
 __global__ void k_gather_sorted(const float* __restrict__ x, const float* __restrict__ y,
@@ -278,45 +298,79 @@ __global__ void k_gather_sorted(const float* __restrict__ x, const float* __rest
   pts[i] = make_float4(x[o], y[o], z[o], __uint_as_float(o));
 }
 
-// block rows: entry sizes, then the fill (one thread per cell; the 9 source
-// cells in (z, y) order, each cell's points in pts order)
-__global__ void k_blk_count(const uint32_t* __restrict__ start, GridGeom g, int64_t ncells,
-                            uint32_t* __restrict__ cnt9) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncells) return;
-  const int x = (int)(c % g.dx);
-  const int y = (int)((c / g.dx) % g.dy);
-  const int z = (int)(c / ((int64_t)g.dx * g.dy));
-  uint32_t s = 0;
+// block rows: entry sizes, then the fill, one thread per cell.  A source
+// row (y + j, z + k) whose start[] is equal at both ends of a segment of
+// kBlkSeg x cells is empty there: k_blk_live marks the live rows per segment
+// (2 loads a row), and the cell threads read only those (95 % of a 10M
+// street map's 33M cells are empty; every cell thread used to spend 18 loads).
+// Sources in (z, y) order, each cell's points in pts order.
+constexpr int kBlkSeg = 16;
+constexpr int kBlkAfterPasses = 8;
+__device__ __forceinline__ uint32_t blk_rows_live(const uint32_t* __restrict__ start, GridGeom g, int x0,
+                                                  int x1, int y, int z) {
+  uint32_t live = 0;
   for (int k = -1; k <= 1; ++k)
     for (int j = -1; j <= 1; ++j) {
       const int yy = y + j, zz = z + k;
+      const int q = (k + 1) * 3 + (j + 1);
       if (yy < 0 || yy >= g.dy || zz < 0 || zz >= g.dz) continue;
-      const int64_t sc = ((int64_t)zz * g.dy + yy) * g.dx + x;
-      s += start[sc + 1] - start[sc];
+      const int64_t rb = ((int64_t)zz * g.dy + yy) * g.dx;
+      if (start[rb + x1] != start[rb + x0]) live |= 1u << q;
     }
+  return live;
+}
+
+// live source rows of every segment (9 bits)
+__global__ void k_blk_live(const uint32_t* __restrict__ start, GridGeom g, int64_t nseg,
+                           uint16_t* __restrict__ live) {
+  const int64_t sg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sg >= nseg) return;
+  const int segs = (g.dx + kBlkSeg - 1) / kBlkSeg;
+  const int x0 = (int)(sg % segs) * kBlkSeg, x1 = min(x0 + kBlkSeg, g.dx);
+  const int y = (int)((sg / segs) % g.dy);
+  const int z = (int)(sg / ((int64_t)segs * g.dy));
+  live[sg] = (uint16_t)blk_rows_live(start, g, x0, x1, y, z);
+}
+
+// one thread per cell; only the segment's live source rows are read
+__global__ void k_blk_count(const uint32_t* __restrict__ start, const uint16_t* __restrict__ live,
+                            GridGeom g, int64_t ncells, uint32_t* __restrict__ cnt9) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncells) return;
+  const int x = (int)(c % g.dx);
+  const int64_t row = c / g.dx;
+  const int segs = (g.dx + kBlkSeg - 1) / kBlkSeg;
+  uint32_t m = live[row * segs + x / kBlkSeg];
+  uint32_t s = 0;
+  const int y = (int)(row % g.dy), z = (int)(row / g.dy);
+  for (; m; m &= m - 1) {
+    const int q = __ffs(m) - 1;
+    const int64_t sc = ((int64_t)(z + q / 3 - 1) * g.dy + (y + q % 3 - 1)) * g.dx + x;
+    s += start[sc + 1] - start[sc];
+  }
   cnt9[c] = s;
 }
 
 __global__ void k_blk_fill(const float4* __restrict__ pts, const uint32_t* __restrict__ start,
-                           const uint32_t* __restrict__ bstart, GridGeom g, int64_t ncells,
-                           float4* __restrict__ blk) {
+                           const uint16_t* __restrict__ live, const uint32_t* __restrict__ bstart,
+                           GridGeom g, int64_t ncells, float4* __restrict__ blk) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncells) return;
   const int x = (int)(c % g.dx);
-  const int y = (int)((c / g.dx) % g.dy);
-  const int z = (int)(c / ((int64_t)g.dx * g.dy));
+  const int64_t row = c / g.dx;
+  const int segs = (g.dx + kBlkSeg - 1) / kBlkSeg;
+  uint32_t m = live[row * segs + x / kBlkSeg];
+  if (!m) return;
+  const int y = (int)(row % g.dy), z = (int)(row / g.dy);
   uint32_t o = bstart[c];
-  for (int k = -1; k <= 1; ++k)
-    for (int j = -1; j <= 1; ++j) {
-      const int yy = y + j, zz = z + k;
-      if (yy < 0 || yy >= g.dy || zz < 0 || zz >= g.dz) continue;
-      const int64_t sc = ((int64_t)zz * g.dy + yy) * g.dx + x;
-      for (uint32_t p = start[sc]; p < start[sc + 1]; ++p) {
-        const float4 v = pts[p];
-        blk[o++] = make_float4(v.x, v.y, v.z, __uint_as_float(p));
-      }
+  for (; m; m &= m - 1) {
+    const int q = __ffs(m) - 1;
+    const int64_t sc = ((int64_t)(z + q / 3 - 1) * g.dy + (y + q % 3 - 1)) * g.dx + x;
+    for (uint32_t p = start[sc]; p < start[sc + 1]; ++p) {
+      const float4 v = pts[p];
+      blk[o++] = make_float4(v.x, v.y, v.z, __uint_as_float(p));
     }
+  }
 }
 
 // coarse level: cell keys of the fine-sorted points, then the gather (values
@@ -2699,6 +2753,7 @@ struct SolveArgs {
 
 static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa);
 static int map_refresh(Ctx& c, bool adds_only = false);
+static int build_blk(MapDev& m, hipStream_t st, const char* who);
 
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
                         int extrinsic_est, const SolveArgs* sa = nullptr,
@@ -2754,6 +2809,8 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.cnt = c.count;
   cfg.nchunks = num_chunks(c.n);
   if (int rc = map_refresh(c); rc) return rc;
+  if (which != 0 && c.map->blk_deferred && ++c.map->stable_passes > kBlkAfterPasses)
+    if (int rc = build_blk(*c.map, c.stream, "slio map"); rc) return rc;
   PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane, c.sel, c.resid,
             c.chunk_part, c.count + 4};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
@@ -3017,13 +3074,6 @@ __global__ void k_cell_keys64(const float4* __restrict__ in, int64_t n, GridGeom
   vals[i] = (uint32_t)i;
 }
 
-__global__ void k_cell_hist64(const uint64_t* __restrict__ keys, int64_t n, int idbits,
-                              uint32_t* __restrict__ counts) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  atomicAdd(&counts[keys[i] >> idbits], 1u);
-}
-
 __global__ void k_gather4(const float4* __restrict__ in, const uint32_t* __restrict__ order, int64_t n,
                           float4* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3093,8 +3143,72 @@ static int grid_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) /
 // bits(id), any order, all ids distinct) with bounding box mn / mx: the cell
 // table, the cell-sorted points, the coarse level and (speed only) the
 // block rows; keep flags all set.  m's index arrays must be empty.
+// block rows wanted: not disabled, positions fit 32 bits
+static bool block_rows_wanted(const MapDev& m) {
+  const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
+  return !(nb9 && nb9[0] && nb9[0] != '0') && m.n > 0 && 9 * m.n < (int64_t)0xFFFFFFF0ll;
+}
+
+// Block rows of m's current index (speed only: on any failure the map just
+// goes without them).  The views are published after the stream has
+// finished them, so a handle sharing the map sees either no block rows or
+// complete ones.
+static int build_blk(MapDev& m, hipStream_t st, const char* who) {
+  m.blk_deferred = false;
+  const GridGeom g = m.g;
+  const int64_t nseg = (int64_t)((g.dx + kBlkSeg - 1) / kBlkSeg) * g.dy * g.dz;
+  size_t t3 = 0;
+  hipError_t e;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, t3, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                            (int)(m.ncells + 1), st)) ||
+      (e = m.take(m.b_tmp[6], 4 * (m.ncells + 1))) || (e = m.take(m.b_tmp[7], t3)) ||
+      (e = m.take(m.b_bstart, sizeof(uint32_t) * (m.ncells + 1)))) {
+    (void)hipGetLastError();
+    return SLIO_OK;
+  }
+  uint32_t* cnt = (uint32_t*)m.b_tmp[6].p;
+  uint32_t* bstart = (uint32_t*)m.b_bstart.p;
+  if ((e = m.take(m.b_tmp[5], 2 * nseg))) {
+    (void)hipGetLastError();
+    return SLIO_OK;
+  }
+  uint16_t* live = (uint16_t*)m.b_tmp[5].p;
+  if ((e = hipMemsetAsync(cnt + m.ncells, 0, 4, st))) {
+    set_error(std::string(who) + ": block rows: " + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  k_blk_live<<<grid_blocks(nseg), 256, 0, st>>>(m.start, g, nseg, live);
+  k_blk_count<<<grid_blocks(m.ncells), 256, 0, st>>>(m.start, live, g, m.ncells, cnt);
+  size_t tb = m.b_tmp[7].cap;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(m.b_tmp[7].p, tb, cnt, bstart, (int)(m.ncells + 1), st))) {
+    set_error(std::string(who) + ": block-row scan: " + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  uint32_t total = 0;  // <= 9 n < 2^32 (block_rows_wanted): the scan cannot wrap
+  if ((e = hipMemcpyAsync(&total, bstart + m.ncells, sizeof(uint32_t), hipMemcpyDeviceToHost, st)) ||
+      (e = hipStreamSynchronize(st))) {
+    set_error(std::string(who) + ": block-row total: " + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  if (m.take(m.b_blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
+    (void)hipGetLastError();
+    return SLIO_OK;
+  }
+  k_blk_fill<<<grid_blocks(m.ncells), 256, 0, st>>>(m.pts, m.start, live, bstart, g, m.ncells,
+                                                     (float4*)m.b_blk.p);
+  if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+    set_error(std::string(who) + ": block-row kernels: " + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  m.bstart = bstart;
+  m.nblk = (int64_t)total;
+  m.blk = (float4*)m.b_blk.p;
+  return SLIO_OK;
+}
+
 static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3], const float mx[3],
-                       hipStream_t st, const char* who) {
+                       hipStream_t st, const char* who, bool with_blk = true) {
+  m.blk_deferred = false;
   GridGeom g;
   float hcell = m.cell0;
   // kGridPad empty cells around the map's bounding box: scan points just
@@ -3202,7 +3316,7 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       rc = fail("sort", e);
       break;
     }
-    k_cell_hist64<<<nb, 256, 0, st>>>(k1, n, idbits, cnt);
+    k_cell_hist_sorted<uint64_t><<<nb, 256, 0, st>>>(k1, n, idbits, cnt);
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.start, (int)(m.ncells + 1), st))) {
       rc = fail("scan", e);
       break;
@@ -3217,7 +3331,7 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       rc = fail("coarse sort", e);
       break;
     }
-    k_cell_hist<<<nb, 256, 0, st>>>(c1, n, cnt);
+    k_cell_hist_sorted<uint32_t><<<nb, 256, 0, st>>>(c1, n, 0, cnt);
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.cstart, (int)(m.nccells + 1), st))) {
       rc = fail("coarse scan", e);
       break;
@@ -3228,40 +3342,11 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       rc = fail("build kernels", e);
       break;
     }
-    // block rows (speed only): skipped when disabled, when their positions
-    // would overflow 32 bits or when the device memory is not there
-    const char* nb9 = std::getenv("SLIO_NO_BLOCK_ROWS");
-    if ((nb9 && nb9[0] && nb9[0] != '0') || 9 * n >= (int64_t)0xFFFFFFF0ll) break;
-    const int ncb = grid_blocks(m.ncells);
-    if (m.take(m.b_bstart, sizeof(uint32_t) * (m.ncells + 1))) {
-      (void)hipGetLastError();
-      break;
-    }
-    m.bstart = (uint32_t*)m.b_bstart.p;
-    k_blk_count<<<ncb, 256, 0, st>>>(m.start, g, m.ncells, cnt);
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.bstart, (int)(m.ncells + 1), st))) {
-      rc = fail("block-row scan", e);
-      break;
-    }
-    uint32_t total = 0;  // <= 9 n < 2^32 (checked above): the scan cannot wrap
-    if ((e = hipMemcpyAsync(&total, m.bstart + m.ncells, sizeof(uint32_t), hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st))) {
-      rc = fail("block-row total", e);
-      break;
-    }
-    if (m.take(m.b_blk, sizeof(float4) * std::max<uint32_t>(total, 1u))) {
-      (void)hipGetLastError();
-      m.blk = nullptr;
-      m.bstart = nullptr;
-      break;
-    }
-    m.blk = (float4*)m.b_blk.p;
-    m.nblk = (int64_t)total;
-    k_blk_fill<<<ncb, 256, 0, st>>>(m.pts, m.start, m.bstart, g, m.ncells, m.blk);
-    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
-      rc = fail("block-row kernels", e);
-      break;
-    }
+    // block rows (speed only): now for an uploaded map; a map rebuilt by
+    // the live-map maintenance gets them once it has stopped changing
+    m.blk_deferred = block_rows_wanted(m);
+    m.stable_passes = 0;
+    if (with_blk && m.blk_deferred) rc = build_blk(m, st, who);
   } while (0);
 #ifdef SLIO_BOUNDS_CHECK
   if (!rc) {
@@ -3806,7 +3891,7 @@ static int map_refresh(Ctx& c, bool adds_only) {
   // in4 is b_ref[0]: build_index reads it while writing the b_* tables
   m.free_index();
   m.nadd = 0;
-  const int rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild");
+  const int rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild", false);
   m.version++;
   m.dirty = false;
   return rc;

@@ -54,6 +54,37 @@ def assert_same_map(L, h, om):
     np.testing.assert_array_equal(gp, op)
 
 
+def test_deferred_block_rows_after_rebuild(L, oracle_mod):
+    """A map rebuilt by the maintenance path is searched without block rows
+    until it has stayed unchanged for 8 search passes; the 9th builds them
+    (k_blk_count / k_blk_fill by x segments).  Every pass, before and after,
+    returns the oracle's exact kNN."""
+    from test_gpu_parity import IDENT, iterate, results, upload_scan
+    rng = np.random.default_rng(11)
+    base = rng.uniform(-20, 20, (30000, 3)).astype(np.float32)
+    base[:, 2] *= 0.2
+    h = mk(L, n_max=2000, cell=1.25)
+    om = oracle_mod.Map(base)
+    try:
+        upload_map(L, h, base)
+        boxes = np.array([[-5, -5, -5, 2, 3, 5]], np.float32)
+        assert delete(L, h, boxes) == om.delete_boxes(boxes)
+        new = rng.uniform(-21, 21, (4000, 3)).astype(np.float32)
+        assert add(L, h, new, True) == om.add_points(new, True, 0.5)
+        q = rng.uniform(-18, 18, (2000, 3)).astype(np.float32)
+        q[:, 2] *= 0.3
+        upload_scan(L, h, q)
+        op, oi = om.dump()
+        ridx, rsqd = oracle_mod.Tree(op).knn(q, 5)
+        for rep in range(12):
+            iterate(L, h, IDENT, True)
+            idx, sqd, *_ = results(L, h, q.shape[0])
+            np.testing.assert_array_equal(idx, oi[ridx].astype(np.int32))
+            np.testing.assert_array_equal(sqd, rsqd)
+    finally:
+        L.load().slio_destroy(h)
+
+
 @pytest.mark.parametrize("cell", [1.25, 0.37])
 def test_add_delete_vs_oracle(L, oracle_mod, cell):
     """Add_Points with downsampling (voxel groups of 1..5 new points against
