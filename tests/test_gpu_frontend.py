@@ -150,3 +150,29 @@ def test_edge_cases(oracle_mod):
             fe.cloud_info()
     finally:
         fe.close()
+
+
+def test_sector_variants_stress(oracle_mod):
+    """The feature stage runs each sector's greedy picks once per possible
+    prefix of suppression marks from the previous sector and chains the
+    variants per ring (slio_lio.hip k_fe_pick / k_fe_ring).  Sparse rings
+    (empty and 1-3 point sectors, marks that reach over an empty sector),
+    planar stretches (dense flat picks right at sector ends) and low
+    thresholds: bit-exact against the sequential oracle in every case."""
+    for seed in range(24):
+        rng = np.random.default_rng(100 + seed)
+        horizon = int(rng.choice([96, 160, 240]))
+        sc = small_scan(seed, n_scan=8, horizon=horizon, dup=0.05)
+        n = sc["x"].size
+        keep = rng.uniform(size=n) < rng.choice([0.04, 0.08, 0.15, 0.3, 0.6, 1.0])
+        sc = {k: (v[keep] if isinstance(v, np.ndarray) and v.shape[:1] == (n,) else v) for k, v in sc.items()}
+        kw = dict(edge_threshold=float(rng.choice([0.05, 0.3, 1.0])),
+                  surf_threshold=float(rng.choice([0.05, 0.1, 0.5, 5.0])))
+        ref = oracle_mod.lio_project(sc, 8, horizon, None)
+        fe = gpu_run(sc, 8, horizon, None, edgeThreshold=kw["edge_threshold"],
+                     surfThreshold=kw["surf_threshold"])
+        try:
+            ci = check_projection(fe, ref, False)
+            check_features(fe, ci, 8, oracle_mod, **kw)
+        finally:
+            fe.close()

@@ -153,3 +153,28 @@ def test_edge_cases(oracle_mod):
             fe.seg_info()
     finally:
         fe.close()
+
+
+def test_sector_variants_stress(oracle_mod):
+    """LeGO-LOAM's feature rules through the per-sector variant chain
+    (k_fe_pick / k_fe_ring): thinned sweeps (empty and tiny sectors), low
+    thresholds (many picks, marks at every sector end), the 4-flat cap whose
+    4th pick does not suppress.  Bit-exact against the sequential oracle."""
+    from agi_lidar_slam_amd.lego import LegoParams
+    for seed in range(16):
+        rng = np.random.default_rng(200 + seed)
+        horizon = int(rng.choice([240, 360, 512]))
+        P = LegoParams(N_SCAN=16, Horizon_SCAN=horizon, ang_res_x=360.0 / horizon, ang_res_y=2.0,
+                       groundScanInd=7, edgeThreshold=float(rng.choice([0.05, 0.1, 0.3])),
+                       surfThreshold=float(rng.choice([0.05, 0.1, 1.0])), segmentValidPointNum=3,
+                       segmentValidLineNum=2)
+        sc = small_sweep(seed, n_scan=16, horizon=horizon, res_y=2.0, dup=0.05, shuffle=bool(seed % 2))
+        n = sc["x"].size
+        keep = rng.uniform(size=n) < rng.choice([0.2, 0.4, 0.7, 1.0])
+        sc = {k: (v[keep] if isinstance(v, np.ndarray) and v.shape[:1] == (n,) else v) for k, v in sc.items()}
+        fe, ref = run_both(oracle_mod, sc, P)
+        try:
+            si = check_image(fe, ref)
+            check_features(oracle_mod, fe, si, P)
+        finally:
+            fe.close()
