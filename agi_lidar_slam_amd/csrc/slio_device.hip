@@ -1037,17 +1037,6 @@ struct PassCfg {
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
   int knn_only;            // 1: neighbours only (nbr_*), no fit / rows / products
-  // fused filter step (single-rank device-resident update, later passes):
-  // the last workgroup of each super-chunk sums its row, the last of those
-  // runs the filter step -- no separate super-sum launch
-  int fuse;
-  int iter, maxit;
-  double R;
-  const IkfCtl* src;
-  IkfCtl* hblk;
-  double* super_out;
-  uint32_t* cnt;  // [1] rows done, [8 + s] chunks of super-chunk s done
-  int64_t nchunks;
 };
 
 // ---------------------------------------------------------------- far queries
@@ -1732,79 +1721,6 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
   }
 }
 
-// LDS of the fused tail (aliases the pass's LDS)
-struct TailLds {
-  double seg[kSuperSeg * SLIO_NPROD];
-  SolveLds L;
-  int flag;
-};
-
-// Fused filter step, after this workgroup's chunk partial is published
-// (write-through, drained): the last workgroup of super-chunk s sums row s in
-// k_super_sums' fixed order (segment g: chunks c0 + g, c0 + g + 8, ...; then
-// the 8 segments), publishes it and arrives on the row counter; the last of
-// the 8 runs the filter step with the other 7 rows (sc1 loads).  Counters are
-// reset by the workgroup that completes them.
-template <int NT>
-__device__ __forceinline__ void fused_tail(const PassCfg& cfg, const double* chunk_part, int64_t chunk,
-                                           TailLds& T) {
-  const int t = threadIdx.x;
-  drain_stores();
-  __syncthreads();
-  const int64_t C = cfg.nchunks;
-  if (t == 0) {
-    int s = 0;
-#pragma unroll
-    for (int k = 1; k < SLIO_NSUPER; ++k)
-      if (super_lo(C, k) <= chunk) s = k;
-    const uint32_t members = (uint32_t)(super_lo(C, s + 1) - super_lo(C, s));
-    T.flag = arrive(cfg.cnt + 8 + s) == members - 1 ? s : -1;
-  }
-  __syncthreads();
-  const int s = T.flag;
-  if (s < 0) return;
-  if (t == 0) reset_counter(cfg.cnt + 8 + s);
-  {
-    constexpr int KP = (kSuperSeg * SLIO_NPROD + NT - 1) / NT;
-    const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
-    double acc[KP];
-    int64_t lim[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int p = t + k * NT;
-      const int g = p / SLIO_NPROD;
-      lim[k] = p < kSuperSeg * SLIO_NPROD ? (c1 - c0 - g + kSuperSeg - 1) / kSuperSeg : 0;
-      acc[k] = 0.0;
-    }
-    const double* cp = chunk_part + c0 * SLIO_NPROD + t;
-#pragma unroll 4
-    for (int64_t j = 0; j < lim[0]; ++j) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k)
-        if (j < lim[k]) acc[k] = acc[k] + ld_sc1(cp + j * (kSuperSeg * SLIO_NPROD) + k * NT);
-    }
-#pragma unroll
-    for (int k = 0; k < KP; ++k)
-      if (t + k * NT < kSuperSeg * SLIO_NPROD) T.seg[t + k * NT] = acc[k];
-  }
-  __syncthreads();
-  if (t < SLIO_NPROD) {
-    double v = T.seg[t];
-#pragma unroll
-    for (int q = 1; q < kSuperSeg; ++q) v = v + T.seg[q * SLIO_NPROD + t];
-    T.L.sup[s][t] = v;
-    st_sc1(cfg.super_out + s * SLIO_NPROD + t, v);
-  }
-  drain_stores();
-  __syncthreads();
-  if (t == 0) T.flag = arrive(cfg.cnt + 1) == (uint32_t)(SLIO_NSUPER - 1);
-  __syncthreads();
-  if (!T.flag) return;
-  if (t == 0) reset_counter(cfg.cnt + 1);
-  if (cfg.src == cfg.ctl && cfg.ctl->done) return;
-  ikf_solve_block<NT>(cfg.ctl, cfg.src, cfg.hblk, cfg.R, cfg.iter, cfg.maxit, T.L, cfg.super_out,
-                      ((1u << SLIO_NSUPER) - 1u) & ~(1u << s));
-}
 
 // Refinement scan of ALL the runs of `mask` (<= 34: 25 rows + 9 right
 // segments) by the RL lanes of a group as ONE flattened candidate list: lane
@@ -1974,8 +1890,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
   static_assert(SLIO_CHUNK % QPP == 0, "chunk must be a multiple of queries/pass");
   static_assert(NT >= SLIO_CHUNK, "fit phase needs one lane per point");
-  // the pass's LDS; the fused filter step's tail reuses it once the
-  // products are written
   // refinement records of the chunk (alias the Jacobian rows, which the fit
   // phase writes only after the refinement)
   struct RefLds {
@@ -2001,9 +1915,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     uint8_t far_slot[SLIO_CHUNK];
     uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
   };
-  __shared__ union {
+  __shared__ struct {
     SearchLds s;
-    TailLds t;
   } lds;
   auto& rows = lds.s.rr.rows;
   auto& ref = lds.s.rr.ref;
@@ -2373,9 +2286,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (tid == 0) STAMP(2);
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
-  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, DEVPOSE && cfg.fuse);
-  if constexpr (DEVPOSE && NT == 256)
-    if (cfg.fuse) fused_tail<NT>(cfg, out.chunk_part, chunk, lds.t);
+  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
   if (tid == 0) STAMP(3);
 }
 
@@ -2791,23 +2702,6 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   cfg.knn_only = knn_only ? 1 : 0;
-  // fused filter step: later search passes of a single-rank device-resident
-  // update in fixed mode (a search pass every iteration); 256-thread blocks
-  // (measured slower than the separate launch: 17.2k vs 19.2k IKF it/s at C2
-  // -- the per-super row sums and the solve on single workgroups at the end of
-  // the pass add more than the launch they save; opt-in for experiments)
-  cfg.fuse = (sa && sa->on && devpose && which == 1 && c.prm.lanes_per_query != 1 && !knn_only &&
-              std::getenv("SLIO_FUSE") != nullptr)
-                 ? 1
-                 : 0;
-  cfg.iter = sa ? sa->iter : 0;
-  cfg.maxit = sa ? sa->maxit : 0;
-  cfg.R = sa ? sa->R : 0.0;
-  cfg.src = sa ? sa->src : nullptr;
-  cfg.hblk = sa ? sa->hblk : nullptr;
-  cfg.super_out = c.d_super;
-  cfg.cnt = c.count;
-  cfg.nchunks = num_chunks(c.n);
   if (int rc = map_refresh(c); rc) return rc;
   if (which != 0 && c.map->blk_deferred && ++c.map->stable_passes > kBlkAfterPasses)
     if (int rc = build_blk(*c.map, c.stream, "slio map"); rc) return rc;
@@ -2871,7 +2765,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
       hipExtLaunchKernelGGL(k_reuse_pass<false>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
                             rcfg, o);
   }
-  if (with_super && !cfg.fuse) enqueue_super(c, ctl, sa);
+  if (with_super) enqueue_super(c, ctl, sa);
   SLIO_HIP(hipGetLastError());
   if (which != 0) {
     c.searched = true;

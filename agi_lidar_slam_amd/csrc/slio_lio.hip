@@ -1,7 +1,7 @@
 // slio_lio.hip -- LIO-SAM front-end on gfx950.
 //
-// One scan = 8 launches on the handle's stream:
-//   memset(cell owners)            reset of rangeMat (imageProjection.cpp:146)
+// One scan = 7 launches on the handle's stream:
+//   (no reset of the cell owners: they carry the scan's generation)
 //   k_lio_claim   per point        projectPointCloud filters (:614-636); the
 //                                  cell goes to the smallest point index
 //                                  (atomicMin) = "first point wins" (:638)
@@ -330,7 +330,12 @@ __device__ __forceinline__ int pow2ceil(int v) {
 }
 
 // ---------------------------------------------------------------- kernels
-__global__ __launch_bounds__(256) void k_lio_claim(In in, Geo g, uint32_t* owner,
+// Cell owners carry the scan's generation in their high word (hi = ~gen, so
+// a newer scan's keys are smaller): atomicMin keeps the smallest point index
+// of this scan and a cell holding an older scan's key reads as empty -- no
+// reset of the owner table before every scan (rangeMat reset,
+// imageProjection.cpp:146).
+__global__ __launch_bounds__(256) void k_lio_claim(In in, Geo g, unsigned long long* owner, uint32_t hi,
                                                    uint32_t* block_first) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   bool ok = i < in.n;
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(256) void k_lio_claim(In in, Geo g, uint32_t* owner
     }
   }
 #ifndef SLIO_ABL_NOATOMIC
-  if (ok) atomicMin(&owner[c], (uint32_t)i);
+  if (ok) atomicMin(&owner[c], ((unsigned long long)hi << 32) | (unsigned long long)i);
 #else
   if (ok && c < 0) owner[0] = 0;  // diagnostic: no cell atomics
 #endif
@@ -401,7 +406,8 @@ __device__ Aff get_rot_sc(float roll, float pitch, float yaw) {
 }
 
 // grid (n_scan, kFillSplit): block (r, s) fills columns [s H / S, (s + 1) H / S) of ring r
-__global__ __launch_bounds__(kFillThreads) void k_lio_fill(In in, Geo g, const uint32_t* owner,
+__global__ __launch_bounds__(kFillThreads) void k_lio_fill(In in, Geo g, const unsigned long long* owner,
+                                                           uint32_t hi,
                                                            const uint32_t* block_first, int nfirst,
                                                            Deskew d, float* range_mat,
                                                            float4* full, int32_t* row_part) {
@@ -447,7 +453,8 @@ __global__ __launch_bounds__(kFillThreads) void k_lio_fill(In in, Geo g, const u
   int cnt = 0;
   for (int col = c0 + t; col < c1; col += kFillThreads) {
     const int64_t c = col + (int64_t)r * g.horizon;
-    const uint32_t o = owner[c];
+    const unsigned long long ok = owner[c];
+    const uint32_t o = (uint32_t)(ok >> 32) == hi ? (uint32_t)ok : kNone;
     if (o == kNone) {
       range_mat[c] = FLT_MAX;
       continue;
@@ -1226,7 +1233,8 @@ struct slio_lio {
   double t0 = 0.0;
   int deskew = 0;
   // projection
-  uint32_t* owner = nullptr;  // cells + 1
+  unsigned long long* owner = nullptr;  // cells + 1: (~generation << 32) | point index
+  uint32_t gen = 0;                      // scans run (owner generation)
   float* range_mat = nullptr;
   float4* full = nullptr;
   int32_t* row_count = nullptr;     // n_scan * kFillSplit partial counts
@@ -1366,7 +1374,7 @@ int slio_lio_create(slio_lio_handle* out, const slio_lio_params* p) {
   A(h->rx, 8 * kMaxImu);
   A(h->ry, 8 * kMaxImu);
   A(h->rz, 8 * kMaxImu);
-  A(h->owner, 4 * (C + 1));
+  A(h->owner, 8 * (C + 1));
   A(h->range_mat, 4 * C);
   A(h->full, 16 * C);
   A(h->row_count, 4 * p->n_scan * kFillSplit);
@@ -1489,14 +1497,18 @@ int slio_lio_run_async(slio_lio_handle h) {
   LIO_CHECK_H(h);
   const Geo& g = h->g;
   const int R = g.n_scan;
-  LIO_HIP(hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream));
+  if (h->gen == 0 || h->gen == 0xFFFFFFFEu) {  // first scan, or the generation wraps
+    LIO_HIP(hipMemsetAsync(h->owner, 0xff, 8 * g.cells, h->stream));
+    h->gen = 0;
+  }
+  const uint32_t hi = ~(++h->gen);
   const In in{h->x, h->y, h->z, h->in, h->ring, h->time, h->n};
   const int nclaim = (int)((h->n + 255) / 256);
   if (h->n > 0)
-    k_lio_claim<<<nclaim, 256, 0, h->stream>>>(in, g, h->owner, h->block_first);
+    k_lio_claim<<<nclaim, 256, 0, h->stream>>>(in, g, h->owner, hi, h->block_first);
   const Deskew d{h->it, h->rx, h->ry, h->rz, h->n_imu - 1, h->t0, h->deskew};
   k_lio_fill<<<dim3(R, kFillSplit), kFillThreads, 0, h->stream>>>(
-      in, g, h->owner, h->block_first, nclaim, d, h->range_mat, h->full, h->row_count);
+      in, g, h->owner, hi, h->block_first, nclaim, d, h->range_mat, h->full, h->row_count);
   const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->prange, h->xyzi, h->n_ext};
   k_lio_extract<<<R, kRowThreads, 0, h->stream>>>(g, h->range_mat, h->full, h->row_count, ci);
   k_lio_smooth<<<(unsigned)((g.cells + 255) / 256), 256, 0, h->stream>>>(
@@ -1576,9 +1588,13 @@ int slio_lio_get_range_image(slio_lio_handle h, float* range_mat, int32_t* cell_
   }
   if (range_mat)
     LIO_HIP(hipMemcpyAsync(range_mat, h->range_mat, 4 * h->cells, hipMemcpyDeviceToHost, h->stream));
-  if (cell_point)  // kNone (0xffffffff) reads back as -1
-    LIO_HIP(hipMemcpyAsync(cell_point, h->owner, 4 * h->cells, hipMemcpyDeviceToHost, h->stream));
+  std::vector<unsigned long long> own(cell_point ? (size_t)h->cells : 0);
+  if (cell_point)
+    LIO_HIP(hipMemcpyAsync(own.data(), h->owner, 8 * h->cells, hipMemcpyDeviceToHost, h->stream));
   LIO_HIP(hipStreamSynchronize(h->stream));
+  const uint32_t hi = ~h->gen;
+  for (size_t c = 0; c < own.size(); ++c)  // a cell of an older scan is empty: -1
+    cell_point[c] = (uint32_t)(own[c] >> 32) == hi ? (int32_t)(uint32_t)own[c] : -1;
   return SLIO_OK;
 }
 
