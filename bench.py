@@ -37,6 +37,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def usable_cores() -> tuple[int, str]:
+    """Cores this process can actually run on: its affinity set, capped by a
+    cgroup CPU quota (the GPU box gives a 1-GPU job a share of a large host:
+    nproc and the affinity set show every core, the quota does not)."""
+    n = len(os.sched_getaffinity(0))
+    why = "affinity set"
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                q = max(1, int(int(quota) // int(period)))
+                if q < n:
+                    n, why = q, f"cgroup quota {quota}/{period}"
+        except (OSError, ValueError):
+            pass
+    try:  # cgroup v1
+        quota = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if quota > 0 and quota // period < n:
+            n, why = max(1, quota // period), f"cgroup quota {quota}/{period}"
+    except (OSError, ValueError):
+        pass
+    return n, why
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -343,7 +368,7 @@ def main():
         cel = time.perf_counter() - t0
         # the same sample on every core this process may use (the reference's
         # MP_PROC_NUM is 3; SURVEY.md 8(d) asks for both)
-        all_cores = len(os.sched_getaffinity(0))
+        all_cores, cores_why = usable_cores()
         t0 = time.perf_counter()
         for _ in range(args.cpu_scans):
             O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=1,
@@ -359,7 +384,7 @@ def main():
                        f"iteration, 24 x m gain formed as esekfom.hpp:314), "
                        f"{args.scan_points}-pt scan vs {args.map_points}-pt map, "
                        f"{args.cpu_threads} OpenMP threads (MP_PROC_NUM), and all_cores = every "
-                       f"core in this process's affinity set; host {cpu_model()}, "
+                       f"core this process may use ({cores_why}); host {cpu_model()}, "
                        f"nproc {os.cpu_count()}"),
         }
 
