@@ -1028,6 +1028,7 @@ struct PassOut {
   float* resid;      // n
   double* chunk_part;  // C * NPROD (global chunk index)
   uint32_t* far_ctr;   // [1]: deferred (far) queries of this pass, all chunks
+  PoseDev* pose;       // the pass's pose (block 0), for nbr_settle
 };
 
 // far_query_margin: squared distance from the query to the grid's bounding box
@@ -1917,8 +1918,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       RefLds ref;
     } rr;
     double part[NT / 128][SLIO_NPROD];
-    uint32_t nb_pos[SLIO_CHUNK][5];
-    float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
+    alignas(16) uint32_t nb_pos[SLIO_CHUNK][5];
+    alignas(16) float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
+    alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
@@ -1937,6 +1939,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& part = lds.s.part;
   auto& nb_pos = lds.s.nb_pos;
   auto& nb_sqd = lds.s.nb_sqd;
+  auto& nb_idx = lds.s.nb_idx;
   auto& nb_d5 = lds.s.nb_d5;
   auto& qw = lds.s.qw;
   auto& far_cnt = lds.s.far_cnt;
@@ -1958,6 +1961,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (tid == 0) {
     far_cnt = 0;
     ref_cnt = 0;
+    if (blockIdx.x == 0 && !cfg.knn_only) *out.pose = pose;
   }
   __syncthreads();
 
@@ -2267,9 +2271,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb[j][0] = c.x;
         nb[j][1] = c.y;
         nb[j][2] = c.z;
-        out.nbr_idx[i * 5 + j] = (int32_t)__float_as_uint(c.w);
-        out.nbr_pos[i * 5 + j] = ps;
-        out.nbr_sqd[i * 5 + j] = nb_sqd[slot][j];
+        nb_idx[slot][j] = (int32_t)__float_as_uint(c.w);
       }
       if (cfg.knn_only) sel = false;
       if (sel) {
@@ -2298,10 +2300,71 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
   __syncthreads();
   if (tid == 0) STAMP(2);
+  // the chunk's cell-sorted neighbour positions ([slot][5] in LDS, [i][5]
+  // in HBM: one contiguous run of 5 * live words, 16-B stores).  Nearest_Points
+  // ids and pointSearchSqDis are derived from them only when read
+  // (nbr_settle: pts[pos].w, and calc_dist from the pass's pose), except in
+  // kNN-only passes, whose callers read the distances on the device.
+  {
+    const int64_t base = chunk * SLIO_CHUNK;
+    const int nw = (int)(5 * min((int64_t)SLIO_CHUNK, scan.n - base));
+    const int na = cfg.knn_only ? 3 : 1;
+    auto dst = [&](int a) {
+      return a == 0 ? out.nbr_pos + base * 5
+                    : (uint32_t*)(a == 1 ? (void*)out.nbr_idx : (void*)out.nbr_sqd) + base * 5;
+    };
+    auto src = [&](int a) {
+      return a == 0 ? &nb_pos[0][0]
+                    : (const uint32_t*)(a == 1 ? (const void*)&nb_idx[0][0] : (const void*)&nb_sqd[0][0]);
+    };
+    if ((nw & 3) == 0) {
+      const int nv = nw >> 2;
+      for (int k = tid; k < na * nv; k += NT) {
+        const int a = k >= nv ? (k >= 2 * nv ? 2 : 1) : 0;
+        const int v = k - a * nv;
+        reinterpret_cast<uint4*>(dst(a))[v] = reinterpret_cast<const uint4*>(src(a))[v];
+      }
+    } else {
+      for (int k = tid; k < na * nw; k += NT) {
+        const int a = k >= nw ? (k >= 2 * nw ? 2 : 1) : 0;
+        const int v = k - a * nw;
+        dst(a)[v] = src(a)[v];
+      }
+    }
+  }
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
   chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
   if (tid == 0) STAMP(3);
+}
+
+// Nearest_Points ids and pointSearchSqDis of the last search pass, derived
+// from its neighbour positions: the id is the map point's .w and the
+// distance is calc_dist (ikd_Tree.cpp:1539-1544) from the same float query
+// (the pass's pose, the same body point), so both equal what the pass found.
+__global__ __launch_bounds__(256) void k_nbr_derive(const ScanDev scan, const float4* __restrict__ pts,
+                                                    const uint32_t* __restrict__ pos,
+                                                    const PoseDev* __restrict__ pose, int64_t b,
+                                                    int64_t e, int32_t* __restrict__ idx,
+                                                    float* __restrict__ sqd) {
+  const int64_t i = b + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= e) return;
+  float qx, qy, qz;
+  body_to_world(*pose, scan.bx[i], scan.by[i], scan.bz[i], qx, qy, qz);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const uint32_t ps = pos[i * 5 + j];
+    int32_t id = -1;
+    float d = __int_as_float(0x7f800000);
+    if (ps != 0xFFFFFFFFu) {
+      const float4 c = pts[ps];
+      const float ddx = qx - c.x, ddy = qy - c.y, ddz = qz - c.z;
+      d = (ddx * ddx + ddy * ddy) + ddz * ddz;
+      id = (int32_t)__float_as_uint(c.w);
+    }
+    idx[i * 5 + j] = id;
+    sqd[i * 5 + j] = d;
+  }
 }
 
 // Non-search pass: reuse neighbours/plane/selection (esekfom.hpp:138-150 with
@@ -2499,6 +2562,8 @@ struct Ctx {
   float* bz = nullptr;
   int32_t* nbr_idx = nullptr;
   uint32_t* nbr_pos = nullptr;
+  PoseDev* nbr_pose = nullptr;  // pose of the last search pass (device)
+  bool nbr_lazy = false;        // nbr_idx / nbr_sqd not yet derived from nbr_pos
   uint64_t search_version = 0;  // map version the last search pass ran on
   float* wbx = nullptr;  // scan-to-map: the scan in the map frame
   float* wby = nullptr;
@@ -2606,6 +2671,9 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->nbr_idx);
   (void)hipFree(c->nbr_pos);
   c->nbr_pos = nullptr;
+  (void)hipFree(c->nbr_pose);
+  c->nbr_pose = nullptr;
+  c->nbr_lazy = false;
   (void)hipFree(c->wbx);
   (void)hipFree(c->wby);
   (void)hipFree(c->wbz);
@@ -2719,8 +2787,8 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   if (int rc = map_refresh(c); rc) return rc;
   if (which != 0 && c.map->blk_deferred && ++c.map->stable_passes > kBlkAfterPasses)
     if (int rc = build_blk(*c.map, c.stream, "slio map"); rc) return rc;
-  PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane, c.sel, c.resid,
-            c.chunk_part, c.count + 4};
+  PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane,   c.sel,
+            c.resid,      c.chunk_part, c.count + 4, c.nbr_pose};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
@@ -2766,6 +2834,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     }
 #undef SLIO_LAUNCH2
 #undef SLIO_LAUNCH
+    c.nbr_lazy = !knn_only;
   }
   if (nblk > 0 && run_reuse) {
     const auto ev = timing(SLIO_KERNEL_REUSE);
@@ -2785,6 +2854,23 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     c.searched = true;
     c.search_version = c.map->version;
   }
+  return SLIO_OK;
+}
+
+// Derive the last search pass's Nearest_Points ids and pointSearchSqDis
+// (k_nbr_derive) while its scan, map and pose are still the handle's: called
+// before they change and before the results are read.
+static int nbr_settle(Ctx& c) {
+  if (!c.nbr_lazy) return SLIO_OK;
+  c.nbr_lazy = false;
+  int64_t c0, c1;
+  rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
+  const int64_t b = c0 * SLIO_CHUNK, e = std::min(c1 * SLIO_CHUNK, c.n);
+  if (e <= b || !c.map) return SLIO_OK;
+  k_nbr_derive<<<(unsigned)((e - b + 255) / 256), 256, 0, c.stream>>>(ScanDev{c.bx, c.by, c.bz, c.n}, c.map->pts,
+                                                         c.nbr_pos, c.nbr_pose, b, e, c.nbr_idx,
+                                                         c.nbr_sqd);
+  SLIO_HIP(hipGetLastError());
   return SLIO_OK;
 }
 
@@ -3294,7 +3380,7 @@ static int ensure_scan_buffers(Ctx& c) {
     hipError_t e;
     if ((e = hipMalloc(&c.bx, 4 * cap)) || (e = hipMalloc(&c.by, 4 * cap)) ||
         (e = hipMalloc(&c.bz, 4 * cap)) || (e = hipMalloc(&c.nbr_idx, 4 * 5 * cap)) ||
-        (e = hipMalloc(&c.nbr_pos, 4 * 5 * cap)) ||
+        (e = hipMalloc(&c.nbr_pos, 4 * 5 * cap)) || (e = hipMalloc(&c.nbr_pose, sizeof(PoseDev))) ||
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {
@@ -3774,6 +3860,7 @@ static int map_refresh(Ctx& c, bool adds_only) {
   if (!c.map || !c.map->dirty) return SLIO_OK;
   MapDev& m = *c.map;
   if (adds_only && m.nadd == 0) return SLIO_OK;
+  if (int rc = nbr_settle(c)) return rc;  // the rebuild moves the points
   hipStream_t st = c.stream;
   const int64_t n0 = m.n, n1 = m.nadd, nt = n0 + n1;
   hipError_t e;
@@ -3882,6 +3969,7 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
   for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)in4})
     if (q) (void)hipFree(q);
   if (rc) return rc;
+  if ((rc = nbr_settle(h->c))) return rc;
   h->c.map = m;
   h->c.searched = false;
   return SLIO_OK;
@@ -3893,6 +3981,7 @@ int slio_map_share(slio_handle h, slio_handle src) {
     set_error("slio_map_share: source has no map on this device");
     return SLIO_EINVAL;
   }
+  if (int rc = nbr_settle(h->c)) return rc;
   h->c.map = src->c.map;
   h->c.searched = false;
   return SLIO_OK;
@@ -4179,7 +4268,8 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
   uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *hd = nullptr, *rk = nullptr;
   int32_t* bb = nullptr;
   void* tmp = nullptr;
-  int rc = SLIO_OK;
+  int rc = nbr_settle(c);  // the scan it was searched with is replaced
+  if (rc) return rc;
   int64_t m = 0;
   bool passthrough = false;
   do {
@@ -4923,6 +5013,7 @@ int slio_scan_upload(slio_handle h, const float* x, const float* y, const float*
     set_error("slio_scan_upload: scan exceeds max_points");
     return SLIO_ECAPACITY;
   }
+  if (int rc = nbr_settle(c)) return rc;  // the scan it was searched with is replaced
   if (int rc = ensure_scan_buffers(c)) return rc;
   c.n = n;
   if (n > 0) {
@@ -5131,6 +5222,7 @@ int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel) {
   int64_t b, e;
   slio_shard_range(h, &b, &e);
   const int64_t n = e - b;
+  if (int rc = nbr_settle(c)) return rc;
   SLIO_HIP(hipStreamSynchronize(c.stream));
   if (n <= 0) return SLIO_OK;
   if (idx) SLIO_HIP(hipMemcpy(idx, c.nbr_idx + b * 5, 4 * 5 * n, hipMemcpyDeviceToHost));

@@ -33,8 +33,38 @@ BYTES_PER_SEARCH_PT = 109   # SURVEY.md §8d compulsory bytes, search pass
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
+L2_PEAK_GBS = 34500.0       # MI355X aggregate L2 read bandwidth (MI355X_MICROARCH.md, L2)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def l2_demand_bytes(mp: np.ndarray, body: np.ndarray, st0: np.ndarray, cell: float) -> float:
+    """Estimated bytes one search launch asks of the L1/L2 (not HBM): per
+    query the 2 block-row bounds (8 B), every candidate of its 3x3x3 block
+    row (16 B each), the scan point (12 B), the 5 neighbours reloaded by the
+    fit (80 B) and the per-point outputs (81 B).  The block is counted on a
+    grid of the same cell edge and bounding-box padding as the device map at
+    the step's initial pose; refinements and far queries are not counted, so
+    this is a lower bound of the kernel's L2-level demand."""
+    from agi_lidar_slam_amd import synth
+    lo = mp.min(0).astype(np.float64) - 2 * cell
+    dims = np.floor((mp.max(0) - lo) / cell).astype(np.int64) + 3
+    def cells(p):
+        return np.floor((p - lo) / cell).astype(np.int64)
+    c = cells(mp.astype(np.float64))
+    cnt = np.bincount((c[:, 2] * dims[1] + c[:, 1]) * dims[0] + c[:, 0],
+                      minlength=int(np.prod(dims))).reshape(dims[2], dims[1], dims[0])
+    R = synth.quat_matrix(st0[3:7])
+    q = (body.astype(np.float64) + st0[11:14]) @ R.T + st0[0:3]
+    qc = np.clip(cells(q), 1, dims - 2)
+    cand = np.zeros(q.shape[0], np.int64)
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                cand += cnt[qc[:, 2] + dz, qc[:, 1] + dy, qc[:, 0] + dx]
+    return float(cand.sum() * 16 + q.shape[0] * (8 + 12 + 80 + 81))
 
 
 def usable_cores() -> tuple[int, str]:
@@ -220,6 +250,9 @@ def main():
                     help="c2: IKF iterations/s, 100k Avia scan vs 10M map (BASELINE.json metric); "
                          "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan")
     ap.add_argument("--cpu-scans-c3", type=int, default=300)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the multi-rank path with several ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "search_traffic.json"))
     args = ap.parse_args()
 
@@ -230,10 +263,12 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # one rank per GPU; the modulo only matters for a gloo rehearsal with more
+    # ranks than devices (device_count() does not initialise the GPU here)
+    dev = local_rank % max(1, torch.cuda.device_count()) if world > 1 else 0
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl" if args.workload == "c2" else "gloo")
-    dev = local_rank if world > 1 else 0
+        torch.cuda.set_device(dev)
+        dist.init_process_group(args.dist_backend if args.workload == "c2" else "gloo")
     if args.workload == "c3":
         bench_c3(args, rank, world, dev, dist)
         if world > 1:
@@ -275,7 +310,11 @@ def main():
     reduce_cb = L.ALLREDUCE_FN()
     keep = []
     if world > 1:
-        stream = torch.cuda.current_stream()
+        # the library and the collective must share one stream: a stream of
+        # our own made current (torch's default stream is handle 0, which
+        # slio_set_stream reads as "the handle's own stream")
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
         lib.slio_set_stream(h, C.c_void_p(stream.cuda_stream))
         sup = torch.zeros(8 * 91, dtype=torch.float64, device=f"cuda:{dev}")
         lib.slio_set_super_buffer(h, C.c_void_p(sup.data_ptr()))
@@ -355,6 +394,15 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    l2 = None
+    if rank == 0 and avg_kernel_s > 0:
+        dem = l2_demand_bytes(mp, fr.body[b.value:e.value], st0, args.cell)
+        l2 = {"demand_bytes_per_launch": dem, "achieved": dem / avg_kernel_s / 1e9,
+              "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": dem / avg_kernel_s / 1e9 / L2_PEAK_GBS,
+              "note": "L2-level roofline of the same launches: block-row candidates + "
+                      "neighbour reloads + outputs per query (bench.l2_demand_bytes, a lower "
+                      "bound: refinements not counted) / avg launch time, vs the L2 bandwidth"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
@@ -428,6 +476,7 @@ def main():
             "launches": int(nl.value),
             "timing": f"HIP events in the dispatch packet, search launches of 1 in {every} timed steps",
         },
+        "roofline_l2": l2,
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -110,7 +110,9 @@ int slio_params_default(slio_params* p);
 int slio_create(slio_handle* out, const slio_params* p);
 int slio_destroy(slio_handle h);
 /* Use an external hipStream_t (e.g. torch's current stream) instead of the
- * handle's own stream; NULL restores the handle's stream. */
+ * handle's own stream; NULL restores the handle's stream.  torch's DEFAULT
+ * stream has the handle NULL: to share a stream with torch collectives, make a
+ * torch.cuda.Stream current and pass that one. */
 int slio_set_stream(slio_handle h, void* hip_stream);
 const char* slio_last_error(void);
 
@@ -229,7 +231,10 @@ int slio_iterate(slio_handle h, const slio_pose* x, int do_search,
 /* ---- per-point results (Nearest_Points / point_selected_surf / normvec) -- */
 /* For the shard's points (n = end - begin): neighbour map indices (-1 if
  * fewer than 5 map points exist), f32 squared distances ascending (the
- * pointSearchSqDis of esekfom.hpp:135-141), final selection flag. */
+ * pointSearchSqDis of esekfom.hpp:135-141), final selection flag.  They are
+ * the last SEARCH pass's results: the search pass stores only the neighbours'
+ * map positions, and ids and distances are derived from them on this call
+ * (or, automatically, before the handle's scan or map is replaced). */
 int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel);
 /* Number of scan points of the last pass (of this handle's shard) whose
  * 5-NN search did not finish on the fine grid -- 5th neighbour beyond the

@@ -9,4 +9,4 @@ for PMC in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_WAV
   i=$((i+1))
   REPS=10 timeout -s KILL 120 rocprofv3 --pmc $PMC --kernel-include-regex k_search_pass -d gpurun_out/${tag}_pmc$i -o pmc --output-format csv -- python3 scripts/run_search.py > gpurun_out/${tag}_pmc$i.log 2>&1 || { echo "pmc $i failed"; tail -3 gpurun_out/${tag}_pmc$i.log; exit 6; }
 done
-python3 scripts/pmc_traffic.py profiles/search_traffic.json gpurun_out/${tag}_pmc*
+python3 scripts/pmc_traffic.py gpurun_out/${tag}_search_traffic.json gpurun_out/${tag}_pmc*

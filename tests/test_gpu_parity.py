@@ -196,6 +196,37 @@ def test_repeated_search_bitexact(L, oracle_mod, c1, shift):
         L.load().slio_destroy(h)
 
 
+def test_neighbors_outlive_scan_and_map_changes(L, oracle_mod, c1):
+    """Nearest_Points ids and pointSearchSqDis are derived from the search
+    pass's neighbour positions when first read; they must still be the last
+    SEARCH pass's (not a later reuse pass's pose) after the handle's scan or
+    map has been replaced."""
+    mp, fr, T = c1["avia"]
+    st = state_of(fr)
+    n = fr.body.shape[0]
+    h = mk(L, cell=1.25)
+    try:
+        upload_map(L, h, mp)
+        upload_scan(L, h, fr.body)
+        iterate(L, h, st, True)
+        st2 = st.copy()
+        st2[0:3] += [0.4, -0.3, 0.1]
+        iterate(L, h, st2, False)          # reuse pass: neighbours unchanged
+        ridx, rsqd = T.knn(oracle_mod.body_to_world(st, fr.body), 5)
+        upload_scan(L, h, fr.body[::-1])    # new scan of the same size
+        idx, sqd, *_ = results(L, h, n)
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_array_equal(sqd, rsqd)
+        iterate(L, h, st2, True)            # search the new scan, then replace the map
+        ridx2, rsqd2 = T.knn(oracle_mod.body_to_world(st2, fr.body[::-1]), 5)
+        upload_map(L, h, mp[: mp.shape[0] // 2])
+        idx, sqd, *_ = results(L, h, n)
+        np.testing.assert_array_equal(idx, ridx2)
+        np.testing.assert_array_equal(sqd, rsqd2)
+    finally:
+        L.load().slio_destroy(h)
+
+
 # ------------------------------------------------------------------ passes
 @pytest.mark.parametrize("pat", ["vlp16", "avia"])
 @pytest.mark.parametrize("ext", [False, True])
