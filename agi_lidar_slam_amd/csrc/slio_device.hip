@@ -1890,6 +1890,11 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
 // LDS.  Phase 2 (fit): one lane per point reloads the 5 neighbours (L2-hot),
 // runs esti_plane, the residual gate and the Jacobian row, and writes the
 // row to LDS.  Phase 3: fixed-order fp64 products -> chunk partial.
+// refinement lanes per query by the chunk's number of refining queries: 8
+// lanes (one round of 32 queries) up to NT / SLIO_RL8_MAX of them, then 4, then 2
+#ifndef SLIO_RL8_MAX
+#define SLIO_RL8_MAX 8
+#endif
 template <int LPQ, int U, bool SPHERE, bool DEVPOSE>
 __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
     const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
@@ -2156,13 +2161,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           const uint64_t rows = sphere_rows(g, rq, rq.lim);
           runs = rows | ((rows & 0x739c0ull) << 32);
         }
-        if (RL >= 16) {
+        if constexpr (RL >= 16) {
           const int gi = (tid >> 6) * (64 / RL) + lane / RL;
           scan_runs_wide<RL, U>(pts, start, g, rq, runs, rsub, tab_pre[gi], tab_dl[gi], tr);
         } else if (has) {
           // many refining queries: each lane scans its own share of the runs
-          // (runs rsub, rsub + 8, ...), one batch of run bounds per lane
-          scan_runs<1, U>(pts, start, g, rq, runs & (0x0101010101010101ull << rsub), 0, tr);
+          // (runs rsub, rsub + RL, ...), one batch of run bounds per lane
+          constexpr uint64_t kShare = RL == 8 ? 0x0101010101010101ull
+                                              : (RL == 4 ? 0x1111111111111111ull : 0x5555555555555555ull);
+          scan_runs<1, U>(pts, start, g, rq, runs & (kShare << rsub), 0, tr);
         }
 #ifdef SLIO_REFINE_DPP_MERGE
         group_merge<RL>(tr);
@@ -2202,8 +2209,12 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         refine_all(std::integral_constant<int, 64>{});
       else if (nref <= NT / 16)
         refine_all(std::integral_constant<int, 16>{});
-      else
+      else if (nref <= NT / SLIO_RL8_MAX)
         refine_all(std::integral_constant<int, 8>{});
+      else if (nref <= NT / 4)
+        refine_all(std::integral_constant<int, 4>{});
+      else
+        refine_all(std::integral_constant<int, 2>{});
       __syncthreads();
     }
     WSTAMP(1, __builtin_amdgcn_s_memrealtime());
