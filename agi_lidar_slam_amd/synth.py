@@ -309,8 +309,13 @@ def make_problem(n_map: int, n_scan: int, seed: int = 20261015, pattern: str = "
     mp = sample_map(scene, seed, n_map)
     fr = make_frame(scene, seed, n_scan, pattern, sensor=sensor)
     if cache_dir:
-        np.savez(fn, map=mp, body=fr.body, gt_rot=fr.gt_rot, gt_pos=fr.gt_pos,
-                 init_rot=fr.init_rot, init_pos=fr.init_pos)
+        # several ranks may build the same problem at once: write a private
+        # file and rename it into place, so no rank ever loads a partial one
+        tmp = f"{fn}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            np.savez(f, map=mp, body=fr.body, gt_rot=fr.gt_rot, gt_pos=fr.gt_pos,
+                     init_rot=fr.init_rot, init_pos=fr.init_pos)
+        os.replace(tmp, fn)
     return mp, fr
 
 
