@@ -168,6 +168,7 @@ SIGNATURES = {
     "slio_destroy": (C.c_int, [_P]),
     "slio_set_stream": (C.c_int, [_P, _P]),
     "slio_last_error": (C.c_char_p, []),
+    "slio_build_id": (C.c_char_p, []),
     "slio_map_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
     "slio_map_share": (C.c_int, [_P, _P]),
     "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),

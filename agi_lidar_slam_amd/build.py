@@ -6,6 +6,7 @@ travels with the repository snapshot to the GPU box.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -32,20 +33,35 @@ FLAGS = [
 ]
 
 
+def _deps() -> list[str]:
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    return deps + [os.path.join(ROOT, "include", h) for h in ("slio.h", "slio_frontend.h")]
+
+
+def source_hash() -> str:
+    """16 hex digits of a SHA-256 over the library's sources and headers; the
+    library reports the digest it was compiled with (slio_build_id)."""
+    h = hashlib.sha256()
+    for d in _deps():
+        if os.path.exists(d):
+            h.update(os.path.basename(d).encode())
+            h.update(open(d, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps += [os.path.join(ROOT, "include", h) for h in ("slio.h", "slio_frontend.h")]
-    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in _deps())
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), *srcs, "-o", LIB + ".tmp"]
+    cmd = [HIPCC, *FLAGS, f'-DSLIO_SOURCE_HASH="{source_hash()}"', "-I", os.path.join(ROOT, "include"),
+           *srcs, "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

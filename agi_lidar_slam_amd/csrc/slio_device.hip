@@ -2955,6 +2955,10 @@ int slio_debug_hwid(uint32_t* out, int nblocks) {
 #endif
 
 const char* slio_last_error(void) { return g_err.c_str(); }
+#ifndef SLIO_SOURCE_HASH
+#define SLIO_SOURCE_HASH "unknown"
+#endif
+const char* slio_build_id(void) { return SLIO_SOURCE_HASH; }
 
 int slio_params_default(slio_params* p) {
   if (!p) return SLIO_EINVAL;

@@ -115,6 +115,10 @@ int slio_destroy(slio_handle h);
  * torch.cuda.Stream current and pass that one. */
 int slio_set_stream(slio_handle h, void* hip_stream);
 const char* slio_last_error(void);
+/* Fingerprint of the sources this library was compiled from (16 hex digits
+ * of a SHA-256 over the csrc sources and these headers; build.py computes the
+ * same digest), so a caller can tell a stale prebuilt library. */
+const char* slio_build_id(void);
 
 /* ---- map (replaces KD_TREE::Build, ikd_Tree.cpp:355-367, for a static map;
  *      the search side replaces KD_TREE::Nearest_Search ikd_Tree.cpp:370) -- */

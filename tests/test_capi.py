@@ -144,3 +144,11 @@ def test_state_boxplus_boxminus(lib):
         yc = y.to_c()
         assert lib.slio_state_boxminus(C.byref(yc), C.byref(xc), L.dptr(d)) == 0
         np.testing.assert_allclose(d, dx, atol=1e-9)
+
+
+def test_library_built_from_these_sources(lib):
+    """slio_build_id is the digest of the sources the library was compiled
+    from; a prebuilt library that does not match the tree is caught here and
+    by __graft_entry__.build()."""
+    from agi_lidar_slam_amd import build
+    assert lib.slio_build_id().decode() == build.source_hash()
