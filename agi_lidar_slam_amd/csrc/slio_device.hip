@@ -432,6 +432,96 @@ __global__ void k_coarse_boxes(const float4* __restrict__ cpts, const uint32_t* 
   }
 }
 
+// Coarse level without a sort.  A coarse cell (edge 4h, same origin) is the
+// 4x4x4 fine cells [4c, 4c + 4) per axis, clipped to the fine grid, so its
+// points are the fine runs of its 16 (y, z) rows -- each a contiguous x-range
+// of cells of the cell-sorted pts -- and taking the rows in order lists them in
+// fine position order, the order a stable sort by coarse cell gave.  (A point
+// lies within tol of its fine cell, hence of that cell's coarse cell; the far
+// search's bounds carry the same tol.)
+__device__ __forceinline__ void coarse_decode(const GridGeom& cg, int64_t c, int& x, int& y, int& z) {
+  x = (int)(c % cg.dx);
+  const int64_t t = c / cg.dx;
+  y = (int)(t % cg.dy);
+  z = (int)(t / cg.dy);
+}
+__global__ void k_coarse_count(const uint32_t* __restrict__ start, GridGeom g, GridGeom cg, int64_t nc,
+                               uint32_t* __restrict__ cnt) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0) cnt[nc] = 0;
+  if (c >= nc) return;
+  int cx, cy, cz;
+  coarse_decode(cg, c, cx, cy, cz);
+  const int x0 = 4 * cx, x1 = min(4 * cx + 4, g.dx);
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int fy = 4 * cy + (k & 3), fz = 4 * cz + (k >> 2);
+    if (fy < g.dy && fz < g.dz) {
+      const int64_t rb = ((int64_t)fz * g.dy + fy) * g.dx;
+      sum += start[rb + x1] - start[rb + x0];
+    }
+  }
+  cnt[c] = sum;
+}
+// one wavefront per coarse cell: copy its rows (.w = fine position) and form
+// its tight box (count in lo.w), as k_coarse_boxes does for sorted points
+__global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __restrict__ start, GridGeom g,
+                              GridGeom cg, const uint32_t* __restrict__ cstart, int64_t nc,
+                              float4* __restrict__ cpts, float4* __restrict__ lo, float4* __restrict__ hi) {
+  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (c >= nc) return;
+  int cx, cy, cz;
+  coarse_decode(cg, c, cx, cy, cz);
+  const int x0 = 4 * cx, x1 = min(4 * cx + 4, g.dx);
+  uint32_t rs = 0, len = 0;
+  if (lane < 16) {
+    const int fy = 4 * cy + (lane & 3), fz = 4 * cz + (lane >> 2);
+    if (fy < g.dy && fz < g.dz) {
+      const int64_t rb = ((int64_t)fz * g.dy + fy) * g.dx;
+      rs = start[rb + x0];
+      len = start[rb + x1] - rs;
+    }
+  }
+  uint32_t inc = len;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  const uint32_t excl = inc - len;
+  const uint32_t base = cstart[c], total = cstart[c + 1] - base;
+  const float INF = __int_as_float(0x7f800000);
+  float l[3] = {INF, INF, INF}, u[3] = {-INF, -INF, -INF};
+  if (total > 0) {
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t s0 = __shfl(rs, r, 64), n = __shfl(len, r, 64), d = base + __shfl(excl, r, 64);
+      for (uint32_t j = lane; j < n; j += 64) {
+        const float4 v = pts[s0 + j];
+        cpts[d + j] = make_float4(v.x, v.y, v.z, __uint_as_float(s0 + j));
+        l[0] = fminf(l[0], v.x);
+        l[1] = fminf(l[1], v.y);
+        l[2] = fminf(l[2], v.z);
+        u[0] = fmaxf(u[0], v.x);
+        u[1] = fmaxf(u[1], v.y);
+        u[2] = fmaxf(u[2], v.z);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        l[a] = fminf(l[a], __shfl_xor(l[a], o, 64));
+        u[a] = fmaxf(u[a], __shfl_xor(u[a], o, 64));
+      }
+  }
+  if (lane == 0) {
+    lo[c] = make_float4(l[0], l[1], l[2], __uint_as_float(total));
+    hi[c] = make_float4(u[0], u[1], u[2], 0.0f);
+  }
+}
+
 // ---------------------------------------------------------------- math helpers
 struct PoseDev {
   double rq[4], pos[3], lq[4], tli[3];  // quaternions (w, x, y, z)
@@ -3236,16 +3326,34 @@ static int build_blk(MapDev& m, hipStream_t st, const char* who) {
   return SLIO_OK;
 }
 
+// in_id_order: `in` is the map's previous cell-sorted points (survivors, in
+// their stored order) followed by points with larger ids in id order -- then,
+// when the grid comes out the same as before (or the map was empty), a STABLE
+// sort by cell alone yields (cell, id) order, and the 32-bit cell key needs
+// about half the radix passes of the 64-bit (cell, id) key.
 static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3], const float mx[3],
-                       hipStream_t st, const char* who, bool with_blk = true) {
+                       hipStream_t st, const char* who, bool with_blk = true, bool in_id_order = false,
+                       bool had_points = false) {
   m.blk_deferred = false;
+  const GridGeom g_old = m.g;
   GridGeom g;
   float hcell = m.cell0;
   // kGridPad empty cells around the map's bounding box: scan points just
   // outside it (ground returns below a flat map's lowest point, range noise)
   // still get a query cell inside the grid, so they take the 3x3x3 fast path
-  constexpr int kGridPad = 2;
-  for (;;) {
+  // A rebuild keeps the previous grid while the points still lie at least one
+  // cell inside it (the grid need not be tight: every bound is conservative),
+  // so the cell-only sort below applies; when they do not, the new grid gets
+  // twice the padding, and a map growing slowly at an edge re-grids rarely.
+  const int kGridPad = in_id_order ? 4 : 2;
+  bool keep_grid = in_id_order && had_points;
+  if (keep_grid) {
+    const float o[3] = {g_old.ox, g_old.oy, g_old.oz};
+    const int d[3] = {g_old.dx, g_old.dy, g_old.dz};
+    for (int a = 0; a < 3; ++a)
+      keep_grid = keep_grid && mn[a] >= o[a] + g_old.h && mx[a] <= o[a] + (float)(d[a] - 1) * g_old.h;
+  }
+  for (; !keep_grid;) {
     g.ox = mn[0] - kGridPad * hcell;
     g.oy = mn[1] - kGridPad * hcell;
     g.oz = mn[2] - kGridPad * hcell;
@@ -3258,10 +3366,20 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     if (nc <= m.max_cells && nc < (int64_t)0xFFFFFFF0ll) break;
     hcell *= 1.25f;  // grow cells until the dense table fits the budget
   }
+  if (keep_grid) g = g_old;
   // largest |coordinate| a cell face can have: |origin| + dims * h per axis
+  // (kept grid: the same tol as before)
   const float mag = std::max(std::fabs(g.ox) + (float)g.dx * g.h,
                              std::max(std::fabs(g.oy) + (float)g.dy * g.h, std::fabs(g.oz) + (float)g.dz * g.h));
   g.tol = mag * 3.814697265625e-06f + 1.0e-5f;  // 2^-18 relative: >= 64 ulps
+  const bool cell_only =
+      in_id_order && (!had_points || (g.ox == g_old.ox && g.oy == g_old.oy && g.oz == g_old.oz &&
+                                      g.h == g_old.h && g.dx == g_old.dx && g.dy == g_old.dy &&
+                                      g.dz == g_old.dz));
+  if (in_id_order && std::getenv("SLIO_DEBUG_REBUILD"))
+    std::fprintf(stderr, "slio rebuild: n %lld cell_only %d grid %d %d %d (was %d %d %d) origin %.6g %.6g %.6g (was %.6g %.6g %.6g)\n",
+                 (long long)n, (int)cell_only, g.dx, g.dy, g.dz, g_old.dx, g_old.dy, g_old.dz, g.ox, g.oy, g.oz,
+                 g_old.ox, g_old.oy, g_old.oz);
   m.g = g;
   m.n = n;
   m.ncells = (int64_t)g.dx * g.dy * g.dz;
@@ -3326,48 +3444,53 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     while (cbits < 32 && ((int64_t)1 << cbits) < m.ncells) ++cbits;
     int ccbits = 1;
     while (ccbits < 32 && ((int64_t)1 << ccbits) < m.nccells) ++ccbits;
-    size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, idbits + cbits, st)) ||
         (e = hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c0, c1, v0, v1, (int)n, 0, ccbits, st)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(nullptr, t5, c0, c1, v0, v1, (int)n, 0, cbits, st)) ||
         (e = hipcub::DeviceScan::ExclusiveSum(nullptr, t3, cnt, m.start, (int)maxc, st))) {
       rc = fail("sort size", e);
       break;
     }
-    t4 = std::max(std::max(t1, t2), t3);
+    t4 = std::max(std::max(std::max(t1, t2), t3), t5);
     if ((e = m.take(m.b_tmp[7], t4))) {
       rc = fail("hipMalloc tmp", e);
       break;
     }
     tmp = m.b_tmp[7].p;
     const int nb = grid_blocks(n);
-    k_cell_keys64<<<nb, 256, 0, st>>>(in, n, g, idbits, k0, v0);
-    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, k0, k1, v0, v1, (int)n, 0, idbits + cbits, st)) ||
-        (e = hipMemsetAsync(cnt, 0, 4 * (m.ncells + 1), st))) {
-      rc = fail("sort", e);
-      break;
+    if (cell_only) {
+      k_coarse_keys<<<nb, 256, 0, st>>>(in, n, g, c0, v0);  // fine cell keys (same formula)
+      if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, c0, c1, v0, v1, (int)n, 0, cbits, st)) ||
+          (e = hipMemsetAsync(cnt, 0, 4 * (m.ncells + 1), st))) {
+        rc = fail("sort", e);
+        break;
+      }
+      k_cell_hist_sorted<uint32_t><<<nb, 256, 0, st>>>(c1, n, 0, cnt);
+    } else {
+      k_cell_keys64<<<nb, 256, 0, st>>>(in, n, g, idbits, k0, v0);
+      if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, k0, k1, v0, v1, (int)n, 0, idbits + cbits, st)) ||
+          (e = hipMemsetAsync(cnt, 0, 4 * (m.ncells + 1), st))) {
+        rc = fail("sort", e);
+        break;
+      }
+      k_cell_hist_sorted<uint64_t><<<nb, 256, 0, st>>>(k1, n, idbits, cnt);
     }
-    k_cell_hist_sorted<uint64_t><<<nb, 256, 0, st>>>(k1, n, idbits, cnt);
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.start, (int)(m.ncells + 1), st))) {
       rc = fail("scan", e);
       break;
     }
     k_gather4<<<nb, 256, 0, st>>>(in, v1, n, m.pts);
     k_fill_u8<<<nb, 256, 0, st>>>(m.keep, n, 1);
-    // coarse level: points re-sorted by coarse cell (stable: fine positions
-    // ascend inside a coarse cell), tight boxes
-    k_coarse_keys<<<nb, 256, 0, st>>>(m.pts, n, cg, c0, v0);
-    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, t4, c0, c1, v0, v1, (int)n, 0, ccbits, st)) ||
-        (e = hipMemsetAsync(cnt, 0, 4 * (m.nccells + 1), st))) {
-      rc = fail("coarse sort", e);
-      break;
-    }
-    k_cell_hist_sorted<uint32_t><<<nb, 256, 0, st>>>(c1, n, 0, cnt);
+    // coarse level from the fine cell table (k_coarse_count / k_coarse_fill:
+    // no sort), tight boxes
+    k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, cg, m.nccells, cnt);
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.cstart, (int)(m.nccells + 1), st))) {
       rc = fail("coarse scan", e);
       break;
     }
-    k_coarse_gather<<<nb, 256, 0, st>>>(m.pts, v1, n, m.cpts);
-    k_coarse_boxes<<<grid_blocks(m.nccells * 64), 256, 0, st>>>(m.cpts, m.cstart, m.nccells, m.clo, m.chi);
+    k_coarse_fill<<<grid_blocks(m.nccells * 64), 256, 0, st>>>(m.pts, m.start, g, cg, m.cstart, m.nccells,
+                                                                  m.cpts, m.clo, m.chi);
     if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
       rc = fail("build kernels", e);
       break;
@@ -3920,9 +4043,10 @@ static int map_refresh(Ctx& c, bool adds_only) {
       mx[a] = fkey_inv(got[3 + a]);
     }
   // in4 is b_ref[0]: build_index reads it while writing the b_* tables
+  const bool had_points = n0 > 0;
   m.free_index();
   m.nadd = 0;
-  const int rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild", false);
+  const int rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild", false, true, had_points);
   m.version++;
   m.dirty = false;
   return rc;

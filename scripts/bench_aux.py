@@ -62,7 +62,8 @@ def mapping(n_map, n_scan, frames_n=6):
     tr = np.median([r[1] for r in rows[1:]])
     print(json.dumps({"bench": "live_mapping_per_scan", "map_points": n_map, "scan_points": n_scan,
                       "ms_fov_ikf4_map_incremental": tt, "ms_index_rebuild": tr,
-                      "ms_per_scan": tt + tr, "map_size_after": rows[-1][2],
+                      "ms_per_scan": tt + tr, "ms_index_rebuild_each": [round(r[1], 3) for r in rows],
+                      "map_size_after": rows[-1][2],
                       "map_incremental_counts_last": rows[-1][3]}), flush=True)
 
 

@@ -1,0 +1,9 @@
+# sort-free coarse level: full GPU suite, live-mapping timing
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=${1:-s12}
+bash scripts/gpu_round.sh ${tag} tests || exit $?
+grep -q " passed" gpurun_out/${tag}_tests.log && ! grep -q "failed" gpurun_out/${tag}_tests.log || { echo "tests not green"; exit 3; }
+SLIO_DEBUG_REBUILD=1 timeout -k 10 300 python scripts/bench_aux.py mapping > gpurun_out/${tag}_aux.jsonl 2> gpurun_out/${tag}_aux.err || { tail -5 gpurun_out/${tag}_aux.err; exit 4; }
+cat gpurun_out/${tag}_aux.jsonl
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 scripts/bench_aux.py mapping > gpurun_out/${tag}_prof.log 2>&1 || { echo "prof failed"; tail -5 gpurun_out/${tag}_prof.log; exit 5; }
