@@ -472,6 +472,15 @@ __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __
   const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (c >= nc) return;
+  const uint32_t base = cstart[c], total = cstart[c + 1] - base;
+  const float INF = __int_as_float(0x7f800000);
+  if (total == 0) {  // most coarse cells of a surface map: no row bounds needed
+    if (lane == 0) {
+      lo[c] = make_float4(INF, INF, INF, __uint_as_float(0u));
+      hi[c] = make_float4(-INF, -INF, -INF, 0.0f);
+    }
+    return;
+  }
   int cx, cy, cz;
   coarse_decode(cg, c, cx, cy, cz);
   const int x0 = 4 * cx, x1 = min(4 * cx + 4, g.dx);
@@ -491,22 +500,29 @@ __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __
     if (lane >= o) inc += v;
   }
   const uint32_t excl = inc - len;
-  const uint32_t base = cstart[c], total = cstart[c + 1] - base;
-  const float INF = __int_as_float(0x7f800000);
   float l[3] = {INF, INF, INF}, u[3] = {-INF, -INF, -INF};
-  if (total > 0) {
+  {
+    // the cell's points as one flat list over its rows: lane j takes list
+    // entries j, j + 64, ... (row r = the last row starting at or before the
+    // entry), so one round trip serves 64 points whatever the rows
+    uint32_t E[16], S[16];
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const uint32_t s0 = __shfl(rs, r, 64), n = __shfl(len, r, 64), d = base + __shfl(excl, r, 64);
-      for (uint32_t j = lane; j < n; j += 64) {
-        const float4 v = pts[s0 + j];
-        cpts[d + j] = make_float4(v.x, v.y, v.z, __uint_as_float(s0 + j));
-        l[0] = fminf(l[0], v.x);
-        l[1] = fminf(l[1], v.y);
-        l[2] = fminf(l[2], v.z);
-        u[0] = fmaxf(u[0], v.x);
-        u[1] = fmaxf(u[1], v.y);
-        u[2] = fmaxf(u[2], v.z);
-      }
+      E[r] = __shfl(excl, r, 64);
+      S[r] = __shfl(rs, r, 64) - E[r];  // list entry j of row r is pts[S[r] + j]
+    }
+    for (uint32_t j = lane; j < total; j += 64) {
+      uint32_t src = S[0] + j;
+#pragma unroll
+      for (int r = 1; r < 16; ++r) src = (j >= E[r]) ? S[r] + j : src;
+      const float4 v = pts[src];
+      cpts[base + j] = make_float4(v.x, v.y, v.z, __uint_as_float(src));
+      l[0] = fminf(l[0], v.x);
+      l[1] = fminf(l[1], v.y);
+      l[2] = fminf(l[2], v.z);
+      u[0] = fmaxf(u[0], v.x);
+      u[1] = fmaxf(u[1], v.y);
+      u[2] = fmaxf(u[2], v.z);
     }
 #pragma unroll
     for (int a = 0; a < 3; ++a)
