@@ -50,10 +50,13 @@ def source_hash() -> str:
 
 
 def _stale() -> bool:
+    """The library is stale unless it carries the digest of the current
+    sources (slio_build_id's string is embedded in the binary); file times
+    are not trusted, as a copy or checkout changes them."""
     if not os.path.exists(LIB):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in _deps())
+    with open(LIB, "rb") as f:
+        return source_hash().encode() not in f.read()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
