@@ -3073,7 +3073,7 @@ int slio_params_default(slio_params* p) {
   p->max_points = 100000;
   p->rank = 0;
   p->nranks = 1;
-  p->grid_cell = 1.25f;      // tuned on MI355X for 0.5 m map resolution
+  p->grid_cell = 1.0f;       // tuned on MI355X for 0.5 m map resolution (C2 street scene)
   p->search_radius = 0.0f;   // 3x3x3 block first (tuned); > 0 selects the sphere search
   p->plane_threshold = 0.1f;
   p->max_match_sqd = 5.0f;

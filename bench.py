@@ -231,7 +231,9 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--map-points", type=int, default=10_000_000)
     ap.add_argument("--scan-points", type=int, default=100_000)
-    ap.add_argument("--cell", type=float, default=1.25)
+    ap.add_argument("--cell", type=float, default=1.0,
+                    help="map grid cell edge (speed only; results are exact at any edge): "
+                         "1.0 m is the sweep's best for the 0.5 m map, profiles/r02_cell_sweep.log")
     ap.add_argument("--scan-order", choices=["voxel", "capture"], default="voxel",
                     help="voxel: pcl::VoxelGrid output order, as feats_down_body reaches "
                          "h_share_model in the reference; capture: rosette firing order")

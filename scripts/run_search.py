@@ -15,7 +15,7 @@ from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 def main():
     lib = L.load(os.environ.get("SLIO_LIB", L.LIB_PATH))
     lpq = int(os.environ.get("LPQ", "2"))
-    cell = float(os.environ.get("CELL", "1.25"))
+    cell = float(os.environ.get("CELL", "1.0"))
     reps = int(os.environ.get("REPS", "20"))
     mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
     nscan = int(os.environ.get("NSCAN", "100000"))

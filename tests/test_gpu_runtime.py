@@ -7,7 +7,7 @@
   loop (slio_ikf_update_device, k_ikf_solve after the reduce) vs the
   single-rank update (bitwise) and the oracle (north_star tolerance).
 * The benchmarked C2 configuration at full size (100k scan vs 10M map, cell
-  1.25 m, block rows, device loop, 4 iterations, REFERENCE and FIXED control
+  1.0 m, block rows, device loop, 4 iterations, REFERENCE and FIXED control
   flow) vs oracle.ikf_update, and the whole scan's Nearest_Points bit-exact
   vs the oracle's ikd-Tree restatement at the final pose.
 * C5's batched replay with a DIFFERENT scan per handle, each replica equal
@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 
 TOL_POS = 1e-4   # m   (north_star)
 TOL_ROT = 1e-5   # rad (north_star)
-C2_CELL = 1.25   # bench.py's grid cell
+C2_CELL = 1.0    # bench.py's grid cell
 
 
 def slio_state(st):
@@ -175,7 +175,7 @@ def test_multirank_threads_reduce_hook(L, oracle_mod, c2, device_loop):
 
 @pytest.mark.parametrize("mode", [0, 1])
 def test_c2_full_size_pinned(L, oracle_mod, c2, mode):
-    """The benchmarked configuration (C2, cell 1.25, block rows, device loop,
+    """The benchmarked configuration (C2, cell 1.0, block rows, device loop,
     4 iterations) vs oracle.ikf_update: state within 1e-4 m / 1e-5 rad, the
     same control flow; then one search pass at the GPU's final pose gives
     Nearest_Points and the selection bit-exact vs the oracle over all 100k
