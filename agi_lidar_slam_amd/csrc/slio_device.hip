@@ -3073,7 +3073,7 @@ int slio_params_default(slio_params* p) {
   p->max_points = 100000;
   p->rank = 0;
   p->nranks = 1;
-  p->grid_cell = 1.0f;       // tuned on MI355X for 0.5 m map resolution (C2 street scene)
+  p->grid_cell = 0.0f;       // auto: 1.0 m, or 1.25 m for a grid of more than 2^27 cells
   p->search_radius = 0.0f;   // 3x3x3 block first (tuned); > 0 selects the sphere search
   p->plane_threshold = 0.1f;
   p->max_match_sqd = 5.0f;
@@ -3108,7 +3108,7 @@ int slio_create(slio_handle* out, const slio_params* p) {
   if (rc) return rc;
   auto* h = new slio_ctx();
   h->c.prm = *p;
-  if (h->c.prm.grid_cell <= 0.0f) h->c.prm.grid_cell = 1.0f;
+  if (!(h->c.prm.grid_cell > 0.0f)) h->c.prm.grid_cell = 0.0f;  // auto (build_index)
   if (h->c.prm.max_grid_cells <= 0) h->c.prm.max_grid_cells = (int64_t)1 << 29;
   {
     const int l = h->c.prm.lanes_per_query;
@@ -3353,7 +3353,12 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
   m.blk_deferred = false;
   const GridGeom g_old = m.g;
   GridGeom g;
-  float hcell = m.cell0;
+  // cell edge: the caller's, or auto (cell0 == 0): 1.0 m -- the best edge for the
+  // 10M-point, 0.5 m map (cell edge) -- unless that grid has more
+  // than 2^27 cells, whose tables overflow the Infinity Cache and slow every
+  // query's first loads: then 1.25 m (the 50M-point map's best)
+  const bool auto_cell = !(m.cell0 > 0.0f);
+  float hcell = auto_cell ? 1.0f : m.cell0;
   // kGridPad empty cells around the map's bounding box: scan points just
   // outside it (ground returns below a flat map's lowest point, range noise)
   // still get a query cell inside the grid, so they take the 3x3x3 fast path
@@ -3379,6 +3384,10 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     g.dy = cell_coord(mx[1], g.oy, g.inv_h) + 1 + kGridPad;
     g.dz = cell_coord(mx[2], g.oz, g.inv_h) + 1 + kGridPad;
     const int64_t nc = (int64_t)g.dx * g.dy * g.dz;
+    if (auto_cell && hcell == 1.0f && nc > ((int64_t)1 << 27)) {
+      hcell = 1.25f;
+      continue;
+    }
     if (nc <= m.max_cells && nc < (int64_t)0xFFFFFFF0ll) break;
     hcell *= 1.25f;  // grow cells until the dense table fits the budget
   }

@@ -96,7 +96,7 @@ class KdTreeMap(_Handle):
     reported by the filter refer to rows of the array passed to Build.
     """
 
-    def __init__(self, device: int = 0, grid_cell: float = 1.0):
+    def __init__(self, device: int = 0, grid_cell: float = 0.0):  # 0: the library's auto edge
         super().__init__(_params(device, 1, 0, 1, grid_cell, 0.1, 5.0))
         self.points = np.zeros((0, 3), np.float32)
         # bumped by every Build: a filter bound to this map re-shares it (a

@@ -231,9 +231,9 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--map-points", type=int, default=10_000_000)
     ap.add_argument("--scan-points", type=int, default=100_000)
-    ap.add_argument("--cell", type=float, default=1.0,
-                    help="map grid cell edge (speed only; results are exact at any edge): "
-                         "1.0 m is the sweep's best for the 0.5 m map, profiles/r02_cell_sweep.log")
+    ap.add_argument("--cell", type=float, default=0.0,
+                    help="map grid cell edge (speed only; results are exact at any edge); 0: the "
+                         "library's auto edge, 1.0 m at C2 (the sweep's best, profiles/r02_cell_sweep.log)")
     ap.add_argument("--scan-order", choices=["voxel", "capture"], default="voxel",
                     help="voxel: pcl::VoxelGrid output order, as feats_down_body reaches "
                          "h_share_model in the reference; capture: rosette firing order")
@@ -303,6 +303,9 @@ def main():
     t0 = time.time()
     L.check(lib.slio_map_upload(h, L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")
     log(f"[rank {rank}] map index built in {time.time() - t0:.2f}s")
+    cell_m = C.c_float()
+    L.check(lib.slio_map_info(h, None, C.byref(cell_m), None), "map_info")
+    cell_m = float(cell_m.value)  # the edge the library chose
     bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
     L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]), "scan")
     b, e = C.c_int64(), C.c_int64()
@@ -398,7 +401,7 @@ def main():
 
     l2 = None
     if rank == 0 and avg_kernel_s > 0:
-        dem = l2_demand_bytes(mp, fr.body[b.value:e.value], st0, args.cell)
+        dem = l2_demand_bytes(mp, fr.body[b.value:e.value], st0, cell_m)
         l2 = {"demand_bytes_per_launch": dem, "achieved": dem / avg_kernel_s / 1e9,
               "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": dem / avg_kernel_s / 1e9 / L2_PEAK_GBS,
               "note": "L2-level roofline of the same launches: block-row candidates + "
@@ -460,7 +463,7 @@ def main():
             "scan_points": args.scan_points,
             "iterations_per_step": args.iters,
             "ikf_loop": "host" if args.host_loop else "device-resident",
-            "grid_cell_m": args.cell,
+            "grid_cell_m": cell_m,
             "parallelism": (f"scan points sharded x{world}, map replicated, one RCCL all-reduce "
                             "of 8x91 fp64 per iteration" if world > 1 else "single GPU"),
             "effective_points": int(stats.last_m),

@@ -60,7 +60,9 @@ typedef struct slio_params {
                               (esekfom.hpp:23-29)                             */
   int32_t rank;            /* this handle's shard of the scan points          */
   int32_t nranks;          /* 1, 2, 4 or 8 (must divide SLIO_NSUPER)          */
-  float grid_cell;         /* map grid cell edge in metres (default 1.0)      */
+  float grid_cell;         /* map grid cell edge in metres; 0 (default): auto,
+                              1.0 m, or 1.25 m when the 1.0 m grid would have
+                              more than 2^27 cells (speed only)               */
   float plane_threshold;   /* esti_plane threshold, 0.1f (esekfom.hpp:157)    */
   float max_match_sqd;     /* 5th-NN sq.-distance gate, 5 (esekfom.hpp:147)   */
   int32_t lanes_per_query; /* search lanes per scan point: 1, 2, 4, 8 (0 ->

@@ -54,6 +54,7 @@ def test_params_default(lib):
     assert p.max_points == 100000 and p.nranks == 1
     assert abs(p.plane_threshold - 0.1) < 1e-7 and p.max_match_sqd == 5.0
     assert p.far_query_margin == 0.0 and p.search_radius == 0.0
+    assert p.grid_cell == 0.0   # auto edge (1.0 m, 1.25 m past 2^27 cells)
 
 
 def test_bad_arguments_fail_loudly(lib):

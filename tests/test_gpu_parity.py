@@ -488,3 +488,21 @@ def test_batched_replay_concurrent_bitwise(L, c1):
     finally:
         for h in reversed(hs):
             lib.slio_destroy(h)
+
+
+def test_auto_cell_edge(L):
+    """grid_cell 0 (the default): 1.0 m, or 1.25 m when the 1.0 m grid would
+    exceed 2^27 cells (cell edge)."""
+    lib = L.load()
+    rng = np.random.default_rng(7)
+    for extent, want in ((np.array([200.0, 200.0, 30.0]), 1.0),
+                         (np.array([600.0, 600.0, 400.0]), 1.25)):
+        pts = (rng.random((5000, 3)) * extent).astype(np.float32)
+        h = mk(L, cell=0.0)
+        try:
+            upload_map(L, h, pts)
+            cell = C.c_float()
+            L.check(lib.slio_map_info(h, None, C.byref(cell), None), "info")
+            assert cell.value == want
+        finally:
+            lib.slio_destroy(h)
