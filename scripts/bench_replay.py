@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--map-points", type=int, default=10_000_000)
     ap.add_argument("--scan-points", type=int, default=100_000)
-    ap.add_argument("--cell", type=float, default=1.25)  # 50M map: 1.25 m beats 1.0 m
+    ap.add_argument("--cell", type=float, default=0.0)  # auto: 1.25 m on the 50M map, 1.0 m on 10M
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
     args = ap.parse_args()
 
