@@ -64,8 +64,8 @@ struct IkfCtl {
   slio_state x;      // x_ (current iterate)
   slio_state xprop;  // x_propagated
   double P[576];     // P_ (row-major)
-  double P11i[144];  // (P[:12, :12])^-1 of P_, fixed during an update (host)
-  double G[288];     // P[:, :12] P11i                                   (host)
+  double P11i[144];  // (P[:D, :D])^-1 of P_ (D x D), fixed during an update (host)
+  double G[288];     // P[:, :D] P11i (24 x D)                             (host)
   double dxn[24];    // x [-] x_propagated of the current iterate: 0 on the first
                      // pass (host), then written by the pass kernel (device)
   int32_t converge, t, done, search_now;
@@ -73,11 +73,13 @@ struct IkfCtl {
   int64_t last_m;
   int32_t singular;
   int32_t published;  // mapped host block: set (release, system scope) after x, P and the flags
-  double LM[300];    // Cholesky factor of S = P11i + H^T H / R, H^T H / R and
-                     // 1 / diag of the factor, of the last valid pass (device only)
+  double LM[300];    // Cholesky factor of S = P11i + H^T H / R (D x D), H^T H / R
+                     // (upper triangle, 78) and 1 / diag of the factor, of the
+                     // last valid pass (device only)
 };
 
-// P11^-1 and G = P[:, :12] P11^-1 of an update's prior P (slio_ikf.cpp)
-bool info_constants(const double* P, double P11i[144], double G[288]);
+// P_DD^-1 (D x D) and G = P[:, :D] P_DD^-1 (24 x D) of an update's prior P,
+// D = 6 or 12 (slio_ikf.cpp)
+bool info_constants(const double* P, int D, double P11i[144], double G[288]);
 
 }  // namespace slio

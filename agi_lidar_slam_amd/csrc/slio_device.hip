@@ -27,6 +27,8 @@
 #include <cstring>
 #include <type_traits>
 #include <memory>
+#include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -132,6 +134,8 @@ struct CoarseView {
   const float4* hi;         // per coarse cell: max x, y, z
 };
 
+struct Ctx;
+
 struct MapDev {
   GridGeom g;
   int64_t n = 0;
@@ -163,13 +167,25 @@ struct MapDev {
   uint8_t* akeep = nullptr;
   int64_t nadd = 0, add_cap = 0;
   uint32_t next_id = 0;
-  uint64_t version = 1;           // bumped by every rebuild (positions change)
-  bool dirty = false;
+  std::atomic<uint64_t> version{1};  // bumped by every rebuild (positions change)
+  std::atomic<bool> dirty{false};
   // block rows of a rebuilt map are built once it has been searched
   // kBlkAfterPasses times unchanged (a map changed every scan goes without:
   // they cost ~1 ms per rebuild and save ~5 us per search pass)
-  bool blk_deferred = false;
+  std::atomic<bool> blk_deferred{false};
   int stable_passes = 0;
+  // Sharing (slio_map_share).  Changes -- edits, rebuilds, block rows --
+  // hold mu exclusively; passes and reads hold it shared from reading the
+  // views through their launches.  Streams: a change first orders its stream
+  // after everything the other users have enqueued (they may still be
+  // reading what it overwrites: map_write_begin), then records `ready` and
+  // bumps `epoch`; a reader whose stream has not yet waited for the current
+  // epoch waits for `ready` (map_read_sync).
+  std::shared_mutex mu;
+  std::vector<Ctx*> users;  // handles holding this map
+  hipEvent_t ready = nullptr;
+  uint64_t epoch = 0;
+  bool broken = false;  // an index rebuild failed part-way: unusable until a new upload
   float cell0 = 1.0f;             // requested grid cell and cell budget (slio_params)
   int64_t max_cells = 0;
   // device allocations kept across index rebuilds (capacity in bytes): a
@@ -208,6 +224,7 @@ struct MapDev {
     n = ncells = nccells = nblk = 0;
   }
   ~MapDev() {
+    if (ready) (void)hipEventDestroy(ready);
     for (Buf* b : {&b_pts, &b_keep, &b_cpts, &b_start, &b_cstart, &b_clo, &b_chi, &b_bstart, &b_blk})
       if (b->p) (void)hipFree(b->p);
     for (Buf& b : b_tmp)
@@ -625,12 +642,14 @@ __device__ __forceinline__ void jacobian_row(const PoseDev& P, float bx, float b
   row[3] = A0;
   row[4] = A1;
   row[5] = A2;
+  // without extrinsic estimation the reference's row ends in six zeros
+  // (esekfom.hpp:218-220): B and C
   row[6] = B0;
   row[7] = B1;
   row[8] = B2;
-  row[9] = C0;
-  row[10] = C1;
-  row[11] = C2;
+  row[9] = extrinsic ? C0 : 0.0;
+  row[10] = extrinsic ? C1 : 0.0;
+  row[11] = extrinsic ? C2 : 0.0;
 }
 
 // body -> world in double, rounded to the float query (esekfom.hpp:128-132)
@@ -1135,6 +1154,7 @@ struct PassOut {
   double* chunk_part;  // C * NPROD (global chunk index)
   uint32_t* far_ctr;   // [1]: deferred (far) queries of this pass, all chunks
   PoseDev* pose;       // the pass's pose (block 0), for nbr_settle
+  uint32_t* chunk_cost;  // per chunk of the rank (relative index): candidates + refinement / far weights
 };
 
 // far_query_margin: squared distance from the query to the grid's bounding box
@@ -1158,6 +1178,7 @@ struct PassCfg {
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
   int knn_only;            // 1: neighbours only (nbr_*), no fit / rows / products
+  const uint32_t* perm;    // block -> chunk order within each XCD's range (chunk_order), or null
 };
 
 // ---------------------------------------------------------------- far queries
@@ -1383,7 +1404,8 @@ __device__ __forceinline__ int64_t xcd_chunk(int64_t c_begin, int64_t nblk) {
 
 // ---------------------------------------------------------------- filter step
 constexpr int kSolveThreads = 256;
-constexpr int kSuperSeg = 8;
+constexpr int kSuperSeg = 8;                     // segments per super-chunk
+constexpr int kNSeg = SLIO_NSUPER * kSuperSeg;   // segment rows per pass: one workgroup each
 
 // global-address-space views for the in-launch hand-off (sc1 accesses)
 typedef __attribute__((address_space(1))) double gdouble;
@@ -1402,38 +1424,36 @@ __device__ __forceinline__ void reset_counter(uint32_t* p) {
   __hip_atomic_store((guint*)p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// LDS of the filter step.
-struct SolveLds {
-  double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums of this pass
-  double S[144];     // P11^-1 + M  (SPD), M = H^T H / R
-  double M[144];
-  double P11i[144];  // (P[:12, :12])^-1
-  double G[288];     // P[:, :12] P11^-1
+// LDS of the filter step.  D = 6 without extrinsic estimation (H's columns
+// 6..11 are zero, esekfom.hpp:218-220), 12 with it.
+struct StepLds {
+  union {
+    double seg[kNSeg][SLIO_NPROD];  // the pass's 64 segment rows (k_super_sums)
+    struct {
+      double Z[144];  // D x D: S^-1 M             (P update)
+      double K[288];  // 24 x D: G S^-1 M = K H[:, :D]
+    } zk;
+  } u;
+  double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums
+  double tot[SLIO_NPROD];               // H^T H (78, upper triangle), H^T h (12), m
+  double Mt[SLIO_NHTH];                 // H^T H / R (upper triangle)
+  double hR[12];                        // H^T h / R
   double P[576];
-  double Lf[144];    // Cholesky factor of S (rows, lower)
-  double invd[12];   // 1 / its diagonal
-  double Z[144];     // S^-1 M           (P update)
-  double K[288];     // G S^-1 M = K H [:, :12]   (P update)
-  double hth[SLIO_NPROD - SLIO_NHTH];  // H^T h (12) and m
-  double dxn[24], dx[24];
-  slio_state x, xprop;  // staged control-block fields
+  double P11i[144];                     // D x D: (P[:D, :D])^-1
+  double G[288];                        // 24 x D: P[:, :D] P11^-1
+  double dxn[24];
+  slio_state x, xprop;                  // staged control-block fields
   int32_t fl[8];
   int ok, s_final;
 };
 static_assert(offsetof(IkfCtl, xprop) == sizeof(slio_state), "IkfCtl: x, xprop adjacent");
-static_assert(offsetof(SolveLds, xprop) - offsetof(SolveLds, x) == sizeof(slio_state),
-              "SolveLds: x, xprop adjacent");
+static_assert(offsetof(StepLds, xprop) - offsetof(StepLds, x) == sizeof(slio_state),
+              "StepLds: x, xprop adjacent");
 static_assert(offsetof(IkfCtl, mode) - offsetof(IkfCtl, converge) == 7 * sizeof(int32_t),
               "IkfCtl: 8 contiguous flags");
 constexpr int kStateD = sizeof(slio_state) / sizeof(double);
 // flag slots of IkfCtl::converge..mode
 enum { F_CONV, F_T, F_DONE, F_SEARCH, F_PASSES, F_SEARCHES, F_VALID, F_MODE };
-
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
 
 // upper-triangle product index of (i, j), i <= j (product_table order)
 __device__ __forceinline__ int tri_index(int i, int j) { return i * 12 - (i * (i - 1)) / 2 + (j - i); }
@@ -1443,224 +1463,250 @@ __device__ __forceinline__ int tri_index(int i, int j) { return i * 12 - (i * (i
 // go through so3 exp / log.
 __device__ __forceinline__ int state_off(int k) { return k < 3 ? k : k + 2; }
 
-// Cholesky S = L L^T of the 12 x 12 SPD S by wave 0, row layout (lane i < 12
-// keeps row i in registers; column j is broadcast with readlane), then
-// S y = b by forward and backward substitution.  S = P11^-1 + M has every
-// eigenvalue >= that of P11^-1 > 0, so no pivoting is needed.  Leaves L in
-// L.Lf (rows) and returns y (uniform); false on a non-positive pivot.
-__device__ __forceinline__ bool chol_solve_wave(SolveLds& L, const double (&b)[12], double (&y)[12]) {
-  const int lane = threadIdx.x;  // wave 0 only
-  const bool row = lane < 12;
-  double a[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) a[k] = row ? L.S[lane * 12 + k] : 0.0;
-  double invd = 0.0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    const double d = readlane_d(a[j], j);
-    if (!(d > 0.0)) return false;
-    // 1 / sqrt(d): hardware estimate + two Newton steps (< 1 ulp), far
-    // shorter than IEEE sqrt followed by IEEE division
-    double inv = __builtin_amdgcn_rsq(d);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const double r = fma(-(d * inv), inv, 1.0);
-      inv = fma(0.5 * inv, r, inv);
-    }
-    const double ljj = d * inv;
-    a[j] = (lane == j) ? ljj : a[j] * inv;  // lanes i > j: L[i][j]
-    invd = (lane == j) ? inv : invd;
-#pragma unroll
-    for (int k = j + 1; k < 12; ++k) {
-      const double lkj = readlane_d(a[j], k);  // L[k][j]
-      a[k] = fma(-a[j], lkj, a[k]);
-    }
-  }
-  if (row) {
-#pragma unroll
-    for (int k = 0; k < 12; ++k) L.Lf[lane * 12 + k] = (k <= lane) ? a[k] : 0.0;
-    L.invd[lane] = invd;
-  }
-  wave_fence();
-  // forward: L z = b (lane i keeps the running residual of row i)
-  double r = 0.0;
-#pragma unroll
-  for (int k = 0; k < 12; ++k) r = (lane == k) ? b[k] : r;
-  double z = 0.0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    const double zj = readlane_d(r * invd, j);
-    z = (lane == j) ? zj : z;
-    r = fma(-a[j], zj, r);
-  }
-  // backward: L^T y = z (lane i holds column i of L = row i of L^T)
-  double lt[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) lt[k] = row ? L.Lf[k * 12 + lane] : 0.0;
-  double s = z;
-#pragma unroll
-  for (int j = 11; j >= 0; --j) {
-    const double yj = readlane_d(s * invd, j);
-    y[j] = yj;
-    s = fma(-lt[j], yj, s);
-  }
-  return true;
-}
-
-// One filter step of update_iterated_dyn_share_modified (esekfom.hpp:303-344)
-// on device by one workgroup of NT threads, in information form:
-//   K_front[:, :12] = (P^-1 + E^T M E)^-1 E^T = G S^-1,  G = P[:, :12] P11^-1,
-//   S = P11^-1 + M,  M = H^T H / R   (push-through identity; P11 = P[:12, :12])
-//   dx = K h + (K H - I) dx_new = G S^-1 v - dx_new,  v = H^T h / R + M dx_new[:12]
-// so a pass is one 12 x 12 Cholesky solve; the final pass forms
-// K H [:, :12] = G S^-1 M and P = (I - K H) P (esekfom.hpp:341-343).  P11^-1
-// and G are fixed during an update (P changes only at its end) and come from
-// the host.  Algebraically the host filter_step (slio_ikf.cpp); rounding
-// differs.
-// L.sup holds the pass's super-chunk sums on entry, except the rows in
-// load_mask, which are loaded here from sup_src (sc1 loads) in the same round
-// trip as the control block.  src is where the control block is read from:
-// the caller's mapped host block on the first pass of an update, else ctl.
-// hblk (the mapped host block) receives x, P and the flags when the update
-// ends.  All threads of the workgroup call this.
-// LDS home of control-block double e (x, xprop | P | P11i | G | dxn)
-__device__ __forceinline__ double& ctl_slot(SolveLds& L, int e) {
+// The control-block doubles a filter step reads, as one compact list:
+// x, x_prop | P | P11^-1 (D x D) | G (24 x D) | dx_new.  ctl_src gives the
+// double offset inside IkfCtl, ctl_dst the LDS home.
+template <int D>
+struct CtlList {
+  static constexpr int nX = 2 * kStateD, nP = 576, nI = D * D, nG = 24 * D, nD = 24;
+  static constexpr int total = nX + nP + nI + nG + nD;
+};
+template <int D>
+__device__ __forceinline__ int ctl_src(int e) {
+  using CL = CtlList<D>;
   constexpr int oP = (int)(offsetof(IkfCtl, P) / sizeof(double));
   constexpr int oI = (int)(offsetof(IkfCtl, P11i) / sizeof(double));
   constexpr int oG = (int)(offsetof(IkfCtl, G) / sizeof(double));
   constexpr int oD = (int)(offsetof(IkfCtl, dxn) / sizeof(double));
-  if (e < oP) return reinterpret_cast<double*>(&L.x)[e];
-  if (e < oI) return L.P[e - oP];
-  if (e < oG) return L.P11i[e - oI];
-  if (e < oD) return L.G[e - oG];
-  return L.dxn[e - oD];
+  if (e < CL::nX) return e;
+  e -= CL::nX;
+  if (e < CL::nP) return oP + e;
+  e -= CL::nP;
+  if (e < CL::nI) return oI + e;
+  e -= CL::nI;
+  if (e < CL::nG) return oG + e;
+  return oD + (e - CL::nG);
 }
-constexpr int kCtlD = (int)(offsetof(IkfCtl, converge) / sizeof(double));
+template <int D>
+__device__ __forceinline__ double& ctl_dst(StepLds& L, int e) {
+  using CL = CtlList<D>;
+  if (e < CL::nX) return reinterpret_cast<double*>(&L.x)[e];
+  e -= CL::nX;
+  if (e < CL::nP) return L.P[e];
+  e -= CL::nP;
+  if (e < CL::nI) return L.P11i[e];
+  e -= CL::nI;
+  if (e < CL::nG) return L.G[e];
+  return L.dxn[e - CL::nG];
+}
 
-template <int NT>
-__device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, double R, int i,
-                                int maxit, SolveLds& L, const double* sup_src,
-                                uint32_t load_mask, bool staged = false) {
-  static_assert(NT >= 256, "solve: at least four wavefronts");
+// One round trip: nrows doubles of pass sums (sc1 loads: written by other
+// workgroups of this launch, or plain ones written before it) into rows_lds,
+// and the control block from src into LDS (kept in HBM at ctl on the first
+// pass of an update, whose src is the caller's mapped host block).  Every
+// load is issued before the first LDS store.  All threads call it.
+template <int NT, int D, int NROWS>
+__device__ __forceinline__ void step_load(StepLds& L, double* rows_lds, const double* rows, bool rows_sc1,
+                                          const IkfCtl* src, IkfCtl* ctl) {
+  constexpr int kR = (NROWS + NT - 1) / NT;
+  constexpr int nC = CtlList<D>::total, kC = (nC + NT - 1) / NT;
   const int t = threadIdx.x;
   const bool first = src != ctl;
-  {
-    // one round trip: every load of the super rows and of the control block
-    // (unless staged) is issued before any LDS store; global-address-space
-    // pointers keep them off the flat path
-    constexpr int kRows = SLIO_NSUPER * SLIO_NPROD;
-    constexpr int kC = (kCtlD + NT - 1) / NT, kR = (kRows + NT - 1) / NT;
-    static_assert(offsetof(SolveLds, xprop) == offsetof(SolveLds, x) + sizeof(slio_state), "");
-    const gdouble* gc = (const gdouble*)(const double*)src;
-    double cv[kC], rv[kR];
+  const gdouble* gc = (const gdouble*)(const double*)src;
+  double rv[kR], cv[kC];
 #pragma unroll
-    for (int u = 0; u < kR; ++u) {
-      const int e = t + u * NT;
-      const bool on = e < kRows && sup_src && ((load_mask >> (e / SLIO_NPROD)) & 1u);
-      rv[u] = on ? ld_sc1(sup_src + e) : 0.0;
-    }
-    if (!staged) {
-#pragma unroll
-      for (int u = 0; u < kC; ++u) {
-        const int e = t + u * NT;
-        cv[u] = e < kCtlD ? gc[e] : 0.0;
-      }
-    }
-    typedef __attribute__((address_space(1))) int32_t gint;
-    const int32_t fl = (!staged && t < 8) ? ((const gint*)(const int32_t*)&src->converge)[t] : 0;
-#pragma unroll
-    for (int u = 0; u < kR; ++u) {
-      const int e = t + u * NT;
-      if (e < kRows && sup_src && ((load_mask >> (e / SLIO_NPROD)) & 1u))
-        L.sup[e / SLIO_NPROD][e % SLIO_NPROD] = rv[u];
-    }
-    // control block doubles -> LDS fields (x, xprop | P | P11i | G | dxn)
-#pragma unroll
-    for (int u = 0; u < kC; ++u) {
-      const int e = t + u * NT;
-      if (e < kCtlD) {
-        if (!staged) ctl_slot(L, e) = cv[u];
-        if (first) reinterpret_cast<double*>(ctl)[e] = staged ? ctl_slot(L, e) : cv[u];  // keep it in HBM
-      }
-    }
-    if (!staged && t < 8) L.fl[t] = fl;
-    if (first && t == 0) ctl->singular = 0;
+  for (int u = 0; u < kR; ++u) {
+    const int e = t + u * NT;
+    rv[u] = e < NROWS ? (rows_sc1 ? ld_sc1(rows + e) : ((const gdouble*)rows)[e]) : 0.0;
   }
-  __syncthreads();
-  SSTAMP(4);
-  // S, M; H^T h and m (dx_new came with the control block: the pass kernel
-  // formed it while the search ran, ikf_dx_new)
-  for (int e = t; e < 144; e += NT) {
-    const int r = e / 12, c = e - r * 12;
-    const int k = r <= c ? tri_index(r, c) : tri_index(c, r);
-    double v = L.sup[0][k];
 #pragma unroll
-    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][k];
-    const double m = v / R;
-    L.M[e] = m;
-    L.S[e] = L.P11i[e] + m;
+  for (int u = 0; u < kC; ++u) {
+    const int e = t + u * NT;
+    cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
   }
-  if (t >= 144 && t < 144 + SLIO_NPROD - SLIO_NHTH) {
-    const int k = SLIO_NHTH + t - 144;
-    double v = L.sup[0][k];
+  typedef __attribute__((address_space(1))) int32_t gint;
+  const int32_t fl = t < 8 ? ((const gint*)(const int32_t*)&src->converge)[t] : 0;
 #pragma unroll
-    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][k];
-    L.hth[t - 144] = v;
+  for (int u = 0; u < kR; ++u) {
+    const int e = t + u * NT;
+    if (e < NROWS) rows_lds[e] = rv[u];
   }
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kC; ++u) {
+    const int e = t + u * NT;
+    if (e < nC) {
+      ctl_dst<D>(L, e) = cv[u];
+      if (first) reinterpret_cast<double*>(ctl)[ctl_src<D>(e)] = cv[u];  // keep it in HBM
+    }
+  }
+  if (t < 8) L.fl[t] = fl;
+  if (first && t == 0) ctl->singular = 0;
+}
+
+// The pass's total (fixed order: super rows 0..7) and M = H^T H / R, H^T h / R
+// from L.sup; threads < 91.  Followed by a barrier in the caller.
+__device__ __forceinline__ void step_totals(StepLds& L, double R) {
+  const int t = threadIdx.x;
+  if (t < SLIO_NPROD) {
+    double v = L.sup[0][t];
+#pragma unroll
+    for (int q = 1; q < SLIO_NSUPER; ++q) v = v + L.sup[q][t];
+    L.tot[t] = v;
+    if (t < SLIO_NHTH)
+      L.Mt[t] = v / R;
+    else if (t < SLIO_NHTH + 12)
+      L.hR[t - SLIO_NHTH] = v / R;
+  }
+}
+
+// 1 / sqrt(d): hardware estimate + two Newton steps (< 1 ulp), far shorter
+// than IEEE sqrt followed by IEEE division
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double inv = __builtin_amdgcn_rsq(d);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double r = fma(-(d * inv), inv, 1.0);
+    inv = fma(0.5 * inv, r, inv);
+  }
+  return inv;
+}
+
+// x [+] dx of a rotation on the device: Sophus SO3::exp (the small-angle
+// Taylor branch of so3_exp for the IKF's increments) and the quaternion
+// product, normalised by one reciprocal square root (rsqrt_nr) instead of
+// sqrt and four divisions -- the same values to rounding, a much shorter
+// dependent chain.  Falls back to so3_exp beyond the Taylor range.
+__device__ __forceinline__ Quat qnormalized_fast(const Quat& q) {
+  const double inv = rsqrt_nr(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  return Quat{q.w * inv, q.x * inv, q.y * inv, q.z * inv};
+}
+__device__ __forceinline__ Quat so3_boxplus_dev(const Quat& q, const double om[3]) {
+  const double theta2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
+  Quat e;
+  if (theta2 >= kSmallEps * kSmallEps && theta2 < 0.0625) {  // half-angle < 0.125
+    const double u = 0.25 * theta2;
+    const double sh = 1.0 + u * (-1.0 / 6 + u * (1.0 / 120 + u * (-1.0 / 5040 + u * (1.0 / 362880 +
+                      u * (-1.0 / 39916800 + u * (1.0 / 6227020800.0))))));
+    const double real = 1.0 + u * (-0.5 + u * (1.0 / 24 + u * (-1.0 / 720 + u * (1.0 / 40320 +
+                        u * (-1.0 / 3628800 + u * (1.0 / 479001600.0))))));
+    const double imag = 0.5 * sh;
+    e = qnormalized_fast(Quat{real, imag * om[0], imag * om[1], imag * om[2]});
+  } else {
+    e = so3_exp(om);
+  }
+  return qnormalized_fast(qmul(q, e));
+}
+
+// One filter step of update_iterated_dyn_share_modified (esekfom.hpp:303-344)
+// by one workgroup of NT threads, in information form restricted to the D
+// columns H can have non-zero (6 without extrinsic estimation, 12 with):
+//   K_front[:, :D] = (P^-1 + E^T M E)^-1 E^T = G S^-1,  G = P[:, :D] P_DD^-1,
+//   S = P_DD^-1 + M,  M = H^T H / R   (push-through identity, P_DD = P[:D, :D])
+//   dx = K h + (K H - I) dx_new = G S^-1 w - dx_new,  w = H^T h / R + M dx_new[:D]
+// so a pass is one D x D Cholesky solve; the final pass forms
+// K H [:, :D] = G S^-1 M and P = (I - K H) P (esekfom.hpp:341-343).  P_DD^-1
+// and G are fixed during an update (P changes only at its end) and come from
+// the host.  Algebraically the host filter_step (slio_ikf.cpp); rounding
+// differs.  On entry L holds tot / Mt / hR (step_totals) and the control
+// block; ctl (HBM) receives the new iterate and flags, hblk (the caller's
+// mapped host block) x, P and the flags when the update ends.  All threads
+// of the workgroup call this.
+template <int NT, int D>
+__device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, int i, int maxit,
+                                         StepLds& L) {
+  static_assert(NT >= 256, "filter step: at least four wavefronts");
+  static_assert(D == 6 || D == 12, "filter step: D is 6 or 12");
+  const int t = threadIdx.x;
   SSTAMP(5);
-  const int64_t m = (int64_t)llround(L.hth[12]);
+  const int64_t m = (int64_t)llround(L.tot[SLIO_NPROD - 1]);
   const bool valid = m >= 1;
-  if (t < 64) {
-    // wave 0: the whole pass-to-pass chain, no workgroup barrier
-    bool big = false;
-    bool ok = true;
-    if (valid) {
-      double b[12];
+  // wave 0: the whole pass-to-pass chain, no workgroup barrier.  The D x D
+  // Cholesky solve runs on every lane with uniform operands (LDS broadcast
+  // reads): no cross-lane traffic on the critical path.
+  double a[D][D];  // lower triangle: S, then its factor L (rows)
+  double invd[D];
 #pragma unroll
-      for (int r = 0; r < 12; ++r) b[r] = 0.0;
-      if (t < 12) {
+  for (int r = 0; r < D; ++r) {
+    invd[r] = 0.0;
+#pragma unroll
+    for (int c = 0; c < D; ++c) a[r][c] = 0.0;
+  }
+  if (t < 64) {
+    bool ok = true, big = false;
+    if (valid) {
+#pragma unroll
+      for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) a[r][c] = L.P11i[r * D + c] + L.Mt[tri_index(c, r)];
+      double y[D];
+#pragma unroll
+      for (int r = 0; r < D; ++r) {
         double s2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) s2 = fma(L.M[t * 12 + k], L.dxn[k], s2);
-        b[0] = L.hth[t] / R + s2;  // v[t], moved to slot t below
+        for (int k = 0; k < D; ++k) s2 = fma(L.Mt[r <= k ? tri_index(r, k) : tri_index(k, r)], L.dxn[k], s2);
+        y[r] = L.hR[r] + s2;  // w
       }
-      {
-        // v as a uniform vector: v[r] from lane r
-        const double vl = b[0];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) b[r] = readlane_d(vl, r);
-      }
-      double y[12];
       SSTAMP(9);
-      ok = chol_solve_wave(L, b, y);
+      // S = L L^T, right-looking (column j scaled by 1 / L[j][j]), then
+      // L z = w, L^T y = z -- the host filter_step's order of operations
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const double d = a[j][j];
+        ok = ok && (d > 0.0);
+        const double inv = rsqrt_nr(d);
+        invd[j] = inv;
+        a[j][j] = d * inv;
+#pragma unroll
+        for (int r = j + 1; r < D; ++r) a[r][j] = a[r][j] * inv;
+#pragma unroll
+        for (int k = j + 1; k < D; ++k)
+#pragma unroll
+          for (int r = k; r < D; ++r) a[r][k] = fma(-a[r][j], a[k][j], a[r][k]);
+      }
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const double zj = y[j] * invd[j];
+        y[j] = zj;
+#pragma unroll
+        for (int r = j + 1; r < D; ++r) y[r] = fma(-a[r][j], zj, y[r]);
+      }
+#pragma unroll
+      for (int j = D - 1; j >= 0; --j) {
+        const double yj = y[j] * invd[j];
+        y[j] = yj;
+#pragma unroll
+        for (int r = 0; r < j; ++r) y[r] = fma(-a[j][r], yj, y[r]);
+      }
       SSTAMP(10);
       if (ok) {
-        // dx = G y - dx_new, |dx| > epsi (esekfom.hpp:17, 325-331)
-        bool bb = false;
-        if (t < 24) {
-          double s2 = 0.0;
+        // dx = G y - dx_new, |dx| > epsi (esekfom.hpp:17, 325-331); lanes
+        // 32 / 33 form their rotation's 3 components themselves
+        const int lane = t;
+        const int q0 = lane < 24 ? lane : (lane == 32 ? 3 : (lane == 33 ? 6 : 0));
+        const int nq = lane < 24 ? 1 : ((lane == 32 || lane == 33) ? 3 : 0);
+        double dq[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-          for (int k = 0; k < 12; ++k) s2 = fma(L.G[t * 12 + k], y[k], s2);
-          const double d = s2 - L.dxn[t];
-          L.dx[t] = d;
-          bb = fabs(d) > 0.001;
-        }
-        big = __ballot(bb) != 0;
-        wave_fence();
-        SSTAMP(11);
-        // x [+] dx (esekfom.hpp:59-73): vector blocks on lanes 0..23, the two
-        // rotations on lanes 32/33
-        if (t < 24) {
-          if (t < 3 || t >= 9) {
-            double* xs = reinterpret_cast<double*>(&L.x);
-            xs[state_off(t)] = xs[state_off(t)] + L.dx[t];
+        for (int c = 0; c < 3; ++c) {
+          if (c < nq) {
+            const int q = q0 + c;
+            double s2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) s2 = fma(L.G[q * D + k], y[k], s2);
+            dq[c] = s2 - L.dxn[q];
           }
-        } else if (t == 32 || t == 33) {
-          const int u = t - 32;
-          double* q = u ? L.x.rli : L.x.rot;
-          const Quat rq =
-              qnormalized(qmul(Quat{q[0], q[1], q[2], q[3]}, so3_exp(L.dx + 3 + 3 * u)));
+        }
+        big = __ballot(lane < 24 && fabs(dq[0]) > 0.001) != 0;
+        SSTAMP(11);
+        // x [+] dx (esekfom.hpp:59-73): vector blocks on lanes 0..23, the
+        // two rotations on lanes 32 / 33
+        if (lane < 24) {
+          if (lane < 3 || lane >= 9) {
+            double* xs = reinterpret_cast<double*>(&L.x);
+            xs[state_off(lane)] = xs[state_off(lane)] + dq[0];
+          }
+        } else if (nq == 3) {
+          double* q = lane == 33 ? L.x.rli : L.x.rot;
+          const Quat rq = so3_boxplus_dev(Quat{q[0], q[1], q[2], q[3]}, dq);
           q[0] = rq.w;
           q[1] = rq.x;
           q[2] = rq.y;
@@ -1699,6 +1745,31 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
       }
       L.s_final = fin;
     }
+    // keep the factor, M and 1 / diag of this pass for a final pass without
+    // effective points: LM = [factor (D x D) | M (upper triangle, 78) | invd]
+    if (valid && ok) {
+      const int lane = t;
+      double fv = 0.0, iv = 0.0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) {
+        iv = lane == r ? invd[r] : iv;
+#pragma unroll
+        for (int c = 0; c <= r; ++c) fv = lane == r * D + c ? a[r][c] : fv;
+      }
+      if (lane < D * D) ctl->LM[lane] = fv;
+      if (D * D > 64)
+        for (int e = lane + 64; e < D * D; e += 64) {
+          const int r = e / D, c = e - r * D;
+          double v = 0.0;
+#pragma unroll
+          for (int rr = 0; rr < D; ++rr)
+#pragma unroll
+            for (int cc = 0; cc <= rr; ++cc) v = (rr == r && cc == c) ? a[rr][cc] : v;
+          ctl->LM[e] = v;
+        }
+      for (int e = lane; e < SLIO_NHTH; e += 64) ctl->LM[144 + e] = L.Mt[e];
+      if (lane < D) ctl->LM[288 + lane] = iv;
+    }
   }
   __syncthreads();
   SSTAMP(6);
@@ -1713,52 +1784,52 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
     }
     return;
   }
-  if (valid)  // keep L and M of this pass for a final pass without effective points
-    for (int e = t; e < 300; e += NT)
-      ctl->LM[e] = e < 144 ? L.Lf[e] : (e < 288 ? L.M[e - 144] : L.invd[e - 288]);
   const bool fin = L.s_final != 0;
   constexpr int kPer = (576 + NT - 1) / NT;
   double pn[kPer];
   if (fin) {
-    // P = (I - K H) P with K H [:, :12] = G S^-1 M (esekfom.hpp:341-343)
-    if (!valid) {
-      for (int e = t; e < 288; e += NT) {
-        const double v = ctl->LM[e];
-        if (e < 144)
-          L.Lf[e] = v;
-        else
-          L.M[e - 144] = v;
+    // P = (I - K H) P with K H [:, :D] = G S^-1 M (esekfom.hpp:341-343)
+    if (t < 64) {
+      if (!valid) {
+        // the last valid pass's factor and M
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+          invd[r] = ctl->LM[288 + r];
+#pragma unroll
+          for (int c = 0; c <= r; ++c) a[r][c] = ctl->LM[r * D + c];
+        }
+        for (int e = t; e < SLIO_NHTH; e += 64) L.Mt[e] = ctl->LM[144 + e];
+        wave_fence();
       }
-      if (t < 12) L.invd[t] = ctl->LM[288 + t];
-      __syncthreads();
-    }
-    if (t < 12) {
-      // column t of Z = S^-1 M = L^-T L^-1 M
-      double zc[12];
+      if (t < D) {
+        // column t of Z = S^-1 M = L^-T L^-1 M
+        const int cc = t;
+        double zc[D];
 #pragma unroll
-      for (int j = 0; j < 12; ++j) {
-        double s2 = L.M[j * 12 + t];
+        for (int j = 0; j < D; ++j) {
+          double s2 = L.Mt[j <= cc ? tri_index(j, cc) : tri_index(cc, j)];
 #pragma unroll
-        for (int k = 0; k < j; ++k) s2 = fma(-L.Lf[j * 12 + k], zc[k], s2);
-        zc[j] = s2 * L.invd[j];
+          for (int k = 0; k < j; ++k) s2 = fma(-a[j][k], zc[k], s2);
+          zc[j] = s2 * invd[j];
+        }
+#pragma unroll
+        for (int j = D - 1; j >= 0; --j) {
+          double s2 = zc[j];
+#pragma unroll
+          for (int k = j + 1; k < D; ++k) s2 = fma(-a[k][j], zc[k], s2);
+          zc[j] = s2 * invd[j];
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) L.u.zk.Z[j * D + cc] = zc[j];
       }
-#pragma unroll
-      for (int j = 11; j >= 0; --j) {
-        double s2 = zc[j];
-#pragma unroll
-        for (int k = j + 1; k < 12; ++k) s2 = fma(-L.Lf[k * 12 + j], zc[k], s2);
-        zc[j] = s2 * L.invd[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 12; ++j) L.Z[j * 12 + t] = zc[j];
     }
     __syncthreads();
-    for (int e = t; e < 288; e += NT) {
-      const int r = e / 12, cc = e - r * 12;
+    for (int e = t; e < 24 * D; e += NT) {
+      const int r = e / D, cc = e - r * D;
       double s2 = 0.0;
 #pragma unroll
-      for (int k = 0; k < 12; ++k) s2 = fma(L.G[r * 12 + k], L.Z[k * 12 + cc], s2);
-      L.K[e] = s2;
+      for (int k = 0; k < D; ++k) s2 = fma(L.G[r * D + k], L.u.zk.Z[k * D + cc], s2);
+      L.u.zk.K[e] = s2;
     }
     __syncthreads();
 #pragma unroll
@@ -1768,7 +1839,7 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
         const int r = e / 24, cc = e - r * 24;
         double s2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) s2 = fma(L.K[r * 12 + k], L.P[k * 24 + cc], s2);
+        for (int k = 0; k < D; ++k) s2 = fma(L.u.zk.K[r * D + k], L.P[k * 24 + cc], s2);
         pn[u] = L.P[e] - s2;
         ctl->P[e] = pn[u];
       }
@@ -1784,7 +1855,6 @@ __device__ __forceinline__ void ikf_solve_block(IkfCtl* ctl, const IkfCtl* src, 
   if (t == 0) ctl->last_m = m;
   if (L.fl[F_DONE]) {
     // the update ends: x, P and the flags to the caller's mapped host block
-    // (visible to the host once the kernel has completed)
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int e = t + u * NT;
@@ -2036,6 +2106,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
     int far_cnt, ref_cnt;
+    uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
     uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
     int32_t tab_dl[NT / 16][kTab];
     float4 far_q[SLIO_CHUNK];
@@ -2061,7 +2132,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& far_slot = lds.s.far_slot;
   auto& far_pre = lds.s.far_pre;
   auto& far_beg = lds.s.far_beg;
-  const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
+  int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
+  if (cfg.perm) {
+    // (a permutation of [0, nblk) by construction; the range check only
+    // keeps a corrupt order from writing outside the chunk arrays)
+    const uint32_t pc = cfg.perm[chunk - cfg.c_begin];
+    if (pc < (uint32_t)(cfg.c_end - cfg.c_begin)) chunk = cfg.c_begin + pc;
+  }
   const int tid = threadIdx.x;
   const int sub = tid & (LPQ - 1);
   const int grp = tid / LPQ;
@@ -2072,6 +2149,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (tid == 0) {
     far_cnt = 0;
     ref_cnt = 0;
+    lds.s.cost = 0;
     if (blockIdx.x == 0 && !cfg.knn_only) *out.pose = pose;
   }
   __syncthreads();
@@ -2119,6 +2197,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
             printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
 #endif
           scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+          if (sub == 0 && out.chunk_cost) atomicAdd(&lds.s.cost, b1 - b0);
         } else {
           RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
           scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
@@ -2417,6 +2496,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
   __syncthreads();
   if (tid == 0) STAMP(2);
+  if (tid == 0 && out.chunk_cost)
+    out.chunk_cost[chunk - cfg.c_begin] = lds.s.cost + 256u * (uint32_t)ref_cnt + 1024u * (uint32_t)nfar;
   // the chunk's cell-sorted neighbour positions ([slot][5] in LDS, [i][5]
   // in HBM: one contiguous run of 5 * live words, 16-B stores).  Nearest_Points
   // ids and pointSearchSqDis are derived from them only when read
@@ -2531,139 +2612,165 @@ __global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan,
   chunk_products<SLIO_CHUNK>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
 }
 
-// Super-chunk sums in a fixed order: segment g of the 8 sums chunks c0+g,
-// c0+g+8, ... sequentially, then the 8 segment sums are added in order.  Rows
-// of super-chunks this rank does not own are written as zeros, so a SUM
-// all-reduce over ranks is an exact gather.
-// ctl != null (single-rank device-resident update): the super rows are
-// published write-through (sc1) and drained, one lane per block arrives on
-// cnt, and the block whose arrival completes the count -- told by the value
-// its add returned -- reads the other seven rows with sc1 loads and runs the
-// filter step (MI355X_MICROARCH.md, inter-workgroup visibility: first row of
-// the sc1 hand-off table).  A pass plus its filter step is two launches.
-__global__ __launch_bounds__(kSolveThreads) void k_super_sums(
-    const double* __restrict__ chunk_part, int64_t C, int s_begin, int s_end, double* super_out,
-    IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, uint32_t* cnt, double R, int iter, int maxit) {
-  constexpr int NT = kSolveThreads;
-  constexpr int KP = (kSuperSeg * SLIO_NPROD + NT - 1) / NT;  // (segment, product) pairs per thread
-  __shared__ double part[kSuperSeg * SLIO_NPROD];
-  __shared__ SolveLds L;
-  __shared__ int last;
-  const int s = blockIdx.x;
+// chunk_order: the order in which the next search pass's workgroups take
+// the chunks of XCD x's range (xcd_chunk gives each XCD a contiguous range,
+// so the map region an XCD's L2 serves does not change).  Workgroups are
+// placed round-robin (block b on CU b mod #CUs; measured: r3a stamps), so
+// local block j of the XCD runs on its CU j mod W in round j / W, and the
+// rounds share the CU.  The chunks are ranked by this pass's cost (heaviest
+// first) and dealt in snake order -- round 0 ranks 0..W-1, round 1 ranks
+// 2W-1..W, ... -- so every CU gets a similar sum of work and the 4th-round
+// blocks of a 782-chunk scan the lightest.  Speed only: every order gives
+// the same chunk partials.
+__device__ __forceinline__ void chunk_order(const uint32_t* __restrict__ cost, uint32_t* __restrict__ perm,
+                                            int64_t nblk, int x, int W, uint32_t* cs) {
+  const int64_t q = nblk >> 3, rr = nblk & 7;
+  const int64_t base = x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q;
+  const int n = (int)(q + (x < rr ? 1 : 0));
   const int t = threadIdx.x;
-  if (ctl) SSTAMP(0);
-  // the control block, in flight with the row sums' loads (used by the
-  // workgroup that runs the filter step; src is complete: written by the
-  // previous launch or by the host before this launch was enqueued)
-  constexpr int kC = (kCtlD + NT - 1) / NT;
-  double cv[kC];
-  int32_t fl = 0;
-  if (ctl) {
-    const gdouble* gc = (const gdouble*)(const double*)src;
-#pragma unroll
-    for (int u = 0; u < kC; ++u) {
-      const int e = t + u * NT;
-      cv[u] = e < kCtlD ? gc[e] : 0.0;
-    }
-    typedef __attribute__((address_space(1))) int32_t gint;
-    if (t < 8) fl = ((const gint*)(const int32_t*)&src->converge)[t];
+  if (n > (int)blockDim.x || W <= 0) {
+    for (int i = t; i < n; i += blockDim.x) perm[base + i] = (uint32_t)(base + i);
+    return;
   }
+  if (t < n) cs[t] = cost[base + t];
+  __syncthreads();
+  if (t < n) {
+    const uint32_t c = cs[t];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+      const uint32_t d = cs[j];
+      rank += (d > c || (d == c && j < t)) ? 1 : 0;
+    }
+    const int round = rank / W, k = rank - round * W;
+    const bool full = (round + 1) * W <= n;
+    const int pos = round * W + (((round & 1) && full) ? (W - 1 - k) : k);
+    perm[base + pos] = (uint32_t)(base + t);
+  }
+}
+
+// Super-chunk sums in a fixed order, one workgroup per segment row: segment
+// g of super-chunk s sums chunks c0+g, c0+g+8, ... sequentially (workgroup
+// 8 s + g, threads < 91 one product each, every chunk load in flight); the
+// last workgroup to arrive adds the 8 segments of each super-chunk in order.
+// Rows of super-chunks this rank does not own are zeros, so a SUM all-reduce
+// over ranks is an exact gather.  The segment rows are handed over
+// write-through (sc1 stores, drained before one agent-scope arrival per
+// workgroup, sc1 loads by the last; MI355X_MICROARCH.md, inter-workgroup
+// visibility).
+// D > 0 (single-rank device-resident update): the last workgroup then runs
+// the filter step (ikf_step) -- a pass plus its filter step is two launches.
+// D == 0: super rows only (host-driven passes, multi-rank all-reduce).
+template <int D>
+__global__ __launch_bounds__(kSolveThreads) void k_super_sums(
+    const double* __restrict__ chunk_part, int64_t C, int s_begin, int s_end, double* seg_out,
+    double* super_out, IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, uint32_t* cnt, double R, int iter,
+    int maxit, const uint32_t* __restrict__ cost, uint32_t* __restrict__ perm, int64_t nblk, int W) {
+  constexpr int NT = kSolveThreads;
+  __shared__ StepLds L;
+  __shared__ int arr;
+  const int b = blockIdx.x;  // segment row b = 8 s + g
+  const int s = b / kSuperSeg, g = b - s * kSuperSeg;
+  const int t = threadIdx.x;
+  if (D && b == 0) SSTAMP(0);
   // the pass kernel before this one is complete: keep its number of far
   // queries (slio_far_queries), reset the queue's head and tail
-  if (s == 0 && t == 0) {
+  if (b == 0 && t == 0) {
     st_sc1_u32(cnt + 6, ld_sc1_u32(cnt + 5));
     st_sc1_u32(cnt + 4, 0u);
     st_sc1_u32(cnt + 5, 0u);
   }
-  {
-    // pair p = g * NPROD + kk: segment g, product kk; chunk c0 + g + 8 j of
-    // pair p sits at chunk_part[(c0 + 8 j) * NPROD + p]
-    double acc[KP];
-    int64_t lim[KP];
+  if (t < SLIO_NPROD) {
     const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
     const bool mine = s >= s_begin && s < s_end;
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int p = t + k * NT;
-      const int g = p / SLIO_NPROD;
-      lim[k] = (mine && p < kSuperSeg * SLIO_NPROD) ? (c1 - c0 - g + kSuperSeg - 1) / kSuperSeg : 0;
-      acc[k] = 0.0;
-    }
-    const int64_t nj = lim[0];  // segment 0 is the longest
-    const double* base = chunk_part + c0 * SLIO_NPROD + t;
-    // the first kJ chunks of every segment in one round trip: all KP * kJ
-    // loads are issued before the first add (a pair past its last chunk
-    // adds 0); C2's 100k-point scan has <= 13 chunks per segment
-    constexpr int kJ = 16;
-    {
-      double v[KP][kJ];
+    const int64_t lim = mine ? (c1 - c0 - g + kSuperSeg - 1) / kSuperSeg : 0;
+    const double* p = chunk_part + (c0 + g) * SLIO_NPROD + t;
+    constexpr int kJ = 16;  // C2's 100k-point scan has <= 13 chunks per segment: one round trip
+    double acc = 0.0;
+    for (int64_t j0 = 0; j0 < lim; j0 += kJ) {
+      double v[kJ];
 #pragma unroll
       for (int j = 0; j < kJ; ++j)
+        v[j] = (j0 + j < lim) ? p[(j0 + j) * (kSuperSeg * SLIO_NPROD)] : 0.0;
 #pragma unroll
-        for (int k = 0; k < KP; ++k)
-          v[k][j] = j < lim[k] ? base[j * (kSuperSeg * SLIO_NPROD) + k * NT] : 0.0;
-      if (ctl) {
-#pragma unroll
-        for (int u = 0; u < kC; ++u) {
-          const int e = t + u * NT;
-          if (e < kCtlD) ctl_slot(L, e) = cv[u];
-        }
-        if (t < 8) L.fl[t] = fl;
-      }
-#pragma unroll
-      for (int j = 0; j < kJ; ++j)
-#pragma unroll
-        for (int k = 0; k < KP; ++k) acc[k] = acc[k] + v[k][j];
+      for (int j = 0; j < kJ; ++j) acc = acc + v[j];
     }
-    // longer scans: the rest, branch-free (a pair past its last chunk
-    // re-reads a valid address and adds 0)
-#pragma unroll 4
-    for (int64_t j = kJ; j < nj; ++j) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        const int64_t jj = j < lim[k] ? j : (lim[k] > 0 ? lim[k] - 1 : 0);
-        const double v = lim[k] > 0 ? base[jj * (kSuperSeg * SLIO_NPROD) + k * NT] : 0.0;
-        acc[k] = acc[k] + (j < lim[k] ? v : 0.0);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < KP; ++k)
-      if (t + k * NT < kSuperSeg * SLIO_NPROD) part[t + k * NT] = acc[k];
+    st_sc1(seg_out + b * SLIO_NPROD + t, acc);
   }
-  __syncthreads();
-  if (t < SLIO_NPROD) {
-    double v = part[t];
-#pragma unroll
-    for (int q = 1; q < kSuperSeg; ++q) v = v + part[q * SLIO_NPROD + t];
-    L.sup[s][t] = v;
-    if (ctl)
-      st_sc1(super_out + s * SLIO_NPROD + t, v);
-    else
-      super_out[s * SLIO_NPROD + t] = v;
-  }
-  if (!ctl) return;
   drain_stores();
   __syncthreads();
-  SSTAMP(1);
-  if (t == 0) last = arrive(cnt) == (uint32_t)(SLIO_NSUPER - 1);
+  if (t == 0) arr = (int)arrive(cnt);
   __syncthreads();
-  if (!last) return;
-  SSTAMP(2);
+  if (arr != kNSeg - 1) {
+    // the next search pass's chunk order of XCD x = arrival index: the
+    // first 8 to arrive (never the last) cover all 8 ranges every pass
+    if (perm && arr < 8) chunk_order(cost, perm, nblk, arr, W, reinterpret_cast<uint32_t*>(&L.u.seg[0][0]));
+    return;
+  }
+  if (D) SSTAMP(2);
   if (t == 0) reset_counter(cnt);
-  if (src == ctl && ctl->done) return;  // the first pass of an update always runs
-  SSTAMP(3);
-  ikf_solve_block<NT>(ctl, src, hblk, R, iter, maxit, L, super_out,
-                      ((1u << SLIO_NSUPER) - 1u) & ~(1u << s), true);
+  if (D) {
+    step_load<NT, D, kNSeg * SLIO_NPROD>(L, &L.u.seg[0][0], seg_out, true, src, ctl);
+  } else {
+    constexpr int kR = (kNSeg * SLIO_NPROD + NT - 1) / NT;
+    double rv[kR];
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const int e = t + u * NT;
+      rv[u] = e < kNSeg * SLIO_NPROD ? ld_sc1(seg_out + e) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const int e = t + u * NT;
+      if (e < kNSeg * SLIO_NPROD) (&L.u.seg[0][0])[e] = rv[u];
+    }
+  }
+  __syncthreads();
+  if (D) SSTAMP(4);
+  // thread k < 91: the 8 super rows of product k (independent chains) and
+  // their ordered total -- the same tree as the super rows summed by
+  // step_totals, with one barrier
+  if (t < SLIO_NPROD) {
+    double sp[SLIO_NSUPER];
+#pragma unroll
+    for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
+      double v = L.u.seg[ss * kSuperSeg][t];
+#pragma unroll
+      for (int q = 1; q < kSuperSeg; ++q) v = v + L.u.seg[ss * kSuperSeg + q][t];
+      sp[ss] = v;
+    }
+    double v = sp[0];
+#pragma unroll
+    for (int ss = 1; ss < SLIO_NSUPER; ++ss) v = v + sp[ss];
+    if constexpr (D > 0) {
+      L.tot[t] = v;
+      if (t < SLIO_NHTH)
+        L.Mt[t] = v / R;
+      else if (t < SLIO_NHTH + 12)
+        L.hR[t - SLIO_NHTH] = v / R;
+    }
+#pragma unroll
+    for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
+  }
+  if constexpr (D > 0) {
+    __syncthreads();
+    if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
+    ikf_step<NT, D>(ctl, hblk, R, iter, maxit, L);
+  }
 }
 
 // ---------------------------------------------------------------- device IKF
 // Filter step after the multi-rank all-reduce: super sums from HBM.
+template <int D>
 __global__ __launch_bounds__(kSolveThreads) void k_ikf_solve(IkfCtl* ctl, const IkfCtl* src,
                                                              IkfCtl* hblk, const double* sup,
                                                              double R, int i, int maxit) {
-  __shared__ SolveLds L;
-  if (src == ctl && ctl->done) return;
-  ikf_solve_block<kSolveThreads>(ctl, src, hblk, R, i, maxit, L, sup, (1u << SLIO_NSUPER) - 1u);
+  __shared__ StepLds L;
+  step_load<kSolveThreads, D, SLIO_NSUPER * SLIO_NPROD>(L, &L.sup[0][0], sup, false, src, ctl);
+  __syncthreads();
+  step_totals(L, R);
+  __syncthreads();
+  if (src == ctl && L.fl[F_DONE]) return;
+  ikf_step<kSolveThreads, D>(ctl, hblk, R, i, maxit, L);
 }
 
 // ---------------------------------------------------------------- context
@@ -2681,7 +2788,10 @@ struct Ctx {
   uint32_t* nbr_pos = nullptr;
   PoseDev* nbr_pose = nullptr;  // pose of the last search pass (device)
   bool nbr_lazy = false;        // nbr_idx / nbr_sqd not yet derived from nbr_pos
+  bool nbr_stale = false;       // ... and no longer derivable: another handle rebuilt the shared map
   uint64_t search_version = 0;  // map version the last search pass ran on
+  uint64_t seen_epoch = 0;      // the map's last change this handle's stream is ordered after
+  hipEvent_t map_ev = nullptr;  // recorded on this stream by another user's map change
   float* wbx = nullptr;  // scan-to-map: the scan in the map frame
   float* wby = nullptr;
   float* wbz = nullptr;
@@ -2691,9 +2801,13 @@ struct Ctx {
   uint8_t* sel = nullptr;
   float* resid = nullptr;
   double* chunk_part = nullptr;
+  uint32_t* chunk_cost = nullptr;  // per chunk of the last search pass (chunk_order)
+  uint32_t* chunk_perm = nullptr;  // search order for the next device-resident pass
+  int cus_per_xcd = 0;             // CUs per XCD (0: chunk_order off)
   // far queue (deferred queries, see far_search)
   double* d_super = nullptr;
   double* d_super_own = nullptr;
+  double* d_seg = nullptr;    // the pass's 64 segment rows (k_super_sums hand-off)
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
                               // (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
@@ -2735,6 +2849,54 @@ static void prof_drain(Ctx& c) {
       c.pool.push_back(p);
     }
     c.pending[k].clear();
+  }
+}
+
+// Map sharing: stream ordering of changes and reads (MapDev::mu held by the
+// caller: exclusively for map_write_begin / _end, either way for
+// map_read_sync).
+static int map_write_begin(Ctx& c) {
+  MapDev& m = *c.map;
+  for (Ctx* u : m.users) {
+    if (u == &c || u->stream == c.stream) continue;
+    if (!u->map_ev) SLIO_HIP(hipEventCreateWithFlags(&u->map_ev, hipEventDisableTiming));
+    SLIO_HIP(hipEventRecord(u->map_ev, u->stream));
+    SLIO_HIP(hipStreamWaitEvent(c.stream, u->map_ev, 0));
+  }
+  if (m.ready && c.seen_epoch != m.epoch) SLIO_HIP(hipStreamWaitEvent(c.stream, m.ready, 0));
+  return SLIO_OK;
+}
+static int map_write_end(Ctx& c) {
+  MapDev& m = *c.map;
+  if (!m.ready) SLIO_HIP(hipEventCreateWithFlags(&m.ready, hipEventDisableTiming));
+  SLIO_HIP(hipEventRecord(m.ready, c.stream));
+  c.seen_epoch = ++m.epoch;
+  return SLIO_OK;
+}
+static int map_read_sync(Ctx& c) {
+  MapDev& m = *c.map;
+  if (c.seen_epoch != m.epoch) {
+    if (m.ready) SLIO_HIP(hipStreamWaitEvent(c.stream, m.ready, 0));
+    c.seen_epoch = m.epoch;
+  }
+  if (m.broken) {
+    set_error("slio map: an index rebuild failed part-way; upload the map again");
+    return SLIO_EDEVICE;
+  }
+  return SLIO_OK;
+}
+// attach c to map m (nullptr: detach), keeping the users list
+static void map_attach(Ctx& c, std::shared_ptr<MapDev> m) {
+  if (c.map) {
+    std::unique_lock<std::shared_mutex> lk(c.map->mu);
+    auto& u = c.map->users;
+    u.erase(std::remove(u.begin(), u.end(), &c), u.end());
+  }
+  c.map = std::move(m);
+  c.seen_epoch = 0;  // the new map's last change is not yet waited for
+  if (c.map) {
+    std::unique_lock<std::shared_mutex> lk(c.map->mu);
+    c.map->users.push_back(&c);
   }
 }
 
@@ -2800,6 +2962,9 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->sel);
   (void)hipFree(c->resid);
   (void)hipFree(c->chunk_part);
+  (void)hipFree(c->chunk_cost);
+  (void)hipFree(c->chunk_perm);
+  c->chunk_cost = c->chunk_perm = nullptr;
   c->bx = c->by = c->bz = nullptr;
   c->nbr_idx = nullptr;
   c->nbr_sqd = nullptr;
@@ -2854,6 +3019,7 @@ static hipError_t wait_published(Ctx& c) {
 // Fused filter step of a single-rank device-resident update.
 struct SolveArgs {
   int on;        // run the filter step in the super-sum kernel (single rank)
+  int dim;       // D of the filter step: 6 without extrinsic estimation, 12 with
   int pass_idx;  // ctl->passes this pass belongs to
   int iter, maxit;
   double R;
@@ -2863,6 +3029,8 @@ struct SolveArgs {
 
 static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa);
 static int map_refresh(Ctx& c, bool adds_only = false);
+static int map_refresh_locked(Ctx& c, bool adds_only);
+static int nbr_settle_shared(Ctx& c);
 static int build_blk(MapDev& m, hipStream_t st, const char* who);
 
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
@@ -2901,11 +3069,25 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   cfg.knn_only = knn_only ? 1 : 0;
+  // later passes of a device-resident update take their chunks in the order
+  // the previous pass's costs call for (chunk_order; pass 0 in index order)
+  static const bool no_order = std::getenv("SLIO_NO_CHUNK_ORDER") != nullptr;
+  cfg.perm = (devpose && c.cus_per_xcd > 0 && !no_order) ? c.chunk_perm : nullptr;
   if (int rc = map_refresh(c); rc) return rc;
-  if (which != 0 && c.map->blk_deferred && ++c.map->stable_passes > kBlkAfterPasses)
-    if (int rc = build_blk(*c.map, c.stream, "slio map"); rc) return rc;
-  PassOut o{c.nbr_idx,    c.nbr_pos, c.nbr_sqd, c.plane,   c.sel,
-            c.resid,      c.chunk_part, c.count + 4, c.nbr_pose};
+  if (which != 0 && c.map->blk_deferred) {
+    std::unique_lock<std::shared_mutex> lk(c.map->mu);
+    if (c.map->blk_deferred && ++c.map->stable_passes > kBlkAfterPasses) {
+      if (int rc = map_write_begin(c)) return rc;
+      if (int rc = build_blk(*c.map, c.stream, "slio map"); rc) return rc;
+      if (int rc = map_write_end(c)) return rc;
+    }
+  }
+  // the views are read and the kernels launched under the shared lock: a
+  // change by another handle waits for these launches (map_write_begin)
+  std::shared_lock<std::shared_mutex> map_lock(c.map->mu);
+  if (int rc = map_read_sync(c)) return rc;
+  PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,   c.sel,
+            c.resid,      c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
@@ -2952,6 +3134,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
 #undef SLIO_LAUNCH2
 #undef SLIO_LAUNCH
     c.nbr_lazy = !knn_only;
+    c.nbr_stale = false;
   }
   if (nblk > 0 && run_reuse) {
     const auto ev = timing(SLIO_KERNEL_REUSE);
@@ -2980,6 +3163,12 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
 static int nbr_settle(Ctx& c) {
   if (!c.nbr_lazy) return SLIO_OK;
   c.nbr_lazy = false;
+  // another handle sharing the map rebuilt it since this handle's last
+  // search pass: the stored positions point into moved points
+  if (!c.map || c.search_version != c.map->version) {
+    c.nbr_stale = true;
+    return SLIO_OK;
+  }
   int64_t c0, c1;
   rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
   const int64_t b = c0 * SLIO_CHUNK, e = std::min(c1 * SLIO_CHUNK, c.n);
@@ -2991,10 +3180,22 @@ static int nbr_settle(Ctx& c) {
   return SLIO_OK;
 }
 
+// nbr_settle from outside any map lock (before the handle's scan or map is
+// replaced, or its neighbours are read)
+static int nbr_settle_shared(Ctx& c) {
+  if (!c.nbr_lazy) return SLIO_OK;
+  if (!c.map) return nbr_settle(c);
+  std::shared_lock<std::shared_mutex> lk(c.map->mu);
+  if (int rc = map_read_sync(c)) return rc;
+  return nbr_settle(c);
+}
+
 // Super-chunk sums of the pass just enqueued (+ the filter step of a
 // single-rank device-resident update).
 static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa) {
   const int64_t C = num_chunks(c.n);
+  int64_t c0, c1;
+  rank_chunks(c.n, c.prm.rank, c.prm.nranks, &c0, &c1);
   const int per = SLIO_NSUPER / c.prm.nranks;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (c.prof && (c.prof_mask & (1 << SLIO_KERNEL_SUPER))) {
@@ -3002,12 +3203,13 @@ static void enqueue_super(Ctx& c, IkfCtl* ctl, const SolveArgs* sa) {
     c.pending[SLIO_KERNEL_SUPER].push_back(ev);
   }
   const bool fuse = sa && sa->on;
-  hipExtLaunchKernelGGL(k_super_sums, dim3(SLIO_NSUPER), dim3(kSolveThreads), 0, c.stream,
-                        ev.first, ev.second, 0, (const double*)c.chunk_part, C,
-                        c.prm.rank * per, (c.prm.rank + 1) * per, c.d_super,
-                        fuse ? ctl : (IkfCtl*)nullptr, fuse ? sa->src : (const IkfCtl*)nullptr,
-                        fuse ? sa->hblk : (IkfCtl*)nullptr, c.count, fuse ? sa->R : 0.0,
-                        fuse ? sa->iter : 0, fuse ? sa->maxit : 0);
+  const auto kern = !fuse ? k_super_sums<0> : (sa->dim == 12 ? k_super_sums<12> : k_super_sums<6>);
+  hipExtLaunchKernelGGL(kern, dim3(kNSeg), dim3(kSolveThreads), 0, c.stream, ev.first, ev.second, 0,
+                        (const double*)c.chunk_part, C, c.prm.rank * per, (c.prm.rank + 1) * per,
+                        c.d_seg, c.d_super, fuse ? ctl : (IkfCtl*)nullptr,
+                        fuse ? sa->src : (const IkfCtl*)nullptr, fuse ? sa->hblk : (IkfCtl*)nullptr,
+                        c.count, fuse ? sa->R : 0.0, fuse ? sa->iter : 0, fuse ? sa->maxit : 0,
+                        (const uint32_t*)c.chunk_cost, c.chunk_perm, c1 - c0, c.cus_per_xcd);
 }
 
 }  // namespace slio
@@ -3120,7 +3322,14 @@ int slio_create(slio_handle* out, const slio_params* p) {
     return SLIO_EDEVICE;
   }
   h->c.stream = h->c.own_stream;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess &&
+        ncu > 0 && ncu % 8 == 0)
+      h->c.cus_per_xcd = ncu / 8;
+  }
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
+      hipMalloc(&h->c.d_seg, sizeof(double) * kNSeg * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.count, sizeof(uint32_t) * 16) != hipSuccess ||
       hipMemset(h->c.count, 0, sizeof(uint32_t) * 16) != hipSuccess) {
@@ -3144,12 +3353,14 @@ int slio_destroy(slio_handle h) {
     (void)hipEventDestroy(p.second);
   }
   (void)hipFree(h->c.d_super_own);
+  (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
   (void)hipFree(h->c.ctl);
   (void)hipHostFree(h->c.h_ctl);
   if (h->c.done_ev) (void)hipEventDestroy(h->c.done_ev);
   (void)hipHostFree(h->c.h_super);
-  h->c.map.reset();
+  map_attach(h->c, nullptr);
+  if (h->c.map_ev) (void)hipEventDestroy(h->c.map_ev);
   if (h->c.own_stream) (void)hipStreamDestroy(h->c.own_stream);
   delete h;
   return SLIO_OK;
@@ -3261,6 +3472,11 @@ __global__ void k_bbox4(const float4* __restrict__ in, int64_t n, int32_t* __res
     for (int q = 0; q < (int)(blockDim.x >> 6); ++q) b |= wb[q];
     if (b) atomicOr(out + 6, 1);
   }
+}
+
+__global__ void k_iota_u32(uint32_t* __restrict__ p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (uint32_t)i;
 }
 
 __global__ void k_fill_u8(uint8_t* __restrict__ p, int64_t n, uint8_t v) {
@@ -3546,11 +3762,14 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.nbr_pos, 4 * 5 * cap)) || (e = hipMalloc(&c.nbr_pose, sizeof(PoseDev))) ||
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
-        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc))) {
+        (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
+        (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));
       return SLIO_ENOMEM;
     }
+    k_iota_u32<<<grid_blocks(capc), 256, 0, c.stream>>>(c.chunk_perm, capc);
+    SLIO_HIP(hipMemsetAsync(c.chunk_cost, 0, 4 * capc, c.stream));
   }
   return SLIO_OK;
 }
@@ -3873,10 +4092,22 @@ static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream
   *total = 0;
   if (n == 0) return SLIO_OK;
   size_t tb = 0;
-  // scan temporaries cached per host thread (no hipMalloc / hipFree per call)
-  static thread_local void* tmp = nullptr;
-  static thread_local size_t tcap = 0;
+  // scan temporaries cached per host thread AND device (no hipMalloc /
+  // hipFree per call; one thread may drive handles on several GPUs, and a
+  // device must never be handed another device's buffer).  The call ends
+  // with a stream synchronisation, so one buffer per (thread, device) is
+  // never in use by two scans at once.
+  constexpr int kMaxDev = 64;
+  static thread_local void* tmps[kMaxDev] = {};
+  static thread_local size_t tcaps[kMaxDev] = {};
+  int dev = 0;
   hipError_t e;
+  if ((e = hipGetDevice(&dev)) || dev < 0 || dev >= kMaxDev) {
+    set_error("slio map: scan: no current device");
+    return SLIO_EDEVICE;
+  }
+  void*& tmp = tmps[dev];
+  size_t& tcap = tcaps[dev];
   if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, rank, (int)n, st))) {
     set_error(std::string("slio map: scan: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
@@ -3960,7 +4191,7 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     return SLIO_OK;
   }
   // the box searches need every stored point in the index
-  if (int rc = map_refresh(c, true)) return rc;
+  if (int rc = map_refresh_locked(c, true)) return rc;
   uint64_t *k0 = nullptr, *k1 = nullptr;
   uint32_t *v0 = nullptr, *v1 = nullptr, *surv = nullptr, *rank = nullptr;
   unsigned long long* dcount = nullptr;
@@ -4021,6 +4252,19 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
 // were added (deletions alone are honoured through the keep flags).
 static int map_refresh(Ctx& c, bool adds_only) {
   if (!c.map || !c.map->dirty) return SLIO_OK;
+  std::unique_lock<std::shared_mutex> lk(c.map->mu);
+  if (!c.map->dirty) return SLIO_OK;  // another user rebuilt it meanwhile
+  if (int rc = map_read_sync(c)) return rc;
+  if (int rc = map_write_begin(c)) return rc;
+  const int rc = map_refresh_locked(c, adds_only);
+  const int rc2 = map_write_end(c);
+  return rc ? rc : rc2;
+}
+
+// the rebuild itself: MapDev::mu held exclusively, the stream ordered after
+// the other users (map_write_begin)
+static int map_refresh_locked(Ctx& c, bool adds_only) {
+  if (!c.map || !c.map->dirty) return SLIO_OK;
   MapDev& m = *c.map;
   if (adds_only && m.nadd == 0) return SLIO_OK;
   if (int rc = nbr_settle(c)) return rc;  // the rebuild moves the points
@@ -4072,6 +4316,12 @@ static int map_refresh(Ctx& c, bool adds_only) {
   m.free_index();
   m.nadd = 0;
   const int rc = build_index(m, in4, n, mn, mx, st, "slio map rebuild", false, true, had_points);
+  if (rc) {
+    // part-way: the stored points are gone from the views; fail every later
+    // use of the map instead of searching a partial index
+    m.broken = true;
+    m.free_index();
+  }
   m.version++;
   m.dirty = false;
   return rc;
@@ -4133,8 +4383,15 @@ int slio_map_upload(slio_handle h, const float* x, const float* y, const float* 
   for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)in4})
     if (q) (void)hipFree(q);
   if (rc) return rc;
-  if ((rc = nbr_settle(h->c))) return rc;
-  h->c.map = m;
+  {
+    // sharers of this map order their streams after its build
+    SLIO_HIP(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+    SLIO_HIP(hipEventRecord(m->ready, st));
+    m->epoch = 1;
+  }
+  if ((rc = nbr_settle_shared(h->c))) return rc;
+  map_attach(h->c, m);
+  h->c.seen_epoch = 1;
   h->c.searched = false;
   return SLIO_OK;
 }
@@ -4145,8 +4402,9 @@ int slio_map_share(slio_handle h, slio_handle src) {
     set_error("slio_map_share: source has no map on this device");
     return SLIO_EINVAL;
   }
-  if (int rc = nbr_settle(h->c)) return rc;
-  h->c.map = src->c.map;
+  if (h == src) return SLIO_OK;
+  if (int rc = nbr_settle_shared(h->c)) return rc;
+  map_attach(h->c, src->c.map);
   h->c.searched = false;
   return SLIO_OK;
 }
@@ -4158,6 +4416,7 @@ int slio_map_info(slio_handle h, int32_t dims[3], float* cell, int64_t* n) {
     return SLIO_ESTATE;
   }
   if (int rc = map_refresh(h->c)) return rc;
+  std::shared_lock<std::shared_mutex> lk(h->c.map->mu);
   if (dims) {
     dims[0] = h->c.map->g.dx;
     dims[1] = h->c.map->g.dy;
@@ -4187,6 +4446,9 @@ int slio_map_add_points(slio_handle h, const float* x, const float* y, const flo
     }
   int64_t cnt = 0;
   if (n > 0) {
+    std::unique_lock<std::shared_mutex> lk(c.map->mu);
+    if (int rc = map_read_sync(c)) return rc;
+    if (int rc = map_write_begin(c)) return rc;
     float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr;
     float4* in4 = nullptr;
     int rc = SLIO_OK;
@@ -4205,6 +4467,7 @@ int slio_map_add_points(slio_handle h, const float* x, const float* y, const flo
       rc = map_add(c, in4, n, downsample != 0, downsample_size, &cnt);
       if (!rc) (void)hipStreamSynchronize(c.stream);
     }
+    if (int rc2 = map_write_end(c); rc2 && !rc) rc = rc2;
     for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)in4})
       if (q) (void)hipFree(q);
     if (rc) return rc;
@@ -4225,6 +4488,9 @@ int slio_map_delete_boxes(slio_handle h, const float* boxes, int64_t nboxes, int
     return SLIO_EINVAL;
   }
   MapDev& m = *c.map;
+  std::unique_lock<std::shared_mutex> lk(m.mu);
+  if (int rc = map_read_sync(c)) return rc;
+  if (int rc = map_write_begin(c)) return rc;
   unsigned long long* dc = nullptr;
   SLIO_HIP(hipMalloc(&dc, 8));
   SLIO_HIP(hipMemsetAsync(dc, 0, 8, c.stream));
@@ -4246,7 +4512,7 @@ int slio_map_delete_boxes(slio_handle h, const float* boxes, int64_t nboxes, int
   }
   if (k) m.dirty = true;
   if (deleted) *deleted = (int64_t)k;
-  return SLIO_OK;
+  return map_write_end(c);
 }
 
 int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_map_min, int ekf_inited,
@@ -4257,10 +4523,17 @@ int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_
     set_error("slio_map_incremental: bad arguments");
     return SLIO_EINVAL;
   }
-  if (!c.map || !c.searched || c.search_version != c.map->version) {
+  if (!c.map) {
+    set_error("slio_map_incremental: no map");
+    return SLIO_ESTATE;
+  }
+  std::unique_lock<std::shared_mutex> map_lock(c.map->mu);
+  if (!c.searched || c.search_version != c.map->version) {
     set_error("slio_map_incremental: no search pass on the current map (Nearest_Points)");
     return SLIO_ESTATE;
   }
+  if (int rc = map_read_sync(c)) return rc;
+  if (int rc = map_write_begin(c)) return rc;
   if (c.prm.nranks != 1) {
     set_error("slio_map_incremental: needs the whole scan (nranks == 1)");
     return SLIO_EINVAL;
@@ -4323,6 +4596,7 @@ int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_
     } while (0);
     for (void* q : {(void*)w4, (void*)l1, (void*)l2, (void*)fa, (void*)fn, (void*)ra, (void*)rn})
       if (q) (void)hipFree(q);
+    if (int rc2 = map_write_end(c); rc2 && !rc) rc = rc2;
     if (rc) return rc;
   }
   if (counts)
@@ -4338,6 +4612,8 @@ int slio_map_download(slio_handle h, float* x, float* y, float* z, uint32_t* ids
     return SLIO_ESTATE;
   }
   if (int rc = map_refresh(c)) return rc;
+  std::shared_lock<std::shared_mutex> lk(c.map->mu);
+  if (int rc = map_read_sync(c)) return rc;
   const MapDev& m = *c.map;
   if (n) *n = m.n;
   if (cap < m.n || (m.n > 0 && (!x || !y || !z || !ids))) {
@@ -4345,7 +4621,10 @@ int slio_map_download(slio_handle h, float* x, float* y, float* z, uint32_t* ids
     return SLIO_ECAPACITY;
   }
   std::vector<float4> buf((size_t)m.n);
-  if (m.n) SLIO_HIP(hipMemcpy(buf.data(), m.pts, 16 * m.n, hipMemcpyDeviceToHost));
+  if (m.n) {
+    SLIO_HIP(hipMemcpyAsync(buf.data(), m.pts, 16 * m.n, hipMemcpyDeviceToHost, c.stream));
+    SLIO_HIP(hipStreamSynchronize(c.stream));
+  }
   std::vector<std::pair<uint32_t, uint32_t>> order((size_t)m.n);
   for (int64_t i = 0; i < m.n; ++i) {
     uint32_t id;
@@ -4432,7 +4711,7 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
   uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *hd = nullptr, *rk = nullptr;
   int32_t* bb = nullptr;
   void* tmp = nullptr;
-  int rc = nbr_settle(c);  // the scan it was searched with is replaced
+  int rc = nbr_settle_shared(c);  // the scan it was searched with is replaced
   if (rc) return rc;
   int64_t m = 0;
   bool passthrough = false;
@@ -4852,6 +5131,8 @@ int slio_s2m_coeffs(slio_handle h, int kind, const float transform[6], int64_t* 
     const PoseDev P = make_pose(&idp);
     const ScanDev sd{c.wbx, c.wby, c.wbz, n};
     if (int rc = enqueue_pass(c, &P, nullptr, 1, 0, nullptr, false, true, &sd)) return rc;
+    std::shared_lock<std::shared_mutex> lk(c.map->mu);
+    if (int rc = map_read_sync(c)) return rc;
     if (kind == 0)
       k_s2m_coeff<0><<<grid_blocks(n), 256, 0, c.stream>>>(c.wbx, c.wby, c.wbz, n, c.nbr_pos, c.nbr_sqd,
                                                             c.map->pts, c.plane, c.sel);
@@ -5177,7 +5458,7 @@ int slio_scan_upload(slio_handle h, const float* x, const float* y, const float*
     set_error("slio_scan_upload: scan exceeds max_points");
     return SLIO_ECAPACITY;
   }
-  if (int rc = nbr_settle(c)) return rc;  // the scan it was searched with is replaced
+  if (int rc = nbr_settle_shared(c)) return rc;  // the scan it was searched with is replaced
   if (int rc = ensure_scan_buffers(c)) return rc;
   c.n = n;
   if (n > 0) {
@@ -5248,6 +5529,9 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   // the bus (then keeps it in HBM); the step that ends the update writes x,
   // P and the flags back.  No copy-engine work on the path.
   const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
+  // H's columns 6..11 are zero without extrinsic estimation (esekfom.hpp:218-220):
+  // the filter step works on the first 6 error-state components
+  const int dim = extrinsic_est ? 12 : 6;
   const PoseDev pose0 = [&] {
     slio_pose p;
     std::memcpy(p.rot, x->rot, sizeof(p.rot));
@@ -5261,7 +5545,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     // multi-rank: pass -> all-reduce of the super sums -> k_ikf_solve
     const bool p0 = i == first;
     const IkfCtl* src = p0 ? (const IkfCtl*)c.d_hctl : c.ctl;
-    const SolveArgs sa{reduce ? 0 : 1, i - first, i, maximum_iter, R, src, c.d_hctl};
+    const SolveArgs sa{reduce ? 0 : 1, dim, i - first, i, maximum_iter, R, src, c.d_hctl};
     // pass 0 always searches (converge starts true, esekfom.hpp:282)
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
     int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, extrinsic_est, &sa, !p0 || reduce);
@@ -5270,7 +5554,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
       // information-form constants of the update (P is fixed until its end),
       // formed on the host while pass 0's search runs; pass 0's filter step
       // reads them from the mapped block
-      if (!info_constants(P, hc.P11i, hc.G)) {
+      if (!info_constants(P, dim, hc.P11i, hc.G)) {
         (void)hipStreamSynchronize(c.stream);
         set_error("slio_ikf_update_device: singular covariance block P[:12, :12]");
         return SLIO_EINVAL;
@@ -5283,8 +5567,12 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
         set_error("slio_ikf_update_device: reduce callback failed");
         return SLIO_EDEVICE;
       }
-      k_ikf_solve<<<1, kSolveThreads, 0, c.stream>>>(c.ctl, src, c.d_hctl, c.d_super, R, i,
-                                                     maximum_iter);
+      if (dim == 12)
+        k_ikf_solve<12><<<1, kSolveThreads, 0, c.stream>>>(c.ctl, src, c.d_hctl, c.d_super, R, i,
+                                                         maximum_iter);
+      else
+        k_ikf_solve<6><<<1, kSolveThreads, 0, c.stream>>>(c.ctl, src, c.d_hctl, c.d_super, R, i,
+                                                        maximum_iter);
     }
   }
   SLIO_HIP(hipGetLastError());
@@ -5386,7 +5674,12 @@ int slio_get_neighbors(slio_handle h, int32_t* idx, float* sqd, uint8_t* sel) {
   int64_t b, e;
   slio_shard_range(h, &b, &e);
   const int64_t n = e - b;
-  if (int rc = nbr_settle(c)) return rc;
+  if (int rc = nbr_settle_shared(c)) return rc;
+  if (c.nbr_stale) {
+    set_error("slio_get_neighbors: another handle sharing the map rebuilt it after this handle's last "
+              "search pass; run a search pass again");
+    return SLIO_ESTATE;
+  }
   SLIO_HIP(hipStreamSynchronize(c.stream));
   if (n <= 0) return SLIO_OK;
   if (idx) SLIO_HIP(hipMemcpy(idx, c.nbr_idx + b * 5, 4 * 5 * n, hipMemcpyDeviceToHost));

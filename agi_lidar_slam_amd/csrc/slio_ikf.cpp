@@ -175,19 +175,22 @@ void covariance_update(double* P, const double K12[288]) {
 
 }  // namespace
 
-// Information-form constants of one update (P_ is fixed until its end):
-// P11^-1 = (P[:12, :12])^-1 and G = P[:, :12] P11^-1.  The device-resident
-// update (slio_ikf_update_device) uses exactly these.
-bool slio::info_constants(const double* P, double P11i[144], double G[288]) {
-  double P11[144];
-  for (int r = 0; r < 12; ++r)
-    for (int q = 0; q < 12; ++q) P11[r * 12 + q] = P[r * 24 + q];
-  if (!invert<12>(P11, P11i)) return false;
+// Information-form constants of one update (P_ is fixed until its end) on
+// the first D error-state components (D = 12, or 6 when H's columns 6..11
+// are zero): P_DD^-1 = (P[:D, :D])^-1 (D x D) and G = P[:, :D] P_DD^-1
+// (24 x D), both row-major and packed.  The device-resident update
+// (slio_ikf_update_device) uses exactly these.
+bool slio::info_constants(const double* P, int D, double P11i[144], double G[288]) {
+  if (D != 6 && D != 12) return false;
+  double PDD[144];
+  for (int r = 0; r < D; ++r)
+    for (int q = 0; q < D; ++q) PDD[r * D + q] = P[r * 24 + q];
+  if (!(D == 12 ? invert<12>(PDD, P11i) : invert<6>(PDD, P11i))) return false;
   for (int r = 0; r < 24; ++r)
-    for (int q = 0; q < 12; ++q) {
+    for (int q = 0; q < D; ++q) {
       double v = 0.0;
-      for (int k = 0; k < 12; ++k) v += P[r * 24 + k] * P11i[k * 12 + q];
-      G[r * 12 + q] = v;
+      for (int k = 0; k < D; ++k) v += P[r * 24 + k] * P11i[k * D + q];
+      G[r * D + q] = v;
     }
   return true;
 }
@@ -224,7 +227,7 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R, int m
   double K12[288];
   double dx[24];
   double P11i[144], G[288];
-  if (!info_constants(P, P11i, G)) {
+  if (!info_constants(P, 12, P11i, G)) {
     set_error("slio_ikf_update: singular covariance block P[:12, :12]");
     return SLIO_EINVAL;
   }

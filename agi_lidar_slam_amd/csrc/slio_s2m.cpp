@@ -5,6 +5,7 @@
 // OpenCV (cv::solve DECOMP_QR, cv::eigen, cv::Mat::inv) is third-party and
 // absent; its algorithms are restated in float: Householder QR, the Jacobi
 // eigensolver of hal::Jacobi, LU inverse with partial pivoting.
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 
@@ -125,7 +126,9 @@ void jacobi(float* A, int n, float* W, float* V) {
   }
 }
 
-// A x = b (6x6, float) by Householder QR
+// A x = b (6x6, float) by Householder QR.  false where OpenCV's QRImpl gives
+// up (cv::solve DECOMP_QR -> hal::QR32f with eps = 10 * FLT_EPSILON: a
+// diagonal entry of R below eps in magnitude)
 bool qr_solve6(const float* A_in, const float* b_in, float* x) {
   float A[36], b[6];
   std::memcpy(A, A_in, sizeof A);
@@ -156,7 +159,7 @@ bool qr_solve6(const float* A_in, const float* b_in, float* x) {
   for (int i = 5; i >= 0; --i) {
     float s = b[i];
     for (int j = i + 1; j < 6; ++j) s -= A[6 * i + j] * x[j];
-    if (A[6 * i + i] == 0) return false;
+    if (std::fabs(A[6 * i + i]) < 10.0f * FLT_EPSILON) return false;
     x[i] = s / A[6 * i + i];
   }
   return true;
@@ -203,10 +206,11 @@ extern "C" int slio_s2m_lm_step(const float AtA[36], const float AtB[6], int64_t
   *converged = 0;
   if (nsel < 50) return 1;  // :1573-1576: too few correspondences, no update
   float X[6];
-  if (!qr_solve6(AtA, AtB, X)) {
-    set_error("slio_s2m_lm_step: singular normal equations");
-    return SLIO_EINVAL;
-  }
+  // cv::solve(matAtA, matAtB, matX, DECOMP_QR) (:1620): on a (numerically)
+  // singular A^T A it returns false with matX zeroed, and LMOptimization
+  // ignores the return value -- a zero step, which then reads as converged
+  if (!qr_solve6(AtA, AtB, X))
+    for (float& v : X) v = 0.0f;
   if (iter_count == 0) {
     // :1633-1656: eigen-decomposition of A^T A; directions with eigenvalue
     // < 100 (smallest first) are not updated

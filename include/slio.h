@@ -385,7 +385,11 @@ int slio_s2m_normal_equations(slio_handle h_corner, slio_handle h_surf,
  * iteration 0 the degeneracy projection matP (eigenvalues < 100) is formed,
  * later iterations reuse it; transform += X; *converged = deltaR < 0.05 deg
  * and deltaT < 0.05 cm.  Returns 1 (nothing done) with fewer than 50
- * correspondences, as the reference's `return false`. */
+ * correspondences, as the reference's `return false`.  A (numerically)
+ * singular A^T A -- an R diagonal below 10 * FLT_EPSILON in the QR, where
+ * cv::solve(DECOMP_QR) gives up and zeroes matX -- is a zero step (then
+ * converged), not an error, as in the reference, which ignores cv::solve's
+ * result. */
 int slio_s2m_lm_step(const float AtA[36], const float AtB[6], int64_t nsel, int iter_count,
                      float transform[6], int* is_degenerate, float matP[36], int* converged);
 

@@ -630,10 +630,11 @@ int64_t h_share_model(const Tree& T, const State& x, PassIO& io, bool do_search,
       row[0] = nv[0];
       row[1] = nv[1];
       row[2] = nv[2];
+      // esekfom.hpp:213-221: [n, A, B, C] with extrinsic_est, [n, A, 0 x 6] without
       for (int k = 0; k < 3; ++k) {
         row[3 + k] = A[k];
         row[6 + k] = B[k];
-        row[9 + k] = C[k];
+        row[9 + k] = extrinsic ? C[k] : 0.0;
       }
       (*hv)[r] = -(double)io.resid[i];
       ++r;

@@ -20,7 +20,7 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         pose = L.SlioPose()
         pose.pos[:] = list(st[0:3]); pose.rot[:] = list(st[3:7])
         pose.rli[:] = list(st[7:11]); pose.tli[:] = list(st[11:14])
-        p = L.SlioParams(); lib.slio_params_default(C.byref(p)); p.grid_cell = 1.25; p.lanes_per_query = lpq
+        p = L.SlioParams(); lib.slio_params_default(C.byref(p)); p.grid_cell = float(os.environ.get("STAMP_CELL", "0")); p.lanes_per_query = lpq
         h = C.c_void_p(); L.check(lib.slio_create(C.byref(h), C.byref(p)), "create")
         x, y, z = (np.ascontiguousarray(mp[:, k]) for k in range(3))
         L.check(lib.slio_map_upload(h, L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")

@@ -153,3 +153,33 @@ def test_library_built_from_these_sources(lib):
     by __graft_entry__.build()."""
     from agi_lidar_slam_amd import build
     assert lib.slio_build_id().decode() == build.source_hash()
+
+
+def test_s2m_lm_step_singular_is_a_zero_step(lib):
+    """LIO-SAM LMOptimization (mapOptmization.cpp:1620): cv::solve(DECOMP_QR)
+    gives up on an R diagonal below 10 * FLT_EPSILON, zeroes matX, and the
+    caller ignores the result -- a zero step that reads as converged, not an
+    abort.  A well-conditioned system still solves."""
+    from agi_lidar_slam_amd import _lib as L
+    f32 = lambda a: np.ascontiguousarray(a, dtype=np.float32)
+    fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+    for AtA in (np.zeros((6, 6)), np.diag([1.0, 1, 1, 1, 1, 0]),
+                np.diag([1.0, 1, 1, 1, 1, 1e-9])):
+        AtA, AtB = f32(AtA), f32(np.arange(1, 7))
+        tf = f32(np.array([0.1, 0.2, 0.3, 1.0, 2.0, 3.0]))
+        tf0 = tf.copy()
+        deg, conv = C.c_int(0), C.c_int(0)
+        matP = f32(np.zeros((6, 6)))
+        rc = lib.slio_s2m_lm_step(fp(AtA), fp(AtB), 100, 1, fp(tf), C.byref(deg), fp(matP), C.byref(conv))
+        assert rc == 0, L.last_error() if hasattr(L, "last_error") else rc
+        np.testing.assert_array_equal(tf, tf0)
+        assert conv.value == 1
+    # regular system: transform moves by the solution
+    A = np.diag([1e3, 2e3, 3e3, 4e3, 5e3, 6e3])
+    b = np.array([1.0, 2, 3, 4, 5, 6]) * 1e-3
+    AtA, AtB = f32(A), f32(b)
+    tf = f32(np.zeros(6))
+    deg, conv = C.c_int(0), C.c_int(0)
+    matP = f32(np.zeros((6, 6)))
+    assert lib.slio_s2m_lm_step(fp(AtA), fp(AtB), 100, 1, fp(tf), C.byref(deg), fp(matP), C.byref(conv)) == 0
+    np.testing.assert_allclose(tf, np.linalg.solve(A, b), rtol=1e-5)
