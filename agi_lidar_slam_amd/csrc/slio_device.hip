@@ -40,9 +40,11 @@
 // builds only; read with slio_dbg_solve_stamps).
 #ifdef SLIO_SOLVE_STAMP
 __device__ unsigned long long g_sstamp[32];
-#define SSTAMP(k)                                     \
-  do {                                                \
+#define SSTAMP(k)                                       \
+  do {                                                  \
+    __builtin_amdgcn_sched_barrier(0);                  \
     if (threadIdx.x == 0) g_sstamp[k] = wall_clock64(); \
+    __builtin_amdgcn_sched_barrier(0);                  \
   } while (0)
 #else
 #define SSTAMP(k) \
@@ -561,6 +563,38 @@ struct PoseDev {
   double R[9];                          // rot.matrix(), row-major
   double RL[9];                         // offset_R_L_I.matrix(), row-major
 };
+
+static_assert(sizeof(PoseDev) == 32 * sizeof(double), "PoseDev: 32 doubles (IkfCtl::pose)");
+static_assert(sizeof(IkfCtl::pose) == sizeof(PoseDev), "IkfCtl::pose holds a PoseDev");
+
+// double e of pose_from_state(x) (the PoseDev layout), for the filter step
+// to store the next pass's pose: the pass kernels then read it with scalar
+// loads (pose_of_ctl) instead of forming the two matrices in vector
+// registers that stay live through the kernel (in the search pass that
+// pushed 3 float4 to scratch)
+__device__ __forceinline__ double pose_elem(const slio_state& x, int e) {
+  if (e < 4) return x.rot[e];
+  if (e < 7) return x.pos[e - 4];
+  if (e < 11) return x.rli[e - 7];
+  if (e < 14) return x.tli[e - 11];
+  const double* q = e < 23 ? x.rot : x.rli;
+  const int k = e < 23 ? e - 14 : e - 23;
+  double R[9];
+  qmatrix(Quat{q[0], q[1], q[2], q[3]}, R);
+  double v = R[0];
+#pragma unroll
+  for (int j = 1; j < 9; ++j) v = k == j ? R[j] : v;
+  return v;
+}
+typedef __attribute__((address_space(4))) const double cdouble;  // constant: scalar loads
+__device__ __forceinline__ PoseDev pose_of_ctl(const IkfCtl* ctl) {
+  PoseDev P;
+  cdouble* src = (cdouble*)(const void*)ctl->pose;
+  double* dst = reinterpret_cast<double*>(&P);
+#pragma unroll
+  for (int e = 0; e < 32; ++e) dst[e] = src[e];
+  return P;
+}
 
 __device__ __forceinline__ PoseDev pose_from_state(const slio_state& x) {
   PoseDev P;
@@ -1583,7 +1617,14 @@ __device__ __forceinline__ Quat qnormalized_fast(const Quat& q) {
 __device__ __forceinline__ Quat so3_boxplus_dev(const Quat& q, const double om[3]) {
   const double theta2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
   Quat e;
-  if (theta2 >= kSmallEps * kSmallEps && theta2 < 0.0625) {  // half-angle < 0.125
+  if (theta2 < kSmallEps * kSmallEps) {
+    // Sophus' small-angle branch: cos(theta / 2) is 1.0 in double below
+    // 1e-10 (a rotation the update leaves alone, e.g. R_LI without
+    // extrinsic estimation)
+    const double t4 = theta2 * theta2;
+    const double imag = 0.5 - 0.0208333 * theta2 + 0.000260417 * t4;
+    e = qnormalized_fast(Quat{1.0, imag * om[0], imag * om[1], imag * om[2]});
+  } else if (theta2 < 0.0625) {  // half-angle < 0.125
     const double u = 0.25 * theta2;
     const double sh = 1.0 + u * (-1.0 / 6 + u * (1.0 / 120 + u * (-1.0 / 5040 + u * (1.0 / 362880 +
                       u * (-1.0 / 39916800 + u * (1.0 / 6227020800.0))))));
@@ -1712,6 +1753,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
           q[2] = rq.y;
           q[3] = rq.z;
         }
+        SSTAMP(12);
       }
     }
     if (t == 0) {
@@ -1745,31 +1787,12 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
       }
       L.s_final = fin;
     }
-    // keep the factor, M and 1 / diag of this pass for a final pass without
-    // effective points: LM = [factor (D x D) | M (upper triangle, 78) | invd]
-    if (valid && ok) {
-      const int lane = t;
-      double fv = 0.0, iv = 0.0;
-#pragma unroll
-      for (int r = 0; r < D; ++r) {
-        iv = lane == r ? invd[r] : iv;
-#pragma unroll
-        for (int c = 0; c <= r; ++c) fv = lane == r * D + c ? a[r][c] : fv;
-      }
-      if (lane < D * D) ctl->LM[lane] = fv;
-      if (D * D > 64)
-        for (int e = lane + 64; e < D * D; e += 64) {
-          const int r = e / D, c = e - r * D;
-          double v = 0.0;
-#pragma unroll
-          for (int rr = 0; rr < D; ++rr)
-#pragma unroll
-            for (int cc = 0; cc <= rr; ++cc) v = (rr == r && cc == c) ? a[rr][cc] : v;
-          ctl->LM[e] = v;
-        }
-      for (int e = lane; e < SLIO_NHTH; e += 64) ctl->LM[144 + e] = L.Mt[e];
-      if (lane < D) ctl->LM[288 + lane] = iv;
-    }
+    SSTAMP(13);
+    SSTAMP(14);
+  } else if (valid) {
+    // waves 1..3, beside wave 0's chain: keep this pass's M for a final pass
+    // without effective points (its factor is formed again from P_DD^-1 + M)
+    for (int e = t - 64; e < SLIO_NHTH; e += NT - 64) ctl->LM[144 + e] = L.Mt[e];
   }
   __syncthreads();
   SSTAMP(6);
@@ -1791,15 +1814,27 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
     // P = (I - K H) P with K H [:, :D] = G S^-1 M (esekfom.hpp:341-343)
     if (t < 64) {
       if (!valid) {
-        // the last valid pass's factor and M
-#pragma unroll
-        for (int r = 0; r < D; ++r) {
-          invd[r] = ctl->LM[288 + r];
-#pragma unroll
-          for (int c = 0; c <= r; ++c) a[r][c] = ctl->LM[r * D + c];
-        }
+        // the last valid pass's M (fixed mode: one exists, or the update
+        // would not end here with a P update); its factor, formed again
         for (int e = t; e < SLIO_NHTH; e += 64) L.Mt[e] = ctl->LM[144 + e];
         wave_fence();
+#pragma unroll
+        for (int r = 0; r < D; ++r)
+#pragma unroll
+          for (int c = 0; c <= r; ++c) a[r][c] = L.P11i[r * D + c] + L.Mt[tri_index(c, r)];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          const double d = a[j][j];
+          const double inv = rsqrt_nr(d);
+          invd[j] = inv;
+          a[j][j] = d * inv;
+#pragma unroll
+          for (int r = j + 1; r < D; ++r) a[r][j] = a[r][j] * inv;
+#pragma unroll
+          for (int k = j + 1; k < D; ++k)
+#pragma unroll
+            for (int r = k; r < D; ++r) a[r][k] = fma(-a[r][j], a[k][j], a[r][k]);
+        }
       }
       if (t < D) {
         // column t of Z = S^-1 M = L^-T L^-1 M
@@ -1850,6 +1885,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
     const double* xs = reinterpret_cast<const double*>(&L.x);
     double* xd = reinterpret_cast<double*>(&ctl->x);
     for (int e = t; e < kStateD; e += NT) xd[e] = xs[e];
+    if (t >= 64 && t < 96) ctl->pose[t - 64] = pose_elem(L.x, t - 64);  // the next pass's pose
   }
   if (t < 8) (&ctl->converge)[t] = L.fl[t];
   if (t == 0) ctl->last_m = m;
@@ -2079,7 +2115,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
     return;
-  const PoseDev pose = DEVPOSE ? pose_from_state(cfg.ctl->x) : pose_arg;
+  const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
   constexpr int NT = search_block<LPQ>();
   if (DEVPOSE) ikf_dx_new(cfg.ctl);
   constexpr int QPP = NT / LPQ;               // queries per kNN pass
@@ -2574,7 +2610,7 @@ __global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan,
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
     return;
-  const PoseDev pose = DEVPOSE ? pose_from_state(cfg.ctl->x) : pose_arg;
+  const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
   if (DEVPOSE) ikf_dx_new(cfg.ctl);
   __shared__ double rows[SLIO_CHUNK][kRow];
   __shared__ double part[1][SLIO_NPROD];
@@ -2708,8 +2744,61 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
   }
   if (D) SSTAMP(2);
   if (t == 0) reset_counter(cnt);
-  if (D) {
-    step_load<NT, D, kNSeg * SLIO_NPROD>(L, &L.u.seg[0][0], seg_out, true, src, ctl);
+  if constexpr (D > 0) {
+    // one round trip, no LDS staging of the rows: thread k < 91 loads the
+    // 64 segment values of product k and adds them in registers (8 super
+    // rows, then their ordered total -- the tree step_totals uses); the
+    // other 165 threads load the control block meanwhile
+    if (t < SLIO_NPROD) {
+      double v[kNSeg];
+#pragma unroll
+      for (int e = 0; e < kNSeg; ++e) v[e] = ld_sc1(seg_out + e * SLIO_NPROD + t);
+      double sp[SLIO_NSUPER];
+#pragma unroll
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
+        double a = v[ss * kSuperSeg];
+#pragma unroll
+        for (int q = 1; q < kSuperSeg; ++q) a = a + v[ss * kSuperSeg + q];
+        sp[ss] = a;
+      }
+      double a = sp[0];
+#pragma unroll
+      for (int ss = 1; ss < SLIO_NSUPER; ++ss) a = a + sp[ss];
+      L.tot[t] = a;
+      if (t < SLIO_NHTH)
+        L.Mt[t] = a / R;
+      else if (t < SLIO_NHTH + 12)
+        L.hR[t - SLIO_NHTH] = a / R;
+#pragma unroll
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
+    } else {
+      constexpr int NC = NT - SLIO_NPROD, nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
+      const int tt = t - SLIO_NPROD;
+      const bool first = src != ctl;
+      const gdouble* gc = (const gdouble*)(const double*)src;
+      double cv[kC];
+#pragma unroll
+      for (int u = 0; u < kC; ++u) {
+        const int e = tt + u * NC;
+        cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
+      }
+      typedef __attribute__((address_space(1))) int32_t gint;
+      const int32_t fl = tt < 8 ? ((const gint*)(const int32_t*)&src->converge)[tt] : 0;
+#pragma unroll
+      for (int u = 0; u < kC; ++u) {
+        const int e = tt + u * NC;
+        if (e < nC) {
+          ctl_dst<D>(L, e) = cv[u];
+          if (first) reinterpret_cast<double*>(ctl)[ctl_src<D>(e)] = cv[u];  // keep it in HBM
+        }
+      }
+      if (tt < 8) L.fl[tt] = fl;
+      if (first && tt == 0) ctl->singular = 0;
+    }
+    __syncthreads();
+    SSTAMP(4);
+    if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
+    ikf_step<NT, D>(ctl, hblk, R, iter, maxit, L);
   } else {
     constexpr int kR = (kNSeg * SLIO_NPROD + NT - 1) / NT;
     double rv[kR];
@@ -2723,38 +2812,17 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
       const int e = t + u * NT;
       if (e < kNSeg * SLIO_NPROD) (&L.u.seg[0][0])[e] = rv[u];
     }
-  }
-  __syncthreads();
-  if (D) SSTAMP(4);
-  // thread k < 91: the 8 super rows of product k (independent chains) and
-  // their ordered total -- the same tree as the super rows summed by
-  // step_totals, with one barrier
-  if (t < SLIO_NPROD) {
-    double sp[SLIO_NSUPER];
-#pragma unroll
-    for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
-      double v = L.u.seg[ss * kSuperSeg][t];
-#pragma unroll
-      for (int q = 1; q < kSuperSeg; ++q) v = v + L.u.seg[ss * kSuperSeg + q][t];
-      sp[ss] = v;
-    }
-    double v = sp[0];
-#pragma unroll
-    for (int ss = 1; ss < SLIO_NSUPER; ++ss) v = v + sp[ss];
-    if constexpr (D > 0) {
-      L.tot[t] = v;
-      if (t < SLIO_NHTH)
-        L.Mt[t] = v / R;
-      else if (t < SLIO_NHTH + 12)
-        L.hR[t - SLIO_NHTH] = v / R;
-    }
-#pragma unroll
-    for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
-  }
-  if constexpr (D > 0) {
     __syncthreads();
-    if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
-    ikf_step<NT, D>(ctl, hblk, R, iter, maxit, L);
+    // thread k < 91: the 8 super rows of product k
+    if (t < SLIO_NPROD) {
+#pragma unroll
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
+        double a = L.u.seg[ss * kSuperSeg][t];
+#pragma unroll
+        for (int q = 1; q < kSuperSeg; ++q) a = a + L.u.seg[ss * kSuperSeg + q][t];
+        super_out[ss * SLIO_NPROD + t] = a;
+      }
+    }
   }
 }
 
@@ -5511,23 +5579,28 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     SLIO_HIP(hipHostGetDevicePointer((void**)&c.d_hctl, c.h_ctl, 0));
   }
   IkfCtl& hc = *c.h_ctl;
-  hc.x = *x;
-  hc.xprop = *x;
-  std::memcpy(hc.P, P, sizeof(double) * 576);
-  hc.converge = 1;
-  hc.t = 0;
-  hc.done = 0;
-  hc.search_now = 1;
-  hc.passes = hc.searches = hc.valid_passes = 0;
-  hc.mode = mode;
-  hc.last_m = 0;
-  hc.singular = 0;
-  hc.published = 0;
-  for (int k = 0; k < 24; ++k) hc.dxn[k] = 0.0;  // x == x_propagated on pass 0
   // The control block comes in and goes out through the mapped host block:
   // pass 0 takes its pose by value and its filter step reads the block over
   // the bus (then keeps it in HBM); the step that ends the update writes x,
-  // P and the flags back.  No copy-engine work on the path.
+  // P and the flags back.  No copy-engine work on the path.  The block is
+  // filled while pass 0's search runs (launched first): the previous
+  // update has published, and its kernels still queued exit at once (done
+  // in the HBM copy), so nothing reads or writes the host block meanwhile.
+  auto fill_block = [&] {
+    hc.x = *x;
+    hc.xprop = *x;
+    std::memcpy(hc.P, P, sizeof(double) * 576);
+    hc.converge = 1;
+    hc.t = 0;
+    hc.done = 0;
+    hc.search_now = 1;
+    hc.passes = hc.searches = hc.valid_passes = 0;
+    hc.mode = mode;
+    hc.last_m = 0;
+    hc.singular = 0;
+    hc.published = 0;
+    for (int k = 0; k < 24; ++k) hc.dxn[k] = 0.0;  // x == x_propagated on pass 0
+  };
   const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
   // H's columns 6..11 are zero without extrinsic estimation (esekfom.hpp:218-220):
   // the filter step works on the first 6 error-state components
@@ -5550,6 +5623,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
     int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, extrinsic_est, &sa, !p0 || reduce);
     if (rc) return rc;
+    if (p0) fill_block();
     if (p0) {
       // information-form constants of the update (P is fixed until its end),
       // formed on the host while pass 0's search runs; pass 0's filter step

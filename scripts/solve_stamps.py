@@ -21,8 +21,8 @@ L.check(lib.slio_map_upload(h, L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "m
 bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
 L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]), "scan")
 st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9), [0, 0, -9.81]])
-names = ["start", "rows-stored", "last-found", "pre-solve", "staged", "S+M+dxn", "chain-done",
-         "P", "end", "v-done", "chol+solve", "dx"]
+names = ["start", "-", "last-found", "-", "staged", "totals", "chain-done",
+         "P", "end", "S+w", "chol+solve", "dx+ballot", "boxplus", "flags", "LM"]
 acc = []
 for rep in range(12):
     for maxit in (1, 2, 4):
@@ -35,12 +35,12 @@ for rep in range(12):
                                            L.ALLREDUCE_FN(), None, C.byref(st)), "ikf")
         buf = (C.c_ulonglong * 32)()
         lib.slio_dbg_solve_stamps(buf)
-        v = np.array(buf[:12], dtype=np.int64)
+        v = np.array(buf[:15], dtype=np.int64)
         if rep >= 2:
             acc.append((maxit, v - v[0]))
 for maxit in (1, 2, 4):
     d = np.array([a for m, a in acc if m == maxit])
     med = np.median(d, axis=0) * 10  # wall_clock64: 100 MHz -> ns
-    order = [0, 1, 2, 3, 4, 5, 9, 10, 11, 6, 7, 8]
+    order = [0, 2, 4, 5, 9, 10, 11, 12, 13, 14, 6, 7, 8]
     print(f"maxit {maxit}: " + "  ".join(f"{names[k]}={med[k]/1e3:.2f}us" for k in order))
 lib.slio_destroy(h)
