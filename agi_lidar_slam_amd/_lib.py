@@ -162,6 +162,8 @@ class SlioImuPose(C.Structure):
                 ("vel", C.c_double * 3), ("pos", C.c_double * 3), ("rot", C.c_double * 9)]
 
 
+SLIO_COMM_ID_BYTES = 128
+
 SIGNATURES = {
     "slio_params_default": (C.c_int, [C.POINTER(SlioParams)]),
     "slio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioParams)]),
@@ -171,6 +173,11 @@ SIGNATURES = {
     "slio_build_id": (C.c_char_p, []),
     "slio_map_upload": (C.c_int, [_P, _FP, _FP, _FP, C.c_int64]),
     "slio_map_share": (C.c_int, [_P, _P]),
+    "slio_create_group": (C.c_int, [C.POINTER(_P), C.c_int, _IP, C.POINTER(SlioParams)]),
+    "slio_group_ikf_update": (C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(SlioState), _DP, C.c_double, C.c_int,
+                                        C.c_int, C.c_int, C.POINTER(SlioIkfStats)]),
+    "slio_comm_unique_id": (C.c_int, [_U8P]),
+    "slio_comm_init": (C.c_int, [_P, _U8P]),
     "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),
     "slio_ikf_predict": (C.c_int, [C.POINTER(SlioState), _DP, C.c_double, _DP, _DP, _DP]),
     "slio_imu_forward": (C.c_int, [C.POINTER(SlioImuSample), C.c_int, C.c_double, C.c_double, _DP, C.c_double,
@@ -258,13 +265,16 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    path = os.environ.get("SLIO_LIB_OVERRIDE", path)  # diagnostic builds (scripts/build_abl.sh)
+    override = os.environ.get("SLIO_LIB_OVERRIDE")  # diagnostic / A-B builds (scripts/build_abl.sh)
+    path = override or path
     if not os.path.exists(path):
         raise RuntimeError(
             f"{path} is missing: build it with `python -m agi_lidar_slam_amd.build` "
             "(there is no CPU fallback for the device path)")
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if override and not hasattr(lib, name):
+            continue  # an older build in an A/B run: entry points it predates stay unbound
         fn = getattr(lib, name)  # AttributeError if the library lacks a declared symbol
         fn.restype = res
         fn.argtypes = args

@@ -30,6 +30,10 @@ FLAGS = [
     "-ffp-contract=off",
     "-fno-fast-math",
     "-Wall",
+    # the in-library all-reduce of the multi-GPU path (RCCL over xGMI)
+    "-L/opt/rocm/lib",
+    "-lrccl",
+    "-Wl,-rpath,/opt/rocm/lib",
 ]
 
 

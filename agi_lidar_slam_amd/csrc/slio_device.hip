@@ -17,6 +17,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1461,13 +1462,10 @@ __device__ __forceinline__ void reset_counter(uint32_t* p) {
 // LDS of the filter step.  D = 6 without extrinsic estimation (H's columns
 // 6..11 are zero, esekfom.hpp:218-220), 12 with it.
 struct StepLds {
-  union {
-    double seg[kNSeg][SLIO_NPROD];  // the pass's 64 segment rows (k_super_sums)
-    struct {
-      double Z[144];  // D x D: S^-1 M             (P update)
-      double K[288];  // 24 x D: G S^-1 M = K H[:, :D]
-    } zk;
-  } u;
+  struct {
+    double Z[144];  // D x D: S^-1 M             (P update)
+    double K[288];  // 24 x D: G S^-1 M = K H[:, :D]
+  } zk;
   double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums
   double tot[SLIO_NPROD];               // H^T H (78, upper triangle), H^T h (12), m
   double Mt[SLIO_NHTH];                 // H^T H / R (upper triangle)
@@ -1855,7 +1853,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
           zc[j] = s2 * invd[j];
         }
 #pragma unroll
-        for (int j = 0; j < D; ++j) L.u.zk.Z[j * D + cc] = zc[j];
+        for (int j = 0; j < D; ++j) L.zk.Z[j * D + cc] = zc[j];
       }
     }
     __syncthreads();
@@ -1863,8 +1861,8 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
       const int r = e / D, cc = e - r * D;
       double s2 = 0.0;
 #pragma unroll
-      for (int k = 0; k < D; ++k) s2 = fma(L.G[r * D + k], L.u.zk.Z[k * D + cc], s2);
-      L.u.zk.K[e] = s2;
+      for (int k = 0; k < D; ++k) s2 = fma(L.G[r * D + k], L.zk.Z[k * D + cc], s2);
+      L.zk.K[e] = s2;
     }
     __syncthreads();
 #pragma unroll
@@ -1874,7 +1872,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
         const int r = e / 24, cc = e - r * 24;
         double s2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < D; ++k) s2 = fma(L.u.zk.K[r * D + k], L.P[k * 24 + cc], s2);
+        for (int k = 0; k < D; ++k) s2 = fma(L.zk.K[r * D + k], L.P[k * 24 + cc], s2);
         pn[u] = L.P[e] - s2;
         ctl->P[e] = pn[u];
       }
@@ -2471,6 +2469,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
 
   // ---------------- phase 2: plane fit, residual gate, Jacobian row
+  // (lanes 0..127, two of the four wavefronts; spreading the fit over the
+  // first lane of each query's pair, all four wavefronts, measured slower:
+  // 25.0k vs 26.0k IKF it/s, the fit's instructions issue twice as often)
   if (tid < SLIO_CHUNK) {
     const int slot = tid;
     const int64_t i = chunk * SLIO_CHUNK + slot;
@@ -2673,7 +2674,15 @@ __device__ __forceinline__ void chunk_order(const uint32_t* __restrict__ cost, u
   if (t < n) {
     const uint32_t c = cs[t];
     int rank = 0;
-    for (int j = 0; j < n; ++j) {
+    int j = 0;
+    for (; j + 8 <= n; j += 8) {  // 8 independent LDS reads in flight
+      uint32_t d[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d[u] = cs[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rank += (d[u] > c || (d[u] == c && j + u < t)) ? 1 : 0;
+    }
+    for (; j < n; ++j) {
       const uint32_t d = cs[j];
       rank += (d > c || (d == c && j < t)) ? 1 : 0;
     }
@@ -2702,7 +2711,11 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
     double* super_out, IkfCtl* ctl, const IkfCtl* src, IkfCtl* hblk, uint32_t* cnt, double R, int iter,
     int maxit, const uint32_t* __restrict__ cost, uint32_t* __restrict__ perm, int64_t nblk, int W) {
   constexpr int NT = kSolveThreads;
-  __shared__ StepLds L;
+  __shared__ union {
+    double seg[kNSeg][SLIO_NPROD];  // the pass's 64 segment rows (D == 0)
+    StepLds L;
+  } sh;
+  StepLds& L = sh.L;
   __shared__ int arr;
   const int b = blockIdx.x;  // segment row b = 8 s + g
   const int s = b / kSuperSeg, g = b - s * kSuperSeg;
@@ -2739,7 +2752,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
   if (arr != kNSeg - 1) {
     // the next search pass's chunk order of XCD x = arrival index: the
     // first 8 to arrive (never the last) cover all 8 ranges every pass
-    if (perm && arr < 8) chunk_order(cost, perm, nblk, arr, W, reinterpret_cast<uint32_t*>(&L.u.seg[0][0]));
+    if (perm && arr < 8) chunk_order(cost, perm, nblk, arr, W, reinterpret_cast<uint32_t*>(&sh.seg[0][0]));
     return;
   }
   if (D) SSTAMP(2);
@@ -2810,16 +2823,16 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
 #pragma unroll
     for (int u = 0; u < kR; ++u) {
       const int e = t + u * NT;
-      if (e < kNSeg * SLIO_NPROD) (&L.u.seg[0][0])[e] = rv[u];
+      if (e < kNSeg * SLIO_NPROD) (&sh.seg[0][0])[e] = rv[u];
     }
     __syncthreads();
     // thread k < 91: the 8 super rows of product k
     if (t < SLIO_NPROD) {
 #pragma unroll
       for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
-        double a = L.u.seg[ss * kSuperSeg][t];
+        double a = sh.seg[ss * kSuperSeg][t];
 #pragma unroll
-        for (int q = 1; q < kSuperSeg; ++q) a = a + L.u.seg[ss * kSuperSeg + q][t];
+        for (int q = 1; q < kSuperSeg; ++q) a = a + sh.seg[ss * kSuperSeg + q][t];
         super_out[ss * SLIO_NPROD + t] = a;
       }
     }
@@ -2876,6 +2889,7 @@ struct Ctx {
   double* d_super = nullptr;
   double* d_super_own = nullptr;
   double* d_seg = nullptr;    // the pass's 64 segment rows (k_super_sums hand-off)
+  void* comm = nullptr;        // RCCL communicator of the rank group (slio_comm_init / slio_create_group)
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
                               // (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
@@ -3400,7 +3414,8 @@ int slio_create(slio_handle* out, const slio_params* p) {
       hipMalloc(&h->c.d_seg, sizeof(double) * kNSeg * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.count, sizeof(uint32_t) * 16) != hipSuccess ||
-      hipMemset(h->c.count, 0, sizeof(uint32_t) * 16) != hipSuccess) {
+      hipMemset(h->c.count, 0, sizeof(uint32_t) * 16) != hipSuccess ||
+      false) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
     return SLIO_ENOMEM;
@@ -3423,6 +3438,7 @@ int slio_destroy(slio_handle h) {
   (void)hipFree(h->c.d_super_own);
   (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
+  if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
   (void)hipFree(h->c.ctl);
   (void)hipHostFree(h->c.h_ctl);
   if (h->c.done_ev) (void)hipEventDestroy(h->c.done_ev);
@@ -5563,22 +5579,45 @@ int slio_iterate_async(slio_handle h, const slio_pose* x, int do_search, int ext
   return SLIO_OK;
 }
 
-int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R,
-                           int maximum_iter, int extrinsic_est, int mode,
-                           slio_allreduce_fn reduce, void* reduce_ctx, slio_ikf_stats* stats) {
-  SLIO_CHECK_H(h);
-  if (!x || !P || !(R > 0.0) || maximum_iter < 1 ||
-      (mode != SLIO_MODE_REFERENCE && mode != SLIO_MODE_FIXED)) {
-    set_error("slio_ikf_update_device: bad arguments");
-    return SLIO_EINVAL;
+}  // extern "C"
+
+namespace slio {
+
+// One device-resident update on one handle (slio_ikf_update_device), in
+// steps, so that the rank handles of a group can interleave their passes
+// with one collective per pass (slio_group_ikf_update).
+struct UpdateRun {
+  Ctx& c;
+  slio_state* x;
+  double* P;
+  double R;
+  int maxit, ext, mode;
+  bool multi;   // the super rows are all-reduced between a pass and its filter step
+  int first = 0, dim = 6;
+  PoseDev pose0{};
+
+  UpdateRun(Ctx& c_, slio_state* x_, double* P_, double R_, int maxit_, int ext_, int mode_, bool multi_)
+      : c(c_), x(x_), P(P_), R(R_), maxit(maxit_), ext(ext_), mode(mode_), multi(multi_) {}
+
+  int begin() {
+    if (!c.ctl) {
+      SLIO_HIP(hipMalloc(&c.ctl, sizeof(IkfCtl)));
+      SLIO_HIP(hipHostMalloc(&c.h_ctl, sizeof(IkfCtl), hipHostMallocMapped | hipHostMallocCoherent));
+      SLIO_HIP(hipHostGetDevicePointer((void**)&c.d_hctl, c.h_ctl, 0));
+    }
+    first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
+    // H's columns 6..11 are zero without extrinsic estimation (esekfom.hpp:218-220):
+    // the filter step works on the first 6 error-state components
+    dim = ext ? 12 : 6;
+    slio_pose p;
+    std::memcpy(p.rot, x->rot, sizeof(p.rot));
+    std::memcpy(p.pos, x->pos, sizeof(p.pos));
+    std::memcpy(p.rli, x->rli, sizeof(p.rli));
+    std::memcpy(p.tli, x->tli, sizeof(p.tli));
+    pose0 = make_pose(&p);
+    return SLIO_OK;
   }
-  Ctx& c = h->c;
-  if (!c.ctl) {
-    SLIO_HIP(hipMalloc(&c.ctl, sizeof(IkfCtl)));
-    SLIO_HIP(hipHostMalloc(&c.h_ctl, sizeof(IkfCtl), hipHostMallocMapped | hipHostMallocCoherent));
-    SLIO_HIP(hipHostGetDevicePointer((void**)&c.d_hctl, c.h_ctl, 0));
-  }
-  IkfCtl& hc = *c.h_ctl;
+
   // The control block comes in and goes out through the mapped host block:
   // pass 0 takes its pose by value and its filter step reads the block over
   // the bus (then keeps it in HBM); the step that ends the update writes x,
@@ -5586,7 +5625,8 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   // filled while pass 0's search runs (launched first): the previous
   // update has published, and its kernels still queued exit at once (done
   // in the HBM copy), so nothing reads or writes the host block meanwhile.
-  auto fill_block = [&] {
+  void fill_block() {
+    IkfCtl& hc = *c.h_ctl;
     hc.x = *x;
     hc.xprop = *x;
     std::memcpy(hc.P, P, sizeof(double) * 576);
@@ -5600,75 +5640,258 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     hc.singular = 0;
     hc.published = 0;
     for (int k = 0; k < 24; ++k) hc.dxn[k] = 0.0;  // x == x_propagated on pass 0
-  };
-  const int first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
-  // H's columns 6..11 are zero without extrinsic estimation (esekfom.hpp:218-220):
-  // the filter step works on the first 6 error-state components
-  const int dim = extrinsic_est ? 12 : 6;
-  const PoseDev pose0 = [&] {
-    slio_pose p;
-    std::memcpy(p.rot, x->rot, sizeof(p.rot));
-    std::memcpy(p.pos, x->pos, sizeof(p.pos));
-    std::memcpy(p.rli, x->rli, sizeof(p.rli));
-    std::memcpy(p.tli, x->tli, sizeof(p.tli));
-    return make_pose(&p);
-  }();
-  for (int i = first; i < maximum_iter; ++i) {
-    // single rank: the filter step runs in the super-sum kernel's last block;
-    // multi-rank: pass -> all-reduce of the super sums -> k_ikf_solve
+  }
+
+  SolveArgs args(int i) const {
     const bool p0 = i == first;
     const IkfCtl* src = p0 ? (const IkfCtl*)c.d_hctl : c.ctl;
-    const SolveArgs sa{reduce ? 0 : 1, dim, i - first, i, maximum_iter, R, src, c.d_hctl};
+    return SolveArgs{multi ? 0 : 1, dim, i - first, i, maxit, R, src, c.d_hctl};
+  }
+
+  // pass i: search / reuse kernels and k_super_sums (with the filter step on
+  // a single rank; super rows only when multi)
+  int pass(int i) {
+    const bool p0 = i == first;
+    const SolveArgs sa = args(i);
     // pass 0 always searches (converge starts true, esekfom.hpp:282)
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
-    int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, extrinsic_est, &sa, !p0 || reduce);
+    int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, !p0 || multi);
     if (rc) return rc;
-    if (p0) fill_block();
     if (p0) {
+      fill_block();
       // information-form constants of the update (P is fixed until its end),
       // formed on the host while pass 0's search runs; pass 0's filter step
       // reads them from the mapped block
-      if (!info_constants(P, dim, hc.P11i, hc.G)) {
+      if (!info_constants(P, dim, c.h_ctl->P11i, c.h_ctl->G)) {
         (void)hipStreamSynchronize(c.stream);
-        set_error("slio_ikf_update_device: singular covariance block P[:12, :12]");
+        set_error("slio_ikf_update_device: singular covariance block P[:D, :D]");
         return SLIO_EINVAL;
       }
-      if (!reduce) enqueue_super(c, c.ctl, &sa);
+      if (!multi) enqueue_super(c, c.ctl, &sa);
     }
+    SLIO_HIP(hipGetLastError());
+    return SLIO_OK;
+  }
+
+  // multi-rank: the filter step of pass i after the all-reduce, on every rank
+  int solve(int i) {
+    const SolveArgs sa = args(i);
+    if (dim == 12)
+      k_ikf_solve<12><<<1, kSolveThreads, 0, c.stream>>>(c.ctl, sa.src, c.d_hctl, c.d_super, R, i, maxit);
+    else
+      k_ikf_solve<6><<<1, kSolveThreads, 0, c.stream>>>(c.ctl, sa.src, c.d_hctl, c.d_super, R, i, maxit);
+    SLIO_HIP(hipGetLastError());
+    return SLIO_OK;
+  }
+
+  int finish(slio_ikf_stats* stats) {
+    SLIO_HIP(wait_published(c));
+    const IkfCtl& hc = *c.h_ctl;
+    if (!hc.done) {
+      set_error("slio_ikf_update_device: the update did not complete");
+      return SLIO_EDEVICE;
+    }
+    if (hc.singular) {
+      set_error("slio_ikf_update_device: singular covariance");
+      return SLIO_EINVAL;
+    }
+    *x = hc.x;
+    std::memcpy(P, hc.P, sizeof(double) * 576);
+    if (stats) {
+      stats->passes = hc.passes;
+      stats->searches = hc.searches;
+      stats->valid_passes = hc.valid_passes;
+      stats->converged = hc.converge;
+      stats->last_m = hc.last_m;
+      stats->device_ms = 0.0;
+    }
+    return SLIO_OK;
+  }
+};
+
+// the in-library all-reduce of a handle's super rows (RCCL), on its stream
+static int comm_allreduce(Ctx& c) {
+  const ncclResult_t r = ncclAllReduce(c.d_super, c.d_super, (size_t)SLIO_NSUPER * SLIO_NPROD, ncclDouble,
+                                       ncclSum, (ncclComm_t)c.comm, c.stream);
+  if (r != ncclSuccess) {
+    set_error(std::string("slio: ncclAllReduce: ") + ncclGetErrorString(r));
+    return SLIO_EDEVICE;
+  }
+  return SLIO_OK;
+}
+
+}  // namespace slio
+
+extern "C" {
+
+int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R,
+                           int maximum_iter, int extrinsic_est, int mode,
+                           slio_allreduce_fn reduce, void* reduce_ctx, slio_ikf_stats* stats) {
+  SLIO_CHECK_H(h);
+  if (!x || !P || !(R > 0.0) || maximum_iter < 1 ||
+      (mode != SLIO_MODE_REFERENCE && mode != SLIO_MODE_FIXED)) {
+    set_error("slio_ikf_update_device: bad arguments");
+    return SLIO_EINVAL;
+  }
+  Ctx& c = h->c;
+  // the caller's reduce hook, else the handle's communicator (any number of
+  // ranks, one included: the same path as several)
+  const bool comm = !reduce && c.comm;
+  if (!reduce && !comm && c.prm.nranks > 1) {
+    set_error("slio_ikf_update_device: nranks > 1 needs a reduce hook or slio_comm_init");
+    return SLIO_ESTATE;
+  }
+  UpdateRun u(c, x, P, R, maximum_iter, extrinsic_est, mode, reduce || comm);
+  if (int rc = u.begin()) return rc;
+  for (int i = u.first; i < maximum_iter; ++i) {
+    // single rank: the filter step runs in the super-sum kernel's last block
+    // (or the search pass's tail); multi-rank: pass -> all-reduce of the
+    // super sums -> k_ikf_solve
+    if (int rc = u.pass(i)) return rc;
     if (reduce) {
-      rc = reduce(reduce_ctx, c.d_super, (int64_t)SLIO_NSUPER * SLIO_NPROD, (void*)c.stream);
-      if (rc) {
+      if (reduce(reduce_ctx, c.d_super, (int64_t)SLIO_NSUPER * SLIO_NPROD, (void*)c.stream)) {
         set_error("slio_ikf_update_device: reduce callback failed");
         return SLIO_EDEVICE;
       }
-      if (dim == 12)
-        k_ikf_solve<12><<<1, kSolveThreads, 0, c.stream>>>(c.ctl, src, c.d_hctl, c.d_super, R, i,
-                                                         maximum_iter);
-      else
-        k_ikf_solve<6><<<1, kSolveThreads, 0, c.stream>>>(c.ctl, src, c.d_hctl, c.d_super, R, i,
-                                                        maximum_iter);
+    } else if (comm) {
+      if (int rc = comm_allreduce(c)) return rc;
     }
+    if (u.multi)
+      if (int rc = u.solve(i)) return rc;
   }
-  SLIO_HIP(hipGetLastError());
-  SLIO_HIP(wait_published(c));
-  if (!c.h_ctl->done) {
-    set_error("slio_ikf_update_device: the update did not complete");
+  return u.finish(stats);
+}
+
+int slio_comm_unique_id(uint8_t id[SLIO_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) <= SLIO_COMM_ID_BYTES, "ncclUniqueId size");
+  if (!id) return SLIO_EINVAL;
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) {
+    set_error(std::string("slio_comm_unique_id: ") + ncclGetErrorString(r));
     return SLIO_EDEVICE;
   }
-  if (c.h_ctl->singular) {
-    set_error("slio_ikf_update_device: singular covariance");
+  std::memset(id, 0, SLIO_COMM_ID_BYTES);
+  std::memcpy(id, &u, sizeof(u));
+  return SLIO_OK;
+}
+
+int slio_comm_init(slio_handle h, const uint8_t id[SLIO_COMM_ID_BYTES]) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!id || c.comm) {
+    set_error("slio_comm_init: null id or communicator already set");
     return SLIO_EINVAL;
   }
-  *x = c.h_ctl->x;
-  std::memcpy(P, c.h_ctl->P, sizeof(double) * 576);
-  if (stats) {
-    stats->passes = c.h_ctl->passes;
-    stats->searches = c.h_ctl->searches;
-    stats->valid_passes = c.h_ctl->valid_passes;
-    stats->converged = c.h_ctl->converge;
-    stats->last_m = c.h_ctl->last_m;
-    stats->device_ms = 0.0;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&comm, c.prm.nranks, u, c.prm.rank);
+  if (r != ncclSuccess) {
+    set_error(std::string("slio_comm_init: ncclCommInitRank: ") + ncclGetErrorString(r));
+    return SLIO_EDEVICE;
   }
+  c.comm = comm;
+  return SLIO_OK;
+}
+
+int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio_params* p) {
+  if (!out || !devices || !p || ndev < 1 || (SLIO_NSUPER % ndev) != 0) {
+    set_error("slio_create_group: bad arguments (ndev must divide 8)");
+    return SLIO_EINVAL;
+  }
+  for (int r = 0; r < ndev; ++r) out[r] = nullptr;
+  int rc = SLIO_OK;
+  for (int r = 0; r < ndev && !rc; ++r) {
+    slio_params q = *p;
+    q.device = devices[r];
+    q.rank = r;
+    q.nranks = ndev;
+    rc = slio_create(&out[r], &q);
+  }
+  std::vector<ncclComm_t> comms((size_t)ndev, nullptr);
+  if (!rc) {
+    const ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devices);
+    if (r != ncclSuccess) {
+      set_error(std::string("slio_create_group: ncclCommInitAll: ") + ncclGetErrorString(r));
+      rc = SLIO_EDEVICE;
+    }
+  }
+  if (rc) {
+    for (int r = 0; r < ndev; ++r) {
+      slio_destroy(out[r]);
+      out[r] = nullptr;
+    }
+    return rc;
+  }
+  for (int r = 0; r < ndev; ++r) out[r]->c.comm = comms[r];
+  return SLIO_OK;
+}
+
+int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], double R, int maximum_iter,
+                          int extrinsic_est, int mode, slio_ikf_stats* stats) {
+  if (!hs || n < 1 || !x || !P || !(R > 0.0) || maximum_iter < 1 ||
+      (mode != SLIO_MODE_REFERENCE && mode != SLIO_MODE_FIXED)) {
+    set_error("slio_group_ikf_update: bad arguments");
+    return SLIO_EINVAL;
+  }
+  for (int r = 0; r < n; ++r)
+    if (!hs[r] || hs[r]->c.prm.nranks != n || hs[r]->c.prm.rank != r || !hs[r]->c.comm) {
+      set_error("slio_group_ikf_update: handles must be ranks 0..n-1 of one group (slio_create_group)");
+      return SLIO_EINVAL;
+    }
+  // every rank starts from the caller's x and P and ends with the same bits
+  std::vector<slio_state> xs((size_t)n, *x);
+  std::vector<std::vector<double>> Ps((size_t)n, std::vector<double>(P, P + 576));
+  std::vector<UpdateRun> runs;
+  runs.reserve((size_t)n);
+  for (int r = 0; r < n; ++r)
+    runs.emplace_back(hs[r]->c, &xs[r], Ps[r].data(), R, maximum_iter, extrinsic_est, mode, true);
+  for (int r = 0; r < n; ++r) {
+    SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
+    if (int rc = runs[r].begin()) return rc;
+  }
+  for (int i = runs[0].first; i < maximum_iter; ++i) {
+    for (int r = 0; r < n; ++r) {
+      SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
+      if (int rc = runs[r].pass(i)) return rc;
+    }
+    {
+      // one RCCL all-reduce of the 8 x 91 super rows per pass, all ranks
+      // enqueued by this thread as one group (each on its own stream)
+      if (ncclGroupStart() != ncclSuccess) {
+        set_error("slio_group_ikf_update: ncclGroupStart");
+        return SLIO_EDEVICE;
+      }
+      int rc = SLIO_OK;
+      for (int r = 0; r < n && !rc; ++r) rc = comm_allreduce(hs[r]->c);
+      if (ncclGroupEnd() != ncclSuccess && !rc) {
+        set_error("slio_group_ikf_update: ncclGroupEnd");
+        rc = SLIO_EDEVICE;
+      }
+      if (rc) return rc;
+      for (int r = 0; r < n; ++r) {
+        SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
+        if (int rc2 = runs[r].solve(i)) return rc2;
+      }
+    }
+  }
+  slio_ikf_stats st0{};
+  for (int r = 0; r < n; ++r) {
+    SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
+    slio_ikf_stats st{};
+    if (int rc = runs[r].finish(&st)) return rc;
+    if (r == 0) st0 = st;
+  }
+  for (int r = 1; r < n; ++r)
+    if (std::memcmp(&xs[r], &xs[0], sizeof(slio_state)) != 0 ||
+        std::memcmp(Ps[r].data(), Ps[0].data(), sizeof(double) * 576) != 0) {
+      set_error("slio_group_ikf_update: ranks disagree (x or P differ bitwise)");
+      return SLIO_EDEVICE;
+    }
+  *x = xs[0];
+  std::memcpy(P, Ps[0].data(), sizeof(double) * 576);
+  if (stats) *stats = st0;
   return SLIO_OK;
 }
 

@@ -304,11 +304,42 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R,
  * 24x24 step after each pass (same operation order as slio_ikf_update), so
  * the passes are enqueued back to back with no host round trip; the host
  * synchronises once at the end.  `reduce` (if any) is called once per pass at
- * enqueue time and must enqueue a stream-ordered SUM all-reduce. */
+ * enqueue time and must enqueue a stream-ordered SUM all-reduce; with NULL
+ * and nranks > 1 the handle's communicator is used (slio_comm_init). */
 int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R,
                            int maximum_iter, int extrinsic_est, int mode,
                            slio_allreduce_fn reduce, void* reduce_ctx,
                            slio_ikf_stats* stats);
+
+/* ---- multi-GPU: the per-pass all-reduce inside the library (RCCL) --------
+ * The scan's points shard across ranks (slio_params rank / nranks); each
+ * pass's 8 x 91 fp64 super rows are SUM-all-reduced (one ncclAllReduce over
+ * xGMI) and every rank runs the identical filter step, so all ranks hold the
+ * same x and P, bit for bit, as one rank would.  Replaces the per-iteration
+ * all-reduce the reference does not have (its laserMapping.cpp:772-774 update
+ * runs on one CPU process). */
+#define SLIO_COMM_ID_BYTES 128
+/* One process, ndev GPUs (the reference's single-process laserMapping node):
+ * out[r] = a handle of rank r on devices[r], all sharing one communicator
+ * (ncclCommInitAll).  p gives the other parameters (rank / nranks / device
+ * are set here); ndev divides 8.  Each handle then takes the map
+ * (slio_map_upload: a replica per GPU) and the whole scan (slio_scan_upload),
+ * and slio_group_ikf_update runs the update on all of them. */
+int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio_params* p);
+/* slio_ikf_update_device on every rank of a group, enqueued from the calling
+ * thread: per pass, each rank's search pass, the ranks' all-reduces as one
+ * ncclGroup, each rank's filter step -- no host round trip until the end.
+ * x and P (in / out) and stats come back from rank 0; the call fails
+ * (SLIO_EDEVICE) if any rank's x or P differs from rank 0's. */
+int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], double R,
+                          int maximum_iter, int extrinsic_est, int mode, slio_ikf_stats* stats);
+/* One process per GPU (e.g. torchrun): rank 0 makes an id (ncclGetUniqueId),
+ * the caller hands it to every rank, each initialises its handle's
+ * communicator (ncclCommInitRank with the handle's rank / nranks, a
+ * collective call); slio_ikf_update_device with reduce == NULL then
+ * all-reduces in the library on the handle's stream. */
+int slio_comm_unique_id(uint8_t id[SLIO_COMM_ID_BYTES]);
+int slio_comm_init(slio_handle h, const uint8_t id[SLIO_COMM_ID_BYTES]);
 
 /* ---- IMU forward propagation and scan undistortion (ImuProcess::UndistortPcl,
  *      src/S-FAST_LIO/src/IMU_Processing.hpp:253-402) ------------------------ */

@@ -1,0 +1,130 @@
+"""GPU tests of the in-library multi-GPU path (include/slio.h, RCCL).
+
+The reference updates on one CPU process (laserMapping.cpp:772-774); the
+drop-in shards the scan over ranks and all-reduces each pass's 8 x 91 fp64
+super rows inside the library:
+
+* slio_create_group / slio_group_ikf_update (one process, ndev GPUs, one
+  ncclCommInitAll communicator, the ranks' all-reduces as one ncclGroup):
+  a group of ONE rank goes through the same path (super rows -> ncclAllReduce
+  on the handle's stream -> k_ikf_solve) and must give x and P bit for bit
+  equal to the plain single-rank update, and within the north_star tolerance
+  of the oracle.  A group of two ranks on this one GPU is run where RCCL
+  accepts it (it refuses two ranks on one device on some builds: then the
+  test says so and skips; the 2..8-GPU runs are the driver's).
+* slio_comm_unique_id / slio_comm_init (one process per GPU, torchrun):
+  one rank, reduce == NULL, bitwise equal to the single-rank update.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_gpu_parity import L, mk, rot_err, state_of, upload_map, upload_scan  # noqa: E402,F401
+from test_gpu_runtime import C2_CELL, TOL_POS, TOL_ROT, c2, slio_state, state_array  # noqa: E402,F401
+
+pytestmark = pytest.mark.gpu
+
+
+def single_update(L, mp, fr, st, maxit=4, mode=None):
+    lib = L.load()
+    mode = L.SLIO_MODE_FIXED if mode is None else mode
+    h = mk(L, cell=C2_CELL)
+    try:
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, fr.body) == 0
+        xs = slio_state(st)
+        P = np.eye(24) * 1e-2
+        stt = L.SlioIkfStats()
+        L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, maxit, 0, mode,
+                                           L.ALLREDUCE_FN(), None, C.byref(stt)), "single")
+        return state_array(xs), P, (stt.passes, stt.searches, stt.valid_passes, stt.last_m)
+    finally:
+        lib.slio_destroy(h)
+
+
+def group_update(L, mp, fr, st, devices, maxit=4, mode=None):
+    lib = L.load()
+    mode = L.SLIO_MODE_FIXED if mode is None else mode
+    n = len(devices)
+    p = L.SlioParams()
+    lib.slio_params_default(C.byref(p))
+    p.max_points, p.grid_cell = fr.body.shape[0], C2_CELL
+    hs = (C.c_void_p * n)()
+    dv = (C.c_int32 * n)(*devices)
+    rc = lib.slio_create_group(hs, n, dv, C.byref(p))
+    if rc:
+        return rc, lib.slio_last_error().decode(), None
+    try:
+        for r in range(n):
+            upload_map(L, hs[r], mp)
+            assert upload_scan(L, hs[r], fr.body) == 0
+        xs = slio_state(st)
+        P = np.eye(24) * 1e-2
+        stt = L.SlioIkfStats()
+        rc = lib.slio_group_ikf_update(hs, n, C.byref(xs), L.dptr(P), 0.001, maxit, 0, mode, C.byref(stt))
+        if rc:
+            return rc, lib.slio_last_error().decode(), None
+        return 0, "", (state_array(xs), P, (stt.passes, stt.searches, stt.valid_passes, stt.last_m))
+    finally:
+        for r in range(n):
+            lib.slio_destroy(hs[r])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_group_one_rank_bitwise(L, oracle_mod, c2, mode):
+    mp, fr, T = c2
+    st = state_of(fr)
+    x1, P1, s1 = single_update(L, mp, fr, st, mode=mode)
+    rc, msg, out = group_update(L, mp, fr, st, [0], mode=mode)
+    assert rc == 0, msg
+    xg, Pg, sg = out
+    np.testing.assert_array_equal(xg, x1)
+    np.testing.assert_array_equal(Pg, P1)
+    assert sg == s1
+    s_ref, *_ = oracle_mod.ikf_update(T, fr.body, st, np.eye(24) * 1e-2, maximum_iter=4, mode=mode,
+                                      reference_gain=0)
+    assert np.abs(xg[0:3] - s_ref[0:3]).max() < TOL_POS
+    assert rot_err(xg[3:7], s_ref[3:7]) < TOL_ROT
+
+
+def test_group_two_ranks_one_device(L, c2):
+    mp, fr, _ = c2
+    st = state_of(fr)
+    x1, P1, s1 = single_update(L, mp, fr, st)
+    rc, msg, out = group_update(L, mp, fr, st, [0, 0])
+    if rc:
+        pytest.skip(f"RCCL refused two ranks on one device here: {msg}")
+    xg, Pg, sg = out
+    np.testing.assert_array_equal(xg, x1)
+    np.testing.assert_array_equal(Pg, P1)
+    assert sg == s1
+
+
+def test_comm_init_one_rank_bitwise(L, c2):
+    """slio_comm_unique_id + slio_comm_init (the torchrun form) with one rank:
+    the update all-reduces in the library (reduce == NULL)."""
+    mp, fr, _ = c2
+    st = state_of(fr)
+    x1, P1, s1 = single_update(L, mp, fr, st)
+    lib = L.load()
+    h = mk(L, cell=C2_CELL)
+    try:
+        uid = (C.c_uint8 * L.SLIO_COMM_ID_BYTES)()
+        L.check(lib.slio_comm_unique_id(uid), "unique id")
+        L.check(lib.slio_comm_init(h, uid), "comm init")
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, fr.body) == 0
+        xs = slio_state(st)
+        P = np.eye(24) * 1e-2
+        stt = L.SlioIkfStats()
+        L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, 4, 0, L.SLIO_MODE_FIXED,
+                                           L.ALLREDUCE_FN(), None, C.byref(stt)), "comm update")
+        np.testing.assert_array_equal(state_array(xs), x1)
+        np.testing.assert_array_equal(P, P1)
+        assert (stt.passes, stt.searches, stt.valid_passes, stt.last_m) == s1
+    finally:
+        lib.slio_destroy(h)
