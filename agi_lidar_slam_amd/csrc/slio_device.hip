@@ -275,18 +275,6 @@ __device__ __host__ __forceinline__ int cell_coord(float p, float o, float inv_h
   return (int)t;
 }
 
-__global__ void k_cell_keys(const float* __restrict__ x, const float* __restrict__ y,
-                            const float* __restrict__ z, int64_t n, GridGeom g,
-                            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int cx = min(max(cell_coord(x[i], g.ox, g.inv_h), 0), g.dx - 1);
-  int cy = min(max(cell_coord(y[i], g.oy, g.inv_h), 0), g.dy - 1);
-  int cz = min(max(cell_coord(z[i], g.oz, g.inv_h), 0), g.dz - 1);
-  keys[i] = ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx + (uint32_t)cx;
-  vals[i] = (uint32_t)i;
-}
-
 // per-cell counts of SORTED keys (cell = key >> shift): one atomic per run of
 // equal cells inside a wavefront (sorted keys put up to 64 lanes on one
 // counter; per-lane atomics serialised there: 0.64 ms for the coarse level
@@ -307,15 +295,6 @@ __global__ void k_cell_hist_sorted(const K* __restrict__ keys, int64_t n, int sh
     const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll((long long)livem);
     atomicAdd(&counts[c], (uint32_t)(end - lane));
   }
-}
-
-__global__ void k_gather_sorted(const float* __restrict__ x, const float* __restrict__ y,
-                                const float* __restrict__ z, const uint32_t* __restrict__ order,
-                                int64_t n, float4* __restrict__ pts) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t o = order[i];
-  pts[i] = make_float4(x[o], y[o], z[o], __uint_as_float(o));
 }
 
 // block rows: entry sizes, then the fill, one thread per cell.  A source
@@ -407,51 +386,6 @@ __global__ void k_coarse_keys(const float4* __restrict__ pts, int64_t n, GridGeo
   vals[i] = (uint32_t)i;
 }
 
-__global__ void k_coarse_gather(const float4* __restrict__ pts, const uint32_t* __restrict__ order,
-                                int64_t n, float4* __restrict__ cpts) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t o = order[i];
-  const float4 p = pts[o];
-  cpts[i] = make_float4(p.x, p.y, p.z, __uint_as_float(o));
-}
-
-// tight bounding box and count of every coarse cell (one thread per cell)
-// tight box of every coarse cell: one wavefront per cell, lanes striding its
-// points (one thread per cell left the few dense cells -- ~400 points each
-// at C2 -- as a serial tail: 148 us per build)
-__global__ void k_coarse_boxes(const float4* __restrict__ cpts, const uint32_t* __restrict__ cstart,
-                               int64_t nc, float4* __restrict__ lo, float4* __restrict__ hi) {
-  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (c >= nc) return;
-  const uint32_t s = cstart[c], e = cstart[c + 1];
-  const float INF = __int_as_float(0x7f800000);
-  float l[3] = {INF, INF, INF}, u[3] = {-INF, -INF, -INF};
-  for (uint32_t p = s + lane; p < e; p += 64) {
-    const float4 v = cpts[p];
-    l[0] = fminf(l[0], v.x);
-    l[1] = fminf(l[1], v.y);
-    l[2] = fminf(l[2], v.z);
-    u[0] = fmaxf(u[0], v.x);
-    u[1] = fmaxf(u[1], v.y);
-    u[2] = fmaxf(u[2], v.z);
-  }
-  if (e - s > 1) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        l[a] = fminf(l[a], __shfl_xor(l[a], o, 64));
-        u[a] = fmaxf(u[a], __shfl_xor(u[a], o, 64));
-      }
-  }
-  if (lane == 0) {
-    lo[c] = make_float4(l[0], l[1], l[2], __uint_as_float(e - s));
-    hi[c] = make_float4(u[0], u[1], u[2], 0.0f);
-  }
-}
-
 // Coarse level without a sort.  A coarse cell (edge 4h, same origin) is the
 // 4x4x4 fine cells [4c, 4c + 4) per axis, clipped to the fine grid, so its
 // points are the fine runs of its 16 (y, z) rows -- each a contiguous x-range
@@ -485,7 +419,7 @@ __global__ void k_coarse_count(const uint32_t* __restrict__ start, GridGeom g, G
   cnt[c] = sum;
 }
 // one wavefront per coarse cell: copy its rows (.w = fine position) and form
-// its tight box (count in lo.w), as k_coarse_boxes does for sorted points
+// its tight box (count in lo.w)
 __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __restrict__ start, GridGeom g,
                               GridGeom cg, const uint32_t* __restrict__ cstart, int64_t nc,
                               float4* __restrict__ cpts, float4* __restrict__ lo, float4* __restrict__ hi) {

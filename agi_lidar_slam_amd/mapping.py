@@ -59,7 +59,7 @@ class LaserMapping:
     def __init__(self, filter_size_map_min: float = 0.5, cube_len: float = 1000.0,
                  det_range: float = DET_RANGE, maximum_iter: int = NUM_MAX_ITERATIONS,
                  extrinsic_est: bool = False, device: int = 0, max_points: int = 100000,
-                 grid_cell: float = 1.25):
+                 grid_cell: float = 0.0):  # 0: the library's auto edge (slio_params.grid_cell)
         self.filter_size_map_min = float(filter_size_map_min)
         self.cube_len = float(cube_len)
         self.det_range = float(det_range)

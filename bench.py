@@ -205,7 +205,7 @@ def bench_c3(args, rank, world, dev, dist):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "feature stage: k_fe_pick + k_fe_chain + k_fe_vrank + k_fe_voxel (one timed span)",
+            "kernel": "feature stage: k_fe_pick + k_fe_ring (one timed span)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -223,13 +223,120 @@ def bench_c3(args, rank, world, dev, dist):
     fe.close()
 
 
+def bench_c5(args, rank, world, dev, dist):
+    """C5 (BASELINE config 5): batched replay -- `--replicas`
+    DIFFERENT 100k-point scans in flight at once per GPU against one shared
+    50M-point map (agi_lidar_slam_amd.replay: one handle, stream and host
+    thread per scan, slio_map_share).  Replicas only: every rank replays its
+    own scans against its own map replica, no collective (weak scaling: 4
+    per GPU, 32 on 8 GPUs).  One step = one full update (4 IKF iterations) of
+    every replica; value = IKF iterations of all replicas of all ranks / the
+    max-over-ranks time.  Every replica's x and P are checked bitwise against
+    its own update run alone before the timed region."""
+    from agi_lidar_slam_amd import build, replay
+    import torch
+
+    if rank == 0:
+        build.build()
+    if world > 1:
+        dist.barrier()
+    t0 = time.time()
+    mp, frames = replay.replay_frames(args.map_points, args.scan_points, args.replicas,
+                                      cache_dir=args.cache_dir, first=rank * args.replicas)
+    log(f"[rank {rank}] map {mp.shape[0]} + {len(frames)} scans in {time.time() - t0:.1f}s")
+    rp = replay.Replay(mp, frames, device=dev, iters=args.iters, cell=args.cell)
+    cell_m = rp.cell()
+    rp.verify()
+    single = rp.solo_rate(max(10, args.steps // 4), args.warmup) if rank == 0 else None
+
+    def before():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def after(el):
+        torch.cuda.synchronize()
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    el = rp.run(args.steps, args.warmup, before, after)
+    same = rp.identical()
+    if world > 1:
+        t = torch.tensor([1 if same else 0], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        same = bool(t.item())
+    rp.close()
+    total = world * args.replicas * args.steps * args.iters / el
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        t0 = time.time()
+        T = O.Tree(mp)
+        log(f"[cpu] oracle kd-tree built in {time.time() - t0:.1f}s")
+        n = max(1, args.cpu_scans_c5)
+        t0 = time.perf_counter()
+        for k in range(n):
+            fr = frames[k % len(frames)]
+            st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth_t_li(), np.zeros(9),
+                                  [0, 0, -9.81]])
+            O.ikf_update(T, fr.body, st0, np.eye(24) * 1e-2, maximum_iter=args.iters, mode=1,
+                         reference_gain=1, threads=args.cpu_threads)
+        cel = time.perf_counter() - t0
+        cpu = {"value": n * args.iters / cel, "unit": "IKF iterations/s", "cores": args.cpu_threads,
+               "kind": "port",
+               "sample": (f"{n} scan updates x {args.iters} IKF iterations of the replay's scans, one at a "
+                          f"time, vs the {args.map_points}-pt map, {args.cpu_threads} OpenMP threads; host "
+                          f"{cpu_model()}")}
+    out = {
+        "metric": "IKF iterations/sec, batched replay of concurrent 100k-pt scans vs a shared 50M-pt map",
+        "value": total,
+        "unit": "IKF iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (kNN, plane) + f64 (Jacobian, reduction, 24x24 update)",
+        "data": "synthetic (seeded urban scene, distinct Avia-like rosette scans)",
+        "config": {
+            "workload": (f"C5: {args.replicas} concurrent distinct {args.scan_points}-pt scans per GPU vs a shared "
+                         f"{args.map_points}-pt map, {args.iters} IKF iterations per update, kNN every "
+                         "iteration"),
+            "map_points": args.map_points,
+            "scan_points": args.scan_points,
+            "replicas_per_gpu": args.replicas,
+            "grid_cell_m": cell_m,
+            "parallelism": (f"replicas: {args.replicas} per GPU x {world} GPUs, map replica per GPU, "
+                            "no collective"),
+            "results_identical_to_solo_runs": same,
+            "single_replica_value": single,
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if not same:
+        raise SystemExit("C5: a concurrent replica's result differs from its solo run")
+
+
+def synth_t_li():
+    from agi_lidar_slam_amd import synth
+    return synth.AVIA_T_LI
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--iters", type=int, default=4)
-    ap.add_argument("--map-points", type=int, default=10_000_000)
+    ap.add_argument("--map-points", type=int, default=None,
+                    help="default: 10M (c2), 50M (c5)")
     ap.add_argument("--scan-points", type=int, default=100_000)
     ap.add_argument("--cell", type=float, default=0.0,
                     help="map grid cell edge (speed only; results are exact at any edge); 0: the "
@@ -248,9 +355,17 @@ def main():
     ap.add_argument("--host-loop", action="store_true",
                     help="run the 24x24 step on the host after every pass (slio_ikf_update)")
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
-    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
                     help="c2: IKF iterations/s, 100k Avia scan vs 10M map (BASELINE.json metric); "
-                         "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan")
+                         "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan; "
+                         "c5: batched replay, --replicas concurrent distinct 100k scans per GPU vs a "
+                         "shared 50M map (BASELINE config 5: 32 scans on 8 GPUs = 4 per GPU)")
+    ap.add_argument("--replicas", type=int, default=4, help="c5: concurrent scans per GPU")
+    ap.add_argument("--cpu-scans-c5", type=int, default=4)
+    ap.add_argument("--reduce-hook", action="store_true",
+                    help="N > 1: all-reduce through a torch.distributed hook (slio_allreduce_fn) "
+                         "instead of the library's own RCCL communicator (slio_comm_init); implied by "
+                         "--dist-backend gloo (RCCL refuses two ranks on one device)")
     ap.add_argument("--cpu-scans-c3", type=int, default=300)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
@@ -268,11 +383,13 @@ def main():
     # one rank per GPU; the modulo only matters for a gloo rehearsal with more
     # ranks than devices (device_count() does not initialise the GPU here)
     dev = local_rank % max(1, torch.cuda.device_count()) if world > 1 else 0
+    if args.map_points is None:
+        args.map_points = 50_000_000 if args.workload == "c5" else 10_000_000
     if world > 1:
         torch.cuda.set_device(dev)
         dist.init_process_group(args.dist_backend if args.workload == "c2" else "gloo")
-    if args.workload == "c3":
-        bench_c3(args, rank, world, dev, dist)
+    if args.workload in ("c3", "c5"):
+        (bench_c3 if args.workload == "c3" else bench_c5)(args, rank, world, dev, dist)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -314,7 +431,19 @@ def main():
 
     reduce_cb = L.ALLREDUCE_FN()
     keep = []
-    if world > 1:
+    comm = "none"
+    if world > 1 and not args.reduce_hook and args.dist_backend == "nccl":
+        # the library's own communicator: rank 0's RCCL id to every rank,
+        # then each pass's all-reduce is enqueued inside slio_ikf_update_device
+        uid = (C.c_uint8 * L.SLIO_COMM_ID_BYTES)()
+        if rank == 0:
+            L.check(lib.slio_comm_unique_id(uid), "comm id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (C.c_uint8 * L.SLIO_COMM_ID_BYTES).from_buffer_copy(obj[0])
+        L.check(lib.slio_comm_init(h, uid), "comm init")
+        comm = "library RCCL communicator (slio_comm_init), one ncclAllReduce per iteration"
+    elif world > 1:
         # the library and the collective must share one stream: a stream of
         # our own made current (torch's default stream is handle 0, which
         # slio_set_stream reads as "the handle's own stream")
@@ -330,6 +459,8 @@ def main():
 
         reduce_cb = L.ALLREDUCE_FN(_allreduce)
         keep.append(reduce_cb)
+        comm = (f"torch.distributed {args.dist_backend} all_reduce through a slio_allreduce_fn hook"
+                + (" (RCCL)" if args.dist_backend == "nccl" else ""))
 
     st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9),
                           [0, 0, -9.81]])
@@ -390,11 +521,15 @@ def main():
     avg_kernel_s = (ms.value / max(nl.value, 1)) * 1e-3
     alg_bytes = BYTES_PER_SEARCH_PT * shard_pts
     achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else None
+    # HBM bytes per launch from the committed PMC summary (rocprofv3 --pmc
+    # cannot run inside this process): only for the same workload, one rank
+    # holding the whole scan, and the library built from the same sources
     traffic = None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(args.traffic_json) and world == 1 and shard_pts == args.scan_points:
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("scan_points") == args.scan_points and tj.get("map_points") == args.map_points:
+            if (tj.get("scan_points") == args.scan_points and tj.get("map_points") == args.map_points
+                    and tj.get("source_hash") == build.source_hash()):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -464,8 +599,8 @@ def main():
             "iterations_per_step": args.iters,
             "ikf_loop": "host" if args.host_loop else "device-resident",
             "grid_cell_m": cell_m,
-            "parallelism": (f"scan points sharded x{world}, map replicated, one RCCL all-reduce "
-                            "of 8x91 fp64 per iteration" if world > 1 else "single GPU"),
+            "parallelism": (f"scan points sharded x{world}, map replicated, one all-reduce of 8x91 fp64 "
+                            f"per iteration: {comm}" if world > 1 else "single GPU"),
             "effective_points": int(stats.last_m),
         },
         "roofline": {

@@ -1,4 +1,5 @@
-# usage: bash scripts/gpu_round.sh <tag> [tests] [sweep] [bench] [prof]
+# usage: bash scripts/gpu_round.sh <tag> <step>...   (one GPU box, steps chained, each under its own limit)
+# steps: tests smoke bench benchc3 benchc5 prof timeline solve ustamps pmc
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 tag=$1; shift
@@ -7,29 +8,33 @@ for step in "$@"; do
   case $step in
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
-      rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/${tag}_tests.log
-      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
-    fetests)
-      timeout -k 10 600 python -m pytest tests/test_gpu_frontend.py tests/test_gpu_lego.py -m gpu -q -rs > gpurun_out/${tag}_fetests.log 2>&1
-      rc=$?; echo "fetests rc=$rc"; tail -40 gpurun_out/${tag}_fetests.log
-      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+      rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/${tag}_tests.log; grep -E "FAILED|SKIPPED" gpurun_out/${tag}_tests.log | head
+      [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/${tag}_smoke.log; exit 6; }
-      tail -3 gpurun_out/${tag}_smoke.log ;;
-    sweep)
-      timeout -k 10 600 python scripts/sweep_search.py > gpurun_out/${tag}_sweep.log 2>&1 || { echo "sweep failed"; tail -20 gpurun_out/${tag}_sweep.log; exit 3; }
-      cat gpurun_out/${tag}_sweep.log | grep -v amdgpu.ids ;;
+      tail -1 gpurun_out/${tag}_smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py --steps 100 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 4; }
+      timeout -k 10 600 python bench.py --steps 200 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 4; }
       cat gpurun_out/${tag}_bench.json ;;
     benchc3)
       timeout -k 10 600 python bench.py --workload c3 --steps 500 --warmup 10 > gpurun_out/${tag}_benchc3.json 2> gpurun_out/${tag}_benchc3.err || { echo "benchc3 failed"; tail -20 gpurun_out/${tag}_benchc3.err; exit 4; }
       cat gpurun_out/${tag}_benchc3.json ;;
-    benchh)
-      timeout -k 10 600 python bench.py --steps 100 --warmup 5 --host-loop --no-cpu-baseline > gpurun_out/${tag}_benchh.json 2> gpurun_out/${tag}_benchh.err || { echo "benchh failed"; tail -20 gpurun_out/${tag}_benchh.err; exit 4; }
-      cat gpurun_out/${tag}_benchh.json ;;
+    benchc5)
+      timeout -k 10 900 python bench.py --workload c5 --steps 50 --warmup 3 > gpurun_out/${tag}_benchc5.json 2> gpurun_out/${tag}_benchc5.err || { echo "benchc5 failed"; tail -20 gpurun_out/${tag}_benchc5.err; exit 4; }
+      cat gpurun_out/${tag}_benchc5.json ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 5; }
-      find gpurun_out/${tag}_prof -name "*stats*" | head; for f in $(find gpurun_out/${tag}_prof -name "*kernel_stats.csv"); do head -8 $f; done ;;
+      for f in $(find gpurun_out/${tag}_prof -name "*kernel_stats.csv"); do head -8 $f; done ;;
+    timeline)
+      timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/${tag}_tl -o run --output-format csv -- python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-kernel-timing > gpurun_out/${tag}_tl.log 2>&1 || { echo "timeline failed"; tail -20 gpurun_out/${tag}_tl.log; exit 5; }
+      python scripts/timeline.py gpurun_out/${tag}_tl 320 | tee gpurun_out/${tag}_timeline.txt ;;
+    solve)
+      SLIO_LIB=agi_lidar_slam_amd/_abl/libslio_SOLVE.so timeout -k 10 200 python scripts/solve_stamps.py > gpurun_out/${tag}_solve.log 2>&1 || { echo "solve failed"; tail gpurun_out/${tag}_solve.log; exit 6; }
+      grep -v amdgpu.ids gpurun_out/${tag}_solve.log ;;
+    ustamps)
+      timeout -k 10 200 python scripts/stamps_update.py > gpurun_out/${tag}_ustamps.log 2>&1 || { echo "ustamps failed"; tail gpurun_out/${tag}_ustamps.log; exit 5; }
+      grep -v amdgpu.ids gpurun_out/${tag}_ustamps.log ;;
+    pmc)
+      bash scripts/pmc_search.sh ${tag} || exit $? ;;
   esac
 done

@@ -21,8 +21,13 @@ def main(out_json, *dirs):
     mean = {k: sum(v) / len(v) for k, v in vals.items()}
     fetch = mean.get("FETCH_SIZE")
     write = mean.get("WRITE_SIZE")
+    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+    from agi_lidar_slam_amd import build
     res = {
         "kernel": "k_search_pass",
+        # bench.py attaches hbm_bytes_per_launch only to runs of the library
+        # built from these sources
+        "source_hash": build.source_hash(),
         "map_points": 10_000_000,
         "scan_points": 100_000,
         "counters_mean_per_launch": mean,

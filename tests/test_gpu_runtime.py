@@ -306,11 +306,13 @@ def test_esekf_follows_map_rebuild(L, oracle_mod):
 
 
 def test_c5_50M_map_exact_and_replay(L, oracle_mod):
-    """C5's 50M-point map: a 100k scan's pass is bit-exact vs the oracle on a
-    4000-query sample (plus sortedness / selection properties over the whole
-    scan), and 8 replicas with distinct scans on the shared 50M map, run
-    concurrently, each equal their own run alone."""
-    from agi_lidar_slam_amd import synth
+    """C5 as BASELINE config 5 states it, per GPU: the shared 50M-point map at
+    the library's own cell edge (auto: 1.25 m at this size), a 100k scan's
+    pass bit-exact vs the oracle on a 4000-query sample (plus sortedness /
+    selection properties over the whole scan), then 4 DISTINCT 100k-point
+    scans replayed concurrently on the shared map (agi_lidar_slam_amd.replay,
+    what bench.py --workload c5 times), each equal to its own run alone."""
+    from agi_lidar_slam_amd import replay, synth
     lib = L.load()
     seed = 20261015
     mp, fr = synth.make_problem(50_000_000, 100_000, pattern="avia", seed=seed,
@@ -318,10 +320,13 @@ def test_c5_50M_map_exact_and_replay(L, oracle_mod):
     fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
     st = state_of(fr)
     T = oracle_mod.Tree(mp)
-    base = mk(L, cell=C2_CELL)
-    hs = []
+    base = mk(L, cell=0.0)   # the library's auto edge
+    rp = None
     try:
         upload_map(L, base, mp)
+        cell = C.c_float()
+        L.check(lib.slio_map_info(base, None, C.byref(cell), None), "map_info")
+        assert abs(cell.value - 1.25) < 1e-6, cell.value
         upload_scan(L, base, fr.body)
         s = iterate(L, base, st, True)
         idx, sqd, sel, pl, rs = results(L, base, fr.body.shape[0])
@@ -332,46 +337,22 @@ def test_c5_50M_map_exact_and_replay(L, oracle_mod):
         ridx, rsqd = T.knn(q, 5)
         np.testing.assert_array_equal(idx[pick], ridx)
         np.testing.assert_array_equal(sqd[pick], rsqd)
-        # replay: 8 distinct 50k-point scans of the same scene
-        scene = synth.make_scene(seed, 50_000_000)
-        frames = [synth.make_frame(scene, seed + 17 * k, 50_000, "avia") for k in range(8)]
-        hs = [mk(L, n_max=50_000, cell=C2_CELL) for _ in frames]
-        for h, f in zip(hs, frames):
-            L.check(lib.slio_map_share(h, base), "share")
-            assert upload_scan(L, h, f.body) == 0
-        cb = L.ALLREDUCE_FN()
-
-        def run(h, f, out, reps):
-            for _ in range(reps):
-                xs = slio_state(state_of(f))
-                P = np.eye(24) * 1e-2
-                stt = L.SlioIkfStats()
-                rc = lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, 4, 0,
-                                                L.SLIO_MODE_FIXED, cb, None, C.byref(stt))
-                out.append((rc, state_array(xs), P.copy()))
-
-        alone = []
-        for h, f in zip(hs, frames):
-            o = []
-            run(h, f, o, 1)
-            assert o[0][0] == 0, lib.slio_last_error()
-            alone.append(o[0])
-        outs = [[] for _ in hs]
-        th = [threading.Thread(target=run, args=(h, f, o, 2)) for h, f, o in zip(hs, frames, outs)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        for o, ref in zip(outs, alone):
-            assert len(o) == 2
-            for rc, x, P in o:
-                assert rc == 0
-                np.testing.assert_array_equal(x, ref[1])
-                np.testing.assert_array_equal(P, ref[2])
-        # the replicas converge near their own ground truth
-        for f, ref in zip(frames, alone):
-            assert np.abs(ref[1][0:3] - f.gt_pos).max() < 0.05
-    finally:
-        for h in reversed(hs):
-            lib.slio_destroy(h)
         lib.slio_destroy(base)
+        base = None
+        # replay: 4 distinct 100k scans of the same scene, concurrently
+        _, frames = replay.replay_frames(50_000_000, 100_000, 4, seed=seed, cache_dir="/tmp/slio_cache")
+        rp = replay.Replay(mp, frames, cell=0.0)
+        assert abs(rp.cell() - 1.25) < 1e-6
+        rp.verify()
+        rp.run(2, 0)
+        assert rp.identical()
+        # the replicas converge near their own ground truth
+        for f, (rx, _) in zip(frames, rp.ref):
+            x = np.frombuffer(rx, dtype=np.float64)
+            pos = x[0:3]   # slio_state: pos[3], rot[4], ...
+            assert np.abs(pos - f.gt_pos).max() < 0.05
+    finally:
+        if rp is not None:
+            rp.close()
+        if base is not None:
+            lib.slio_destroy(base)
