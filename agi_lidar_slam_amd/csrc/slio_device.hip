@@ -189,6 +189,7 @@ struct MapDev {
   hipEvent_t ready = nullptr;
   uint64_t epoch = 0;
   bool broken = false;  // an index rebuild failed part-way: unusable until a new upload
+  int64_t sequential_calls = 0;  // Add_Points calls that took k_ds_sequential (diagnostic)
   float cell0 = 1.0f;             // requested grid cell and cell budget (slio_params)
   int64_t max_cells = 0;
   // device allocations kept across index rebuilds (capacity in bytes): a
@@ -3830,15 +3831,223 @@ __global__ void k_map_delete(const float4* __restrict__ pts, uint8_t* __restrict
 }
 
 // downsample voxel key of a point: the three floor(p / ds) (ikd_Tree.cpp:430-441)
+__device__ __forceinline__ uint64_t ds_key(int64_t kx, int64_t ky, int64_t kz) {
+  return ((uint64_t)((kx + (1 << 20)) & 0x1FFFFF) << 42) | ((uint64_t)((ky + (1 << 20)) & 0x1FFFFF) << 21) |
+         (uint64_t)((kz + (1 << 20)) & 0x1FFFFF);
+}
+
 __global__ void k_ds_keys(const float4* __restrict__ in, int64_t n, float ds, uint64_t* __restrict__ keys,
                           uint32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = in[i];
   const int64_t kx = (int64_t)floorf(p.x / ds), ky = (int64_t)floorf(p.y / ds), kz = (int64_t)floorf(p.z / ds);
-  keys[i] = ((uint64_t)((kx + (1 << 20)) & 0x1FFFFF) << 42) | ((uint64_t)((ky + (1 << 20)) & 0x1FFFFF) << 21) |
-            (uint64_t)((kz + (1 << 20)) & 0x1FFFFF);
+  keys[i] = ds_key(kx, ky, kz);
   vals[i] = (uint32_t)i;
+}
+
+// The downsample box of key (kx, ky, kz): [floor * ds, floor * ds + ds) per
+// axis in float, as Add_Points forms it from a point of that key
+// (ikd_Tree.cpp:430-441); Search_by_range's predicate is half-open
+// (:1127-1128).  For a downsample size that is not a power of two,
+// neighbouring float boxes can overlap by an ulp (or leave an ulp gap).
+struct DsBox {
+  float lo[3], hi[3];
+};
+__device__ __forceinline__ DsBox ds_box(int64_t kx, int64_t ky, int64_t kz, float ds) {
+  DsBox b;
+  const int64_t k[3] = {kx, ky, kz};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    b.lo[a] = (float)k[a] * ds;
+    b.hi[a] = b.lo[a] + ds;
+  }
+  return b;
+}
+__device__ __forceinline__ bool ds_inside(const DsBox& b, float x, float y, float z) {
+  return b.lo[0] <= x && b.hi[0] > x && b.lo[1] <= y && b.hi[1] > y && b.lo[2] <= z && b.hi[2] > z;
+}
+__device__ __forceinline__ int64_t ds_find(const uint64_t* __restrict__ keys, int64_t n, uint64_t k) {
+  int64_t a = 0, b = n;  // first index with keys[i] >= k
+  while (a < b) {
+    const int64_t m = (a + b) >> 1;
+    if (keys[m] < k) a = m + 1; else b = m;
+  }
+  return (a < n && keys[a] == k) ? a : -1;
+}
+// p lies in the box of a key other than `own` that this call also holds a
+// point of (the boxes of the 27 keys around p's own key)
+__device__ __forceinline__ bool ds_shared(float x, float y, float z, uint64_t own, float ds,
+                                          const uint64_t* __restrict__ keys, int64_t n) {
+  const int64_t kx = (int64_t)floorf(x / ds), ky = (int64_t)floorf(y / ds), kz = (int64_t)floorf(z / ds);
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const uint64_t k = ds_key(kx + dx, ky + dy, kz + dz);
+        if (k == own || !ds_inside(ds_box(kx + dx, ky + dy, kz + dz, ds), x, y, z)) continue;
+        if (ds_find(keys, n, k) >= 0) return true;
+      }
+  return false;
+}
+
+// Groups are independent (k_ds_groups) unless some point -- stored and alive
+// in a group's box, or one of the call's new points -- lies in the boxes of
+// two keys of this call (float boxes overlapping by an ulp, or a new point
+// past its own box's upper face inside the next box), or a new point lies
+// outside its own box (an ulp gap): then the call's sequential order
+// matters.  One thread per group; flag[0] = 1 on any.
+__global__ void k_ds_conflicts(const float4* __restrict__ in, const uint64_t* __restrict__ keys,
+                               const uint32_t* __restrict__ order, int64_t n, float ds, MapView map,
+                               const uint8_t* __restrict__ keep, unsigned long long* __restrict__ flag) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= n || (i0 > 0 && keys[i0] == keys[i0 - 1])) return;
+  const uint64_t own = keys[i0];
+  bool hit = false;
+  {
+    const float4 q0 = in[order[i0]];
+    const DsBox ob = ds_box((int64_t)floorf(q0.x / ds), (int64_t)floorf(q0.y / ds), (int64_t)floorf(q0.z / ds), ds);
+    for (int64_t j = i0; j < n && keys[j] == own && !hit; ++j) {
+      const float4 q = in[order[j]];
+      // a new point outside its own box (an ulp gap past the upper face):
+      // the group's later points do not see it (k_ds_groups assumes they do)
+      hit = !ds_inside(ob, q.x, q.y, q.z) || ds_shared(q.x, q.y, q.z, own, ds, keys, n);
+    }
+  }
+  if (!hit && map.n > 0) {
+    const float4 q0 = in[order[i0]];
+    const DsBox bx = ds_box((int64_t)floorf(q0.x / ds), (int64_t)floorf(q0.y / ds), (int64_t)floorf(q0.z / ds), ds);
+    const GridGeom g = map.g;
+    int ca[3], cb[3];
+    const float og[3] = {g.ox, g.oy, g.oz};
+    const int dg[3] = {g.dx, g.dy, g.dz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      ca[a] = min(max(cell_coord(bx.lo[a], og[a], g.inv_h), 0), dg[a] - 1);
+      cb[a] = min(max(cell_coord(bx.hi[a], og[a], g.inv_h), 0), dg[a] - 1);
+    }
+    for (int z = ca[2]; z <= cb[2] && !hit; ++z)
+      for (int y = ca[1]; y <= cb[1] && !hit; ++y) {
+        const uint32_t rb = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx;
+        for (uint32_t ps = map.start[rb + ca[0]]; ps < map.start[rb + cb[0] + 1] && !hit; ++ps) {
+          if (!keep[ps]) continue;
+          const float4 p = map.pts[ps];
+          if (ds_inside(bx, p.x, p.y, p.z)) hit = ds_shared(p.x, p.y, p.z, own, ds, keys, n);
+        }
+      }
+  }
+  if (hit) atomicExch(flag, 1ull);
+}
+
+// The call's exact sequential Add_Points (ikd_Tree.cpp:428-512, the set
+// restatement of oracle/map_oracle.cpp) by ONE thread, point by point in list
+// order, for a call whose groups interact (k_ds_conflicts): stored points in
+// storage order (ascending id), then this call's earlier survivors in list
+// order; the new point wins ties, a stored one only when strictly nearer.
+// Slow (one thread) and rare: only ulp-wide float overlaps of downsample
+// boxes can interact, and only for a size that is not a power of two.
+__global__ void k_ds_sequential(const float4* __restrict__ in, const uint64_t* __restrict__ keys,
+                                const uint32_t* __restrict__ order, int64_t n, float ds, MapView map,
+                                uint8_t* __restrict__ keep, uint32_t* __restrict__ surv,
+                                unsigned long long* __restrict__ counter) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const GridGeom g = map.g;
+  const float og[3] = {g.ox, g.oy, g.oz};
+  const int dg[3] = {g.dx, g.dy, g.dz};
+  unsigned long long ops = 0;
+  for (int64_t li = 0; li < n; ++li) {
+    const float4 q = in[li];
+    const int64_t kx = (int64_t)floorf(q.x / ds), ky = (int64_t)floorf(q.y / ds), kz = (int64_t)floorf(q.z / ds);
+    const DsBox bx = ds_box(kx, ky, kz, ds);
+    const float mx = (float)((double)bx.lo[0] + (double)(bx.hi[0] - bx.lo[0]) / 2.0);
+    const float my = (float)((double)bx.lo[1] + (double)(bx.hi[1] - bx.lo[1]) / 2.0);
+    const float mz = (float)((double)bx.lo[2] + (double)(bx.hi[2] - bx.lo[2]) / 2.0);
+    int ca[3], cb[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      ca[a] = min(max(cell_coord(bx.lo[a], og[a], g.inv_h), 0), dg[a] - 1);
+      cb[a] = min(max(cell_coord(bx.hi[a], og[a], g.inv_h), 0), dg[a] - 1);
+    }
+    // winner: the new point unless a storage entry is strictly nearer; among
+    // entries, the first minimum in storage order
+    int64_t cnt = 0;
+    float bd = map_dist(q.x, q.y, q.z, mx, my, mz);
+    int wk = 0;  // 0: the new point, 1: stored (bpos), 2: this call's earlier survivor (blj)
+    uint32_t bid = 0;
+    int64_t bpos = -1, blj = -1;
+    float4 bp = q;
+    if (map.n > 0)
+      for (int z = ca[2]; z <= cb[2]; ++z)
+        for (int y = ca[1]; y <= cb[1]; ++y) {
+          const uint32_t rb = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx;
+          for (uint32_t ps = map.start[rb + ca[0]]; ps < map.start[rb + cb[0] + 1]; ++ps) {
+            if (!keep[ps]) continue;
+            const float4 p = map.pts[ps];
+            if (!ds_inside(bx, p.x, p.y, p.z)) continue;
+            ++cnt;
+            const float d = map_dist(p.x, p.y, p.z, mx, my, mz);
+            const uint32_t id = __float_as_uint(p.w);
+            if (d < bd || (wk == 1 && d == bd && id < bid)) {
+              bd = d;
+              bid = id;
+              bpos = ps;
+              bp = p;
+              wk = 1;
+            }
+          }
+        }
+    // earlier survivors of this call inside the box: their keys are among
+    // the 27 around q's key; storage order after every stored point, in list order
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          int64_t j = ds_find(keys, n, ds_key(kx + dx, ky + dy, kz + dz));
+          if (j < 0) continue;
+          const uint64_t k = keys[j];
+          for (; j < n && keys[j] == k; ++j) {
+            const uint32_t lj = order[j];
+            if ((int64_t)lj >= li || !surv[lj]) continue;
+            const float4 p = in[lj];
+            if (!ds_inside(bx, p.x, p.y, p.z)) continue;
+            ++cnt;
+            const float d = map_dist(p.x, p.y, p.z, mx, my, mz);
+            // strictly nearer than the best so far, or as near as the best
+            // earlier survivor but earlier in list order (storage order)
+            if (d < bd || (wk == 2 && d == bd && (int64_t)lj < blj)) {
+              bd = d;
+              blj = lj;
+              bp = p;
+              wk = 2;
+            }
+          }
+        }
+    if (cnt > 1 || map_same(q.x, q.y, q.z, bp.x, bp.y, bp.z)) {
+      ++ops;
+      // every storage entry but the winner goes
+      if (map.n > 0)
+        for (int z = ca[2]; z <= cb[2]; ++z)
+          for (int y = ca[1]; y <= cb[1]; ++y) {
+            const uint32_t rb = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx;
+            for (uint32_t ps = map.start[rb + ca[0]]; ps < map.start[rb + cb[0] + 1]; ++ps)
+              if (keep[ps] && !(wk == 1 && (int64_t)ps == bpos) && ds_inside(bx, map.pts[ps].x, map.pts[ps].y,
+                                                                                  map.pts[ps].z))
+                keep[ps] = 0;
+          }
+      for (int dz = -1; dz <= 1; ++dz)
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            int64_t j = ds_find(keys, n, ds_key(kx + dx, ky + dy, kz + dz));
+            if (j < 0) continue;
+            const uint64_t k = keys[j];
+            for (; j < n && keys[j] == k; ++j) {
+              const uint32_t lj = order[j];
+              if ((int64_t)lj >= li || !surv[lj] || (wk == 2 && (int64_t)lj == blj)) continue;
+              if (ds_inside(bx, in[lj].x, in[lj].y, in[lj].z)) surv[lj] = 0;
+            }
+          }
+      if (wk == 0) surv[li] = 1;
+    }
+  }
+  counter[0] = ops;
 }
 
 // One thread per voxel group of the sorted list (the points of one
@@ -3852,6 +4061,7 @@ __global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __res
                             unsigned long long* __restrict__ counter) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i0 >= n || (i0 > 0 && keys[i0] == keys[i0 - 1])) return;
+  if (counter[1]) return;  // interacting groups: k_ds_sequential instead
   const float4 q0 = in[order[i0]];
   float lo[3], hi[3];
   const float c0[3] = {q0.x, q0.y, q0.z};
@@ -4219,7 +4429,7 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     hipError_t e;
     if ((e = hipMalloc(&k0, 8 * n)) || (e = hipMalloc(&k1, 8 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
         (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&surv, 4 * n)) || (e = hipMalloc(&rank, 4 * n)) ||
-        (e = hipMalloc(&dcount, 8))) {
+        (e = hipMalloc(&dcount, 16))) {
       set_error(std::string("slio map: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
       break;
@@ -4234,21 +4444,33 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     const int nb = grid_blocks(n);
     k_ds_keys<<<nb, 256, 0, st>>>(in, n, ds, k0, v0);
     if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 63, st)) ||
-        (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 8, st))) {
+        (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 16, st))) {
       set_error(std::string("slio map: sort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
     }
+    k_ds_conflicts<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, dcount + 1);
     k_ds_groups<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, surv, dcount);
     uint32_t total = 0;
     if ((rc = scan_flags(surv, rank, n, st, &total))) break;
-    unsigned long long ops = 0;
-    if ((e = hipMemcpyAsync(&ops, dcount, 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+    unsigned long long ops[2] = {0, 0};
+    if ((e = hipMemcpyAsync(ops, dcount, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
       set_error(std::string("slio map: groups: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
     }
-    *counter = (int64_t)ops;
+    if (ops[1]) {
+      // interacting groups (k_ds_conflicts): the exact sequential order
+      k_ds_sequential<<<1, 1, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, surv, dcount);
+      if ((rc = scan_flags(surv, rank, n, st, &total))) break;
+      if ((e = hipMemcpyAsync(ops, dcount, 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+        set_error(std::string("slio map: sequential Add_Points: ") + hipGetErrorString(e));
+        rc = SLIO_EDEVICE;
+        break;
+      }
+      ++m.sequential_calls;
+    }
+    *counter = (int64_t)ops[0];
     if ((rc = add_reserve(m, total, st))) break;
     k_append<<<nb, 256, 0, st>>>(in, surv, rank, n, m.add4, m.akeep, m.nadd, m.next_id);
     if ((e = hipGetLastError())) {

@@ -288,3 +288,116 @@ def test_voxel_scan_feeds_update(L, oracle_mod):
         kf.close()
     np.testing.assert_array_equal(out[0], out[1])
     kd.close()
+
+
+def _box_edges(ds, ks):
+    """The float faces of the downsample boxes of integer keys ks (Add_Points
+    forms [floor(p / ds) * ds, + ds) in float, ikd_Tree.cpp:430-441) and their
+    neighbouring floats."""
+    ds = np.float32(ds)
+    lo = (ks.astype(np.float32) * ds).astype(np.float32)
+    hi = (lo + ds).astype(np.float32)
+    vals = np.concatenate([lo, hi, np.nextafter(lo, np.float32(-np.inf)), np.nextafter(hi, np.float32(-np.inf)),
+                           np.nextafter(lo, np.float32(np.inf)), (lo + ds / 2).astype(np.float32)])
+    return vals.astype(np.float32)
+
+
+@pytest.mark.parametrize("ds", [0.5, 0.1, 0.3])
+def test_add_points_on_box_faces_vs_oracle(L, oracle_mod, ds):
+    """Add_Points with downsample on points placed exactly on the float faces
+    of the downsample boxes and one ulp either side.  With ds = 0.1 or 0.3
+    neighbouring float boxes overlap by an ulp (box 6 of 0.1 is [0.6,
+    0.70000005), box 7 starts at 0.7) or leave an ulp gap, so a point can lie
+    in two boxes of one call and the call's sequential order decides
+    (k_ds_conflicts -> k_ds_sequential); 0.5 tiles exactly.  Stored and new
+    points, several calls: the device map equals the oracle's bit for bit
+    (ikd_Tree.cpp:419-512 and the Search_by_range predicate
+    :1127-1128)."""
+    rng = np.random.default_rng(int(ds * 1000))
+    ks = np.arange(-40, 40)
+    edges = _box_edges(ds, ks)
+    mid = (np.float32(ds) * np.arange(-40, 40).astype(np.float32) + np.float32(ds) / 2).astype(np.float32)
+
+    def pick(n, p_edge):
+        out = np.empty((n, 3), np.float32)
+        for a in range(3):
+            e = rng.random(n) < p_edge
+            out[:, a] = np.where(e, rng.choice(edges, n), rng.choice(mid, n) + rng.uniform(-ds / 3, ds / 3, n))
+        return out.astype(np.float32)
+
+    base = pick(4000, 0.6)
+    # an x-overlap of boxes k and k+1 (none for 0.5): a stored point on it
+    f = np.float32(ds)
+    kov = [k for k in range(1, 200) if np.float32(np.float32(k) * f + f) > np.float32(np.float32(k + 1) * f)]
+    if kov:
+        k = kov[0]
+        lo1 = np.float32(np.float32(k + 1) * f)
+        ym = np.float32(np.float32(2) * f + f / 2)
+        base[0] = [lo1, ym, ym]
+    h = mk(L, n_max=4000, cell=1.0)
+    try:
+        upload_map(L, h, base)
+        om = oracle_mod.Map(base)
+        for call in range(4):
+            new = pick(3000, 0.6)
+            # the construction that separates sequential from independent
+            # groups: a stored point in two boxes, one new point per box, the
+            # second box's new point farther from its centre than the stored one
+            if kov:
+                lo0 = np.float32(np.float32(k) * f)
+                new[:2] = [[lo0 + f / 2, ym, ym], [lo1 + f / 2, ym + f * 0.4, ym + f * 0.4]]
+            new[2] = [edges[0], edges[1], edges[2]]
+            got = add(L, h, new, True, ds)
+            ref = om.add_points(new, True, ds)
+            assert got == ref, (call, got, ref)
+            assert_same_map(L, h, om)
+    finally:
+        L.load().slio_destroy(h)
+
+
+def test_exact_distance_tie_and_map_incremental(L, oracle_mod):
+    """A documented deviation made visible: exact squared-distance ties for
+    the 5th neighbour.  The device breaks them by position in its cell-sorted
+    map (cell, then map index), the reference ikd-Tree by its traversal /
+    MANUAL_HEAP order (oracle/slio_oracle.cpp restates it).  Six map points
+    at exactly distance 1 from a scan point (the axis points) plus a far
+    background: both sides return five neighbours at squared distance 1.0
+    (bitwise), possibly not the same five; map_incremental's decision for the
+    point (laserMapping.cpp:391-422: the nearest neighbour against the voxel
+    centre, then any of the five nearer the centre than the point) does not
+    depend on which five: every axis point is 0.6875 or more from the centre
+    (0.25, 0.25, 0.25), the point 0.1875 -- the device's map after
+    map_incremental (its own Nearest_Points) equals the oracle's (driven by
+    the oracle's own Nearest_Points)."""
+    from test_gpu_parity import IDENT, iterate, results, upload_scan
+    axis = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float32)
+    rng = np.random.default_rng(3)
+    far = rng.uniform(5, 20, (2000, 3)).astype(np.float32) * rng.choice([-1, 1], (2000, 3)).astype(np.float32)
+    base = np.concatenate([far[:1000], axis, far[1000:]]).astype(np.float32)
+    scan = np.zeros((1, 3), np.float32)
+    st = IDENT.copy()
+    st[11:14] = 0.0   # T_LI = 0: the world point is the body point
+    h = mk(L, n_max=16, cell=1.0)
+    try:
+        upload_map(L, h, base)
+        om = oracle_mod.Map(base)
+        assert upload_scan(L, h, scan) == 0
+        iterate(L, h, st, True)
+        idx, sqd, sel, pl, rs = results(L, h, 1)
+        T = oracle_mod.Tree(base)
+        ridx, rsqd = T.knn(oracle_mod.body_to_world(st, scan), 5)
+        np.testing.assert_array_equal(sqd, rsqd)                  # the same five distances, bitwise
+        np.testing.assert_array_equal(sqd[0], np.ones(5, np.float32))
+        dev5, orc5 = set(idx[0].tolist()), set(ridx[0].tolist())
+        assert dev5 <= set(range(1000, 1006)) and orc5 <= set(range(1000, 1006))
+        print(f"device keeps axis points {sorted(i - 1000 for i in dev5)}, the oracle "
+              f"{sorted(i - 1000 for i in orc5)} (ids of the six tied points: 1000..1005)")
+        xs = __import__("test_gpu_runtime").slio_state(st)
+        counts = np.zeros(3, np.int64)
+        L.check(L.load().slio_map_incremental(h, C.byref(xs), 0.5, 1, L.i64ptr(counts)), "incremental")
+        ref = om.incremental(st, scan, ridx.astype(np.int32), 0.5, True, 0.5)
+        np.testing.assert_array_equal(counts, ref)
+        assert counts[0] + counts[1] == 1   # the point is added either way
+        assert_same_map(L, h, om)
+    finally:
+        L.load().slio_destroy(h)
