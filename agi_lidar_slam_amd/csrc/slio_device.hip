@@ -2000,6 +2000,73 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
   RSTAMP(3);
 }
 
+// The pass total and the filter step, by the workgroup that summed the last
+// segment row: thread k < 91 loads the 64 segment values of product k (sc1:
+// written by other workgroups of this launch) and adds them in registers (8
+// super rows, then their ordered total -- the tree step_totals uses); the
+// other 165 threads load the control block meanwhile (one round trip, no LDS
+// staging of the rows).  DXN_SC1: dx_new was written in this launch (by
+// block 0 of a fused search pass), so it is read past the L2 as well.
+template <int NT, int D, bool DXN_SC1>
+__device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, double* super_out, IkfCtl* ctl,
+                                           const IkfCtl* src, IkfCtl* hblk, double R, int iter, int maxit) {
+  const int t = threadIdx.x;
+  if (t < SLIO_NPROD) {
+    double v[kNSeg];
+#pragma unroll
+    for (int e = 0; e < kNSeg; ++e) v[e] = ld_sc1(seg_out + e * SLIO_NPROD + t);
+    double sp[SLIO_NSUPER];
+#pragma unroll
+    for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
+      double a = v[ss * kSuperSeg];
+#pragma unroll
+      for (int q = 1; q < kSuperSeg; ++q) a = a + v[ss * kSuperSeg + q];
+      sp[ss] = a;
+    }
+    double a = sp[0];
+#pragma unroll
+    for (int ss = 1; ss < SLIO_NSUPER; ++ss) a = a + sp[ss];
+    L.tot[t] = a;
+    if (t < SLIO_NHTH)
+      L.Mt[t] = a / R;
+    else if (t < SLIO_NHTH + 12)
+      L.hR[t - SLIO_NHTH] = a / R;
+#pragma unroll
+    for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
+  } else {
+    constexpr int NC = NT - SLIO_NPROD, nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
+    constexpr int kDxn = nC - CtlList<D>::nD;  // dx_new: the list's last 24 entries
+    const int tt = t - SLIO_NPROD;
+    const bool first = src != ctl;
+    const gdouble* gc = (const gdouble*)(const double*)src;
+    double cv[kC];
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int e = tt + u * NC;
+      if (DXN_SC1 && e >= kDxn)
+        cv[u] = e < nC ? ld_sc1(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : 0.0;
+      else
+        cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
+    }
+    typedef __attribute__((address_space(1))) int32_t gint;
+    const int32_t fl = tt < 8 ? ((const gint*)(const int32_t*)&src->converge)[tt] : 0;
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int e = tt + u * NC;
+      if (e < nC) {
+        ctl_dst<D>(L, e) = cv[u];
+        if (first) reinterpret_cast<double*>(ctl)[ctl_src<D>(e)] = cv[u];  // keep it in HBM
+      }
+    }
+    if (tt < 8) L.fl[tt] = fl;
+    if (first && tt == 0) ctl->singular = 0;
+  }
+  __syncthreads();
+  SSTAMP(4);
+  if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
+  ikf_step<NT, D>(ctl, hblk, R, iter, maxit, L);
+}
+
 template <int LPQ>
 constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
 
@@ -2007,7 +2074,9 @@ constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
 // device-resident pass runs at, for that pass's filter step: formed by block
 // 0 of the pass kernel (lanes 0..23 the vector blocks, lanes 32 / 64 the
 // two rotations, on different wavefronts) while the pass itself runs, off
-// the filter step's critical path.  Needs >= 128 threads.
+// the filter step's critical path.  Needs >= 128 threads.  Stored
+// write-through (sc1): a fused pass's filter step reads it in the same launch,
+// possibly from another XCD.
 __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
   if (blockIdx.x != 0) return;
   const int t = threadIdx.x;
@@ -2016,7 +2085,7 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
     if (k < 3 || k >= 9) {
       const double* xs = reinterpret_cast<const double*>(&ctl->x);
       const double* ps = reinterpret_cast<const double*>(&ctl->xprop);
-      ctl->dxn[k] = xs[state_off(k)] - ps[state_off(k)];
+      st_sc1(&ctl->dxn[k], xs[state_off(k)] - ps[state_off(k)]);
     }
   } else if (t == 32 || t == 64) {
     const int u = t == 32;
@@ -2024,10 +2093,84 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
     const double* q2 = u ? ctl->xprop.rli : ctl->xprop.rot;
     double d[3];
     so3_boxminus(Quat{q1[0], q1[1], q1[2], q1[3]}, Quat{q2[0], q2[1], q2[2], q2[3]}, d);
-    ctl->dxn[3 + 3 * u] = d[0];
-    ctl->dxn[4 + 3 * u] = d[1];
-    ctl->dxn[5 + 3 * u] = d[2];
+    st_sc1(&ctl->dxn[3 + 3 * u], d[0]);
+    st_sc1(&ctl->dxn[4 + 3 * u], d[1]);
+    st_sc1(&ctl->dxn[5 + 3 * u], d[2]);
   }
+}
+
+// Fused pass (single rank, device-resident update, the filter step in the
+// pass's own launch): what the search workgroups need to finish the pass's
+// sums and run its filter step.  Segment row b = 8 s + g of super-chunk s
+// sums chunks c0 + g, c0 + g + 8, ... (k_super_sums' order); the workgroup
+// that completes a segment's last chunk sums the row, and the one that
+// completes the 64th row runs final_step.
+struct FuseArgs {
+  double* seg_out;    // 64 segment rows
+  double* super_out;  // 8 super rows (slio_super_download)
+  const IkfCtl* src;  // control block source (ctl: passes after the first)
+  IkfCtl* hblk;       // mapped host block
+  uint32_t* cnt;      // [0] row arrivals, [4..6] far queue, [kSegCnt + b] chunk arrivals of row b
+  double R;
+  int iter, maxit;
+  int64_t C;          // chunks of the scan
+};
+constexpr int kSegCnt = 16;
+constexpr int kCountWords = kSegCnt + kNSeg;
+
+// the segment row of chunk c (single rank) and its number of chunks
+__device__ __forceinline__ int seg_of_chunk(int64_t C, int64_t c, int64_t& lim) {
+  int s = 0;
+#pragma unroll
+  for (int q = 1; q < SLIO_NSUPER; ++q) s = super_lo(C, q) <= c ? q : s;
+  const int64_t c0 = super_lo(C, s), c1 = super_lo(C, s + 1);
+  const int g = (int)((c - c0) % kSuperSeg);
+  lim = (c1 - c0 - g + kSuperSeg - 1) / kSuperSeg;
+  return s * kSuperSeg + g;
+}
+
+// After the chunk partial is stored (sc1): arrival on the chunk's segment row;
+// the last arrival sums the row, and the last row runs the filter step.
+// Every thread of the workgroup calls it.
+template <int NT>
+__device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl,
+                                           const double* chunk_part, int64_t chunk) {
+  const int t = threadIdx.x;
+  int64_t lim;
+  const int b = seg_of_chunk(fa.C, chunk, lim);
+  drain_stores();
+  __syncthreads();
+  if (t == 0) bcast = (int)arrive(fa.cnt + kSegCnt + b);
+  __syncthreads();
+  if (bcast != (int)lim - 1) return;
+  if (t < SLIO_NPROD) {
+    const int s = b / kSuperSeg, g = b - s * kSuperSeg;
+    const double* p = chunk_part + (super_lo(fa.C, s) + g) * SLIO_NPROD + t;
+    constexpr int kJ = 16;  // C2's 100k-point scan has <= 13 chunks per segment: one round trip
+    double acc = 0.0;
+    for (int64_t j0 = 0; j0 < lim; j0 += kJ) {
+      double v[kJ];
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) v[j] = (j0 + j < lim) ? ld_sc1(p + (j0 + j) * (kSuperSeg * SLIO_NPROD)) : 0.0;
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) acc = acc + v[j];
+    }
+    st_sc1(fa.seg_out + b * SLIO_NPROD + t, acc);
+  }
+  if (t == 0) reset_counter(fa.cnt + kSegCnt + b);
+  drain_stores();
+  __syncthreads();
+  if (t == 0) bcast = (int)arrive(fa.cnt);
+  __syncthreads();
+  if (bcast != kNSeg - 1) return;
+  if (t == 0) {
+    reset_counter(fa.cnt);
+    // the pass's number of far queries (slio_far_queries); queue reset
+    st_sc1_u32(fa.cnt + 6, ld_sc1_u32(fa.cnt + 5));
+    st_sc1_u32(fa.cnt + 4, 0u);
+    st_sc1_u32(fa.cnt + 5, 0u);
+  }
+  final_step<NT, 6, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
 }
 
 // One h_share_model search pass over one 128-point chunk.
@@ -2040,10 +2183,11 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
 #ifndef SLIO_RL8_MAX
 #define SLIO_RL8_MAX 8
 #endif
-template <int LPQ, int U, bool SPHERE, bool DEVPOSE>
+template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE = false>
 __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
     const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
-    const PassOut out) {
+    const PassOut out, const FuseArgs fa) {
+  static_assert(!FUSE || (DEVPOSE && search_block<LPQ>() == kSolveThreads), "fused pass: device pose, 256 threads");
   // DEVPOSE: pose and pass selection come from the device-resident update
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
@@ -2082,9 +2226,11 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     uint8_t far_slot[SLIO_CHUNK];
     uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
   };
-  __shared__ struct {
+  __shared__ union {
     SearchLds s;
+    StepLds L;  // a fused pass's filter step, after the search is done
   } lds;
+  __shared__ int fuse_bcast;
   auto& rows = lds.s.rr.rows;
   auto& ref = lds.s.rr.ref;
   auto& part = lds.s.part;
@@ -2504,8 +2650,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
-  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
+  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, FUSE);
   if (tid == 0) STAMP(3);
+  if constexpr (FUSE) fused_tail<NT>(lds.L, fuse_bcast, fa, cfg.ctl, out.chunk_part, chunk);
 }
 
 // Nearest_Points ids and pointSearchSqDis of the last search pass, derived
@@ -2693,60 +2840,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_super_sums(
   if (D) SSTAMP(2);
   if (t == 0) reset_counter(cnt);
   if constexpr (D > 0) {
-    // one round trip, no LDS staging of the rows: thread k < 91 loads the
-    // 64 segment values of product k and adds them in registers (8 super
-    // rows, then their ordered total -- the tree step_totals uses); the
-    // other 165 threads load the control block meanwhile
-    if (t < SLIO_NPROD) {
-      double v[kNSeg];
-#pragma unroll
-      for (int e = 0; e < kNSeg; ++e) v[e] = ld_sc1(seg_out + e * SLIO_NPROD + t);
-      double sp[SLIO_NSUPER];
-#pragma unroll
-      for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
-        double a = v[ss * kSuperSeg];
-#pragma unroll
-        for (int q = 1; q < kSuperSeg; ++q) a = a + v[ss * kSuperSeg + q];
-        sp[ss] = a;
-      }
-      double a = sp[0];
-#pragma unroll
-      for (int ss = 1; ss < SLIO_NSUPER; ++ss) a = a + sp[ss];
-      L.tot[t] = a;
-      if (t < SLIO_NHTH)
-        L.Mt[t] = a / R;
-      else if (t < SLIO_NHTH + 12)
-        L.hR[t - SLIO_NHTH] = a / R;
-#pragma unroll
-      for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
-    } else {
-      constexpr int NC = NT - SLIO_NPROD, nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
-      const int tt = t - SLIO_NPROD;
-      const bool first = src != ctl;
-      const gdouble* gc = (const gdouble*)(const double*)src;
-      double cv[kC];
-#pragma unroll
-      for (int u = 0; u < kC; ++u) {
-        const int e = tt + u * NC;
-        cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
-      }
-      typedef __attribute__((address_space(1))) int32_t gint;
-      const int32_t fl = tt < 8 ? ((const gint*)(const int32_t*)&src->converge)[tt] : 0;
-#pragma unroll
-      for (int u = 0; u < kC; ++u) {
-        const int e = tt + u * NC;
-        if (e < nC) {
-          ctl_dst<D>(L, e) = cv[u];
-          if (first) reinterpret_cast<double*>(ctl)[ctl_src<D>(e)] = cv[u];  // keep it in HBM
-        }
-      }
-      if (tt < 8) L.fl[tt] = fl;
-      if (first && tt == 0) ctl->singular = 0;
-    }
-    __syncthreads();
-    SSTAMP(4);
-    if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
-    ikf_step<NT, D>(ctl, hblk, R, iter, maxit, L);
+    final_step<NT, D, false>(L, seg_out, super_out, ctl, src, hblk, R, iter, maxit);
   } else {
     constexpr int kR = (kNSeg * SLIO_NPROD + NT - 1) / NT;
     double rv[kR];
@@ -3052,7 +3146,8 @@ static int build_blk(MapDev& m, hipStream_t st, const char* who);
 
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
                         int extrinsic_est, const SolveArgs* sa = nullptr,
-                        bool with_super = true, bool knn_only = false, const ScanDev* sd = nullptr) {
+                        bool with_super = true, bool knn_only = false, const ScanDev* sd = nullptr,
+                        const FuseArgs* fuse = nullptr) {
   if (!c.map) {
     set_error("slio pass: no map uploaded");
     return SLIO_ESTATE;
@@ -3130,7 +3225,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     const dim3 nb((unsigned)nblk);
 #define SLIO_LAUNCH(L, SPH, DEV)                                                                   \
   hipExtLaunchKernelGGL(k_search_pass<L, SLIO_SEARCH_U, SPH, DEV>, nb, dim3(search_block<L>()), 0, c.stream, \
-                        ev.first, ev.second, 0, mv, s, P, cfg, o)
+                        ev.first, ev.second, 0, mv, s, P, cfg, o, FuseArgs{})
 #define SLIO_LAUNCH2(L, SPH) \
   do {                        \
     if (devpose)              \
@@ -3138,6 +3233,12 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     else                      \
       SLIO_LAUNCH(L, SPH, false); \
   } while (0)
+    if (fuse) {
+      // fused pass (fusable() checked the configuration): the filter step
+      // runs in this launch, no k_super_sums
+      hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, true, true>, nb, dim3(kSolveThreads), 0,
+                            c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse);
+    } else
     switch (c.prm.lanes_per_query * 2 + (sph ? 1 : 0)) {
       case 2: SLIO_LAUNCH2(1, false); break;
       case 3: SLIO_LAUNCH2(1, true); break;
@@ -3165,7 +3266,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
       hipExtLaunchKernelGGL(k_reuse_pass<false>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
                             rcfg, o);
   }
-  if (with_super) enqueue_super(c, ctl, sa);
+  if (with_super && !fuse) enqueue_super(c, ctl, sa);
   SLIO_HIP(hipGetLastError());
   if (which != 0) {
     c.searched = true;
@@ -3348,8 +3449,8 @@ int slio_create(slio_handle* out, const slio_params* p) {
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.d_seg, sizeof(double) * kNSeg * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
-      hipMalloc(&h->c.count, sizeof(uint32_t) * 16) != hipSuccess ||
-      hipMemset(h->c.count, 0, sizeof(uint32_t) * 16) != hipSuccess ||
+      hipMalloc(&h->c.count, sizeof(uint32_t) * kCountWords) != hipSuccess ||
+      hipMemset(h->c.count, 0, sizeof(uint32_t) * kCountWords) != hipSuccess ||
       false) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
@@ -5811,6 +5912,13 @@ struct UpdateRun {
     const SolveArgs sa = args(i);
     // pass 0 always searches (converge starts true, esekfom.hpp:282)
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
+    if (!p0 && fusable()) {
+      const FuseArgs fa{c.d_seg, c.d_super, c.ctl, c.d_hctl, c.count, R, i, maxit, num_chunks(c.n)};
+      int rc = enqueue_pass(c, nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
+      if (rc) return rc;
+      SLIO_HIP(hipGetLastError());
+      return SLIO_OK;
+    }
     int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, !p0 || multi);
     if (rc) return rc;
     if (p0) {
@@ -5827,6 +5935,20 @@ struct UpdateRun {
     }
     SLIO_HIP(hipGetLastError());
     return SLIO_OK;
+  }
+
+  // A later pass runs as one fused launch (search + sums + filter step,
+  // fused_tail) in the bench's configuration: single rank, fixed mode (a
+  // search every pass), no extrinsic estimation, 2 lanes per query without
+  // the sphere-first search, and at least 8 chunks per super-chunk (every
+  // segment row has a chunk).  SLIO_NO_FUSE=1 keeps two launches per pass.
+  bool fusable() const {
+    const char* e = std::getenv("SLIO_NO_FUSE");
+    const bool off = e && e[0] && e[0] != '0';
+    const int lpq = c.prm.lanes_per_query;
+    return !off && !multi && mode == SLIO_MODE_FIXED && dim == 6 && c.prm.nranks == 1 &&
+           (lpq != 1 && lpq != 4 && lpq != 8) && !(c.prm.search_radius > 0.0f) &&
+           num_chunks(c.n) >= (int64_t)kNSeg;
   }
 
   // multi-rank: the filter step of pass i after the all-reduce, on every rank

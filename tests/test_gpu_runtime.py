@@ -228,6 +228,55 @@ def test_c2_full_size_pinned(L, oracle_mod, c2, mode):
         kd.close()
 
 
+def _update_once(L, h, st, maxit=4, mode=1):
+    lib = L.load()
+    xs = slio_state(st)
+    P = np.eye(24) * 1e-2
+    stt = L.SlioIkfStats()
+    L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, maxit, 0, mode, L.ALLREDUCE_FN(), None,
+                                       C.byref(stt)), "ikf")
+    n = lib.slio_get_neighbors
+    b, e = C.c_int64(), C.c_int64()
+    lib.slio_shard_range(h, C.byref(b), C.byref(e))
+    ii = np.zeros((e.value - b.value, 5), np.int32)
+    sq = np.zeros((e.value - b.value, 5), np.float32)
+    se = np.zeros(e.value - b.value, np.uint8)
+    L.check(n(h, L.iptr(ii), L.fptr(sq), L.u8ptr(se)), "nbrs")
+    sup = np.zeros(8 * 91)
+    L.check(lib.slio_super_download(h, L.dptr(sup)), "super")
+    return (state_array(xs), P, (stt.passes, stt.searches, stt.valid_passes, stt.converged, stt.last_m),
+            ii, sq, se, sup)
+
+
+@pytest.mark.parametrize("npts", [100_000, 8_191, 8_320, 20_013])
+def test_fused_pass_bitwise(L, c2, npts, monkeypatch):
+    """Passes after the first run as ONE launch (search + segment sums + the
+    filter step in the search kernel's tail, fused_tail) in the bench's
+    configuration; the two-launch path (SLIO_NO_FUSE=1: k_search_pass then
+    k_super_sums) sums in the same order and runs the same filter step, so
+    x, P, the flags, the super rows and Nearest_Points are bit-for-bit
+    equal.  Scan sizes: C2, 64 chunks exactly (the smallest fused scan),
+    65 chunks, and uneven super-chunks."""
+    mp, fr, _ = c2
+    st = state_of(fr)
+    body = np.ascontiguousarray(fr.body[:npts])
+    lib = L.load()
+    h = mk(L, cell=C2_CELL)
+    try:
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, body) == 0
+        monkeypatch.setenv("SLIO_NO_FUSE", "1")
+        two = _update_once(L, h, st)
+        monkeypatch.delenv("SLIO_NO_FUSE")
+        for rep in range(3):   # repeated: counters are reset by each pass
+            one = _update_once(L, h, st)
+            for a, b in zip(one, two):
+                np.testing.assert_array_equal(a, b)
+        assert two[2][0] == 4 and two[2][2] == 4
+    finally:
+        lib.slio_destroy(h)
+
+
 def test_batched_replay_distinct_scans(L, oracle_mod):
     """C5 replay: 4 handles share one map, each runs a DIFFERENT scan (own
     seed, own pose) from its own host thread, 3 updates each; every result
