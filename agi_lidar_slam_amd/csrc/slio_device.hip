@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -198,8 +199,8 @@ struct MapDev {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf b_pts, b_keep, b_cpts, b_start, b_cstart, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6];
-  hipError_t take(Buf& b, size_t bytes) {
+  Buf b_pts, b_keep, b_cpts, b_start, b_cstart, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6], b_add[8], b_start2;
+  static hipError_t take(Buf& b, size_t bytes) {
     bytes = std::max<size_t>(bytes, 16);
     if (bytes <= b.cap) return hipSuccess;
     if (b.p) (void)hipFree(b.p);
@@ -229,11 +230,13 @@ struct MapDev {
   }
   ~MapDev() {
     if (ready) (void)hipEventDestroy(ready);
-    for (Buf* b : {&b_pts, &b_keep, &b_cpts, &b_start, &b_cstart, &b_clo, &b_chi, &b_bstart, &b_blk})
+    for (Buf* b : {&b_pts, &b_keep, &b_cpts, &b_start, &b_cstart, &b_clo, &b_chi, &b_bstart, &b_blk, &b_start2})
       if (b->p) (void)hipFree(b->p);
     for (Buf& b : b_tmp)
       if (b.p) (void)hipFree(b.p);
     for (Buf& b : b_ref)
+      if (b.p) (void)hipFree(b.p);
+    for (Buf& b : b_add)
       if (b.p) (void)hipFree(b.p);
     if (add4) (void)hipFree(add4);
     if (akeep) (void)hipFree(akeep);
@@ -736,6 +739,57 @@ __device__ __forceinline__ void group_merge_rolled(Top5& t, int width) {
   }
 }
 
+// Top5 with a payload per entry: the block-row index of the candidate, so the
+// fit phase reloads the winners from the block rows the kNN has just read
+// (L2-resident) instead of from pts.  Same keys and order as Top5.
+struct Top5B {
+  uint64_t k[5];
+  uint32_t b[5];
+};
+
+__device__ __forceinline__ void top5b_clear(Top5B& t) {
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    t.k[j] = kInfKey;
+    t.b[j] = 0xFFFFFFFFu;
+  }
+}
+
+__device__ __forceinline__ void top5b_insert(Top5B& t, uint64_t key, uint32_t bi) {
+  bool c[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) c[j] = key < t.k[j];
+#pragma unroll
+  for (int j = 4; j > 0; --j) {
+    t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
+    t.b[j] = c[j - 1] ? t.b[j - 1] : (c[j] ? bi : t.b[j]);
+  }
+  t.k[0] = c[0] ? key : t.k[0];
+  t.b[0] = c[0] ? bi : t.b[0];
+}
+
+template <int CTRL>
+__device__ __forceinline__ void merge_round_dpp_b(Top5B& t) {
+  uint64_t ok[5];
+  uint32_t ob[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    ok[j] = dpp64<CTRL>(t.k[j]);
+    ob[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t.b[j], CTRL, 0xF, 0xF, false);
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) top5b_insert(t, ok[j], ob[j]);
+}
+
+template <int LPQ>
+__device__ __forceinline__ void group_merge_b(Top5B& t) {
+  static_assert(LPQ <= 16, "group_merge_b: up to 16 lanes (DPP)");
+  if (LPQ >= 2) merge_round_dpp_b<0xB1>(t);
+  if (LPQ >= 4) merge_round_dpp_b<0x4E>(t);
+  if (LPQ >= 8) merge_round_dpp_b<0x141>(t);
+  if (LPQ >= 16) merge_round_dpp_b<0x140>(t);
+}
+
 // Conservative lower bound of the distance from coordinate q to the points
 // assigned to grid cell i along one axis (cell edges are known to +-tol).
 __device__ __forceinline__ float axis_gap(float q, int i, float o, float h, float tol) {
@@ -953,10 +1007,10 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
 // The 3x3x3 block from the block rows: one contiguous range, so a flat
 // position is an address (no run lookup); keys carry the pts position (.w),
 // identical to the keys of the 9-run scan.  Same pipeline as scan_flat.
-template <int LPQ, int U>
+template <int LPQ, int U, typename TOP>
 __device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, uint32_t s,
                                                 uint32_t T, int sub, float qx, float qy, float qz,
-                                                Top5& t) {
+                                                TOP& t) {
   uint32_t t0 = sub;
   if (t0 >= T) return;
   constexpr uint32_t kStep = U * LPQ;
@@ -971,7 +1025,10 @@ __device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, 
       const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
       const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
       const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c[u].w);
-      top5_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
+      if constexpr (std::is_same<TOP, Top5B>::value)
+        top5b_insert(t, (tb + u * LPQ < T) ? key : kInfKey, s + tb + u * LPQ);
+      else
+        top5_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
     }
   };
   for (;;) {
@@ -1148,6 +1205,7 @@ struct PassCfg {
   int64_t c_begin, c_end;  // global chunk range of this rank
   int pass_idx;            // with ctl: run only if ctl->passes == pass_idx
   int knn_only;            // 1: neighbours only (nbr_*), no fit / rows / products
+  int mfma;                // chunk sums on the matrix cores (chunk_products_mfma), else VALU
   const uint32_t* perm;    // block -> chunk order within each XCD's range (chunk_order), or null
 };
 
@@ -1882,6 +1940,46 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
 }
 
 
+// The same 91 chunk sums on the matrix cores: they are entries of the Gram
+// matrix R^T R of the chunk's 128 x 14 row block R (H^T H, H^T h and m =
+// rows[:, 13] . rows[:, 13]), one 16 x 16 f64 tile with the columns
+// zero-padded.  Wave w forms R_w^T R_w of rows 32w..32w+31 in 8 k-steps of
+// v_mfma_f64_16x16x4_f64 (A = R^T and B = R take the same operand: lane l
+// holds R[k0 + (l >> 4)][l & 15]; D: col = l & 15, row = (l >> 4) + 4 reg),
+// writes its tile over its own rows in LDS, and thread k < 91 adds the four
+// tiles in a fixed order ((w0 + w1) + (w2 + w3)).  Deterministic, so chunk
+// partials stay the same for any rank count; different rounding from
+// chunk_products (rtol ~1e-16 of the sums).
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ void chunk_products_mfma(double (*rows)[kRow], double* __restrict__ out,
+                                                    bool sc1 = false) {
+  static_assert(NT == 256 && SLIO_CHUNK == 128 && kRow <= 16, "4 waves x 32 rows, 16 columns");
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const int col = l & 15, kq = l >> 4;
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  double v[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) v[s] = col < kRow ? rows[32 * w + 4 * s + kq][col] : 0.0;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[s], v[s], acc, 0, 0, 0);
+  // (the wave's LDS reads precede these writes in its own LDS queue)
+  double* tile = &rows[32 * w][0];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tile[(kq + 4 * r) * 16 + col] = acc[r];
+  __syncthreads();
+  if (t < SLIO_NPROD) {
+    const int e = (int)c_pa[t] * 16 + (int)c_pb[t];
+    const double* r0 = &rows[0][0];
+    constexpr int kW = 32 * kRow;  // doubles between the waves' tiles
+    const double s2 = (r0[e] + r0[kW + e]) + (r0[2 * kW + e] + r0[3 * kW + e]);
+    if (sc1)
+      st_sc1(out + t, s2);
+    else
+      out[t] = s2;
+  }
+}
+
 // Refinement scan of ALL the runs of `mask` (<= 34: 25 rows + 9 right
 // segments) by the RL lanes of a group as ONE flattened candidate list: lane
 // j fetches the bounds of runs j, j + RL, ... (one round trip for all), the
@@ -2106,6 +2204,7 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
 // that completes a segment's last chunk sums the row, and the one that
 // completes the 64th row runs final_step.
 struct FuseArgs {
+  IkfCtl* ctl;        // the update's control block in HBM
   double* seg_out;    // 64 segment rows
   double* super_out;  // 8 super rows (slio_super_download)
   const IkfCtl* src;  // control block source (ctl: passes after the first)
@@ -2187,7 +2286,7 @@ template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE = false>
 __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
     const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
     const PassOut out, const FuseArgs fa) {
-  static_assert(!FUSE || (DEVPOSE && search_block<LPQ>() == kSolveThreads), "fused pass: device pose, 256 threads");
+  static_assert(!FUSE || search_block<LPQ>() == kSolveThreads, "fused pass: 256 threads");
   // DEVPOSE: pose and pass selection come from the device-resident update
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
@@ -2215,6 +2314,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     alignas(16) uint32_t nb_pos[SLIO_CHUNK][5];
     alignas(16) float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
     alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
+    uint32_t nb_blk[SLIO_CHUNK][5];  // block-row index of each winner of the 3x3x3 fast path (FITB), else ~0
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
@@ -2237,6 +2337,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& nb_pos = lds.s.nb_pos;
   auto& nb_sqd = lds.s.nb_sqd;
   auto& nb_idx = lds.s.nb_idx;
+  auto& nb_blk = lds.s.nb_blk;
+  // the fast path's winners carry their block-row index, and the fit phase
+  // reloads them from the block rows (just read by the kNN: L2-resident)
+#ifdef SLIO_NO_FITB
+  constexpr bool FITB = false;
+#else
+  constexpr bool FITB = LPQ == 2 && !SPHERE;
+#endif
   auto& nb_d5 = lds.s.nb_d5;
   auto& qw = lds.s.qw;
   auto& far_cnt = lds.s.far_cnt;
@@ -2282,6 +2390,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     }
     Top5 t;
     top5_clear(t);
+    uint32_t bw[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     const bool finite = live && isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0 &&
                         !far_outside(g, cfg.far_sq, qx, qy, qz);
     int cx = 0, cy = 0, cz = 0, r = 1;
@@ -2311,13 +2420,26 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           if (b1 < b0 || (int64_t)b1 > map.nblk)
             printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
 #endif
-          scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+          if constexpr (FITB) {
+            Top5B tb;
+            top5b_clear(tb);
+            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, tb);
+            group_merge_b<LPQ>(tb);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+              t.k[j] = tb.k[j];
+              bw[j] = tb.b[j];
+            }
+          } else {
+            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+            group_merge<LPQ>(t);
+          }
           if (sub == 0 && out.chunk_cost) atomicAdd(&lds.s.cost, b1 - b0);
         } else {
           RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
           scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
+          group_merge<LPQ>(t);
         }
-        group_merge<LPQ>(t);
         bool covers;
         const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
         const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
@@ -2417,6 +2539,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb_sqd[slot][j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                  : __uint_as_float((uint32_t)(mk >> 32));
         nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
+        if constexpr (FITB) nb_blk[slot][j] = bw[j];
       }
     }
     if (sub == 0) {
@@ -2494,6 +2617,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
               nb_sqd[slot][j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                        : __uint_as_float((uint32_t)(mk >> 32));
               nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
+              if constexpr (FITB) nb_blk[slot][j] = 0xFFFFFFFFu;
             }
             nb_d5[slot] = (tr.k[4] != kInfKey) ? d5n : __int_as_float(0x7f800000);
           } else {
@@ -2541,6 +2665,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb_sqd[slot][lane] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                     : __uint_as_float((uint32_t)(mk >> 32));
         nb_pos[slot][lane] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
+        if constexpr (FITB) nb_blk[slot][lane] = 0xFFFFFFFFu;
       }
       if (lane == 0)
         nb_d5[slot] = (tf.k[4] != kInfKey) ? __uint_as_float((uint32_t)(tf.k[4] >> 32))
@@ -2581,7 +2706,11 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           continue;
         }
 #endif
-        if (ps != 0xFFFFFFFFu) c = pts[ps];
+        if (ps != 0xFFFFFFFFu) {
+          // (kNN-only passes read the map index in .w: from pts)
+          const uint32_t bi = (FITB && !cfg.knn_only) ? nb_blk[slot][j] : 0xFFFFFFFFu;
+          c = bi != 0xFFFFFFFFu ? map.blk[bi] : pts[ps];
+        }
         nb[j][0] = c.x;
         nb[j][1] = c.y;
         nb[j][2] = c.z;
@@ -2650,9 +2779,12 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
-  chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, FUSE);
+  if (NT == 256 && cfg.mfma)
+    chunk_products_mfma<256>(rows, out.chunk_part + chunk * SLIO_NPROD, FUSE);
+  else
+    chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, FUSE);
   if (tid == 0) STAMP(3);
-  if constexpr (FUSE) fused_tail<NT>(lds.L, fuse_bcast, fa, cfg.ctl, out.chunk_part, chunk);
+  if constexpr (FUSE) fused_tail<NT>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
 }
 
 // Nearest_Points ids and pointSearchSqDis of the last search pass, derived
@@ -2920,6 +3052,7 @@ struct Ctx {
   double* d_seg = nullptr;    // the pass's 64 segment rows (k_super_sums hand-off)
   void* comm = nullptr;        // RCCL communicator of the rank group (slio_comm_init / slio_create_group)
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
+  MapDev::Buf inc[7];         // map_incremental temporaries, kept across scans
                               // (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
   IkfCtl* h_ctl = nullptr;  // mapped, coherent host block: update input and output
@@ -3181,6 +3314,10 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   cfg.knn_only = knn_only ? 1 : 0;
+  {
+    const char* e = std::getenv("SLIO_NO_MFMA");
+    cfg.mfma = !(e && e[0] && e[0] != '0');
+  }
   // later passes of a device-resident update take their chunks in the order
   // the previous pass's costs call for (chunk_order; pass 0 in index order)
   static const bool no_order = std::getenv("SLIO_NO_CHUNK_ORDER") != nullptr;
@@ -3236,8 +3373,12 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     if (fuse) {
       // fused pass (fusable() checked the configuration): the filter step
       // runs in this launch, no k_super_sums
-      hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, true, true>, nb, dim3(kSolveThreads), 0,
-                            c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse);
+      if (devpose)
+        hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, true, true>, nb, dim3(kSolveThreads), 0,
+                              c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse);
+      else
+        hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, false, true>, nb, dim3(kSolveThreads), 0,
+                              c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse);
     } else
     switch (c.prm.lanes_per_query * 2 + (sph ? 1 : 0)) {
       case 2: SLIO_LAUNCH2(1, false); break;
@@ -3474,6 +3615,8 @@ int slio_destroy(slio_handle h) {
   (void)hipFree(h->c.d_super_own);
   (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
+  for (auto& b : h->c.inc)
+    if (b.p) (void)hipFree(b.p);
   if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
   (void)hipFree(h->c.ctl);
   (void)hipHostFree(h->c.h_ctl);
@@ -4416,16 +4559,14 @@ __global__ void k_vg_centroids(const float* __restrict__ x, const float* __restr
   oz[r] = sz / cnt;
 }
 
-// exclusive scan of n flags into rank; returns the total
-static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream_t st, uint32_t* total) {
-  *total = 0;
-  if (n == 0) return SLIO_OK;
+// exclusive scan of n flags into rank, enqueued on st (no readback)
+static int scan_launch(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream_t st) {
   size_t tb = 0;
   // scan temporaries cached per host thread AND device (no hipMalloc /
   // hipFree per call; one thread may drive handles on several GPUs, and a
-  // device must never be handed another device's buffer).  The call ends
-  // with a stream synchronisation, so one buffer per (thread, device) is
-  // never in use by two scans at once.
+  // device must never be handed another device's buffer).  Scans reusing
+  // the buffer are ordered on one stream, and a buffer is replaced only
+  // after the device is idle (hipFree synchronises).
   constexpr int kMaxDev = 64;
   static thread_local void* tmps[kMaxDev] = {};
   static thread_local size_t tcaps[kMaxDev] = {};
@@ -4455,16 +4596,46 @@ static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream
     set_error(std::string("slio map: scan: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
   }
-  uint32_t last[2] = {0, 0};
-  e = hipMemcpyAsync(&last[0], rank + n - 1, 4, hipMemcpyDeviceToHost, st);
-  if (!e) e = hipMemcpyAsync(&last[1], flag + n - 1, 4, hipMemcpyDeviceToHost, st);
+  return SLIO_OK;
+}
+
+// exclusive scans of k flag arrays (n each) into ranks; totals read back
+// with one synchronisation
+static int scan_flags_k(int k, const uint32_t* const* flag, uint32_t* const* rank, int64_t n, hipStream_t st,
+                        uint32_t* total) {
+  for (int j = 0; j < k; ++j) total[j] = 0;
+  if (n == 0) return SLIO_OK;
+  uint32_t last[4] = {0, 0, 0, 0};
+  hipError_t e = hipSuccess;
+  for (int j = 0; j < k; ++j) {
+    if (int rc = scan_launch(flag[j], rank[j], n, st)) return rc;
+    if (!e) e = hipMemcpyAsync(&last[2 * j], rank[j] + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (!e) e = hipMemcpyAsync(&last[2 * j + 1], flag[j] + n - 1, 4, hipMemcpyDeviceToHost, st);
+  }
   if (!e) e = hipStreamSynchronize(st);
   if (e) {
     set_error(std::string("slio map: scan total: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
   }
-  *total = last[0] + last[1];
+  for (int j = 0; j < k; ++j) total[j] = last[2 * j] + last[2 * j + 1];
   return SLIO_OK;
+}
+
+// exclusive scan of n flags into rank; returns the total
+static int scan_flags(const uint32_t* flag, uint32_t* rank, int64_t n, hipStream_t st, uint32_t* total) {
+  return scan_flags_k(1, &flag, &rank, n, st, total);
+}
+
+// two exclusive flag scans on one stream, one readback of both totals
+static int scan_flags2(const uint32_t* f1, uint32_t* r1, const uint32_t* f2, uint32_t* r2, int64_t n,
+                       hipStream_t st, uint32_t* t1, uint32_t* t2) {
+  const uint32_t* f[2] = {f1, f2};
+  uint32_t* r[2] = {r1, r2};
+  uint32_t t[2];
+  const int rc = scan_flags_k(2, f, r, n, st, t);
+  *t1 = t[0];
+  *t2 = t[1];
+  return rc;
 }
 
 static int add_reserve(MapDev& m, int64_t more, hipStream_t st) {
@@ -4527,21 +4698,33 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
   void* tmp = nullptr;
   int rc = SLIO_OK;
   do {
+    // temporaries kept on the map across calls (a live map adds every scan;
+    // hipFree would also synchronise the device)
     hipError_t e;
-    if ((e = hipMalloc(&k0, 8 * n)) || (e = hipMalloc(&k1, 8 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
-        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&surv, 4 * n)) || (e = hipMalloc(&rank, 4 * n)) ||
-        (e = hipMalloc(&dcount, 16))) {
+    auto& B = m.b_add;
+    if ((e = m.take(B[0], 8 * n)) || (e = m.take(B[1], 8 * n)) || (e = m.take(B[2], 4 * n)) ||
+        (e = m.take(B[3], 4 * n)) || (e = m.take(B[4], 4 * n)) || (e = m.take(B[5], 4 * n)) ||
+        (e = m.take(B[6], 16))) {
       set_error(std::string("slio map: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
       break;
     }
+    k0 = (uint64_t*)B[0].p;
+    k1 = (uint64_t*)B[1].p;
+    v0 = (uint32_t*)B[2].p;
+    v1 = (uint32_t*)B[3].p;
+    surv = (uint32_t*)B[4].p;
+    rank = (uint32_t*)B[5].p;
+    dcount = (unsigned long long*)B[6].p;
     size_t tb = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 63, st)) ||
-        (e = hipMalloc(&tmp, tb))) {
+        (e = m.take(B[7], tb))) {
       set_error(std::string("slio map: sort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
     }
+    tmp = B[7].p;
+    tb = B[7].cap;
     const int nb = grid_blocks(n);
     k_ds_keys<<<nb, 256, 0, st>>>(in, n, ds, k0, v0);
     if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 63, st)) ||
@@ -4583,9 +4766,213 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     m.next_id += total;
     m.dirty = true;  // deletions (keep flags) and / or additions
   } while (0);
-  for (void* q : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)surv, (void*)rank, (void*)dcount, tmp})
-    if (q) (void)hipFree(q);
   return rc;
+}
+
+// ---------------------------------------------------------------- merge rebuild
+// A rebuild that keeps the grid does not sort the map again: the survivors
+// are already in (cell, id) order and every addition has a larger id than
+// every stored point, so the new order is, cell by cell, the cell's survivors
+// (old order) followed by its additions (id order).  With rank = the
+// survivors' exclusive prefix count and lb(c) = the number of (live, sorted)
+// additions in cells < c:
+//   new_start[c]       = rank(old_start[c]) + lb(c)
+//   survivor p, cell c -> new_start[c] + rank[p] - rank(old_start[c])
+//   addition j, cell c -> new_start[c + 1] - (lb(c + 1) - j)
+// (rank(n0) = the survivor count).  Bit-identical to the sort: same points,
+// same order, same cell table.
+constexpr int kMergeTile = 1024;  // cells per workgroup of k_merge_start
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t lo, uint32_t hi,
+                                                    uint32_t v) {
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict__ old_start,
+                                                     const uint32_t* __restrict__ rank, int64_t n0, uint32_t n0p,
+                                                     const uint32_t* __restrict__ sk, uint32_t na,
+                                                     int64_t ncells1, uint32_t* __restrict__ new_start) {
+  __shared__ uint32_t lk[kMergeTile];
+  __shared__ uint32_t jj[2];
+  const int64_t c0 = (int64_t)blockIdx.x * kMergeTile;
+  const int64_t c1 = min(c0 + (int64_t)kMergeTile, ncells1);
+  const int t = threadIdx.x;
+  if (t < 2) jj[t] = lower_bound_u32(sk, 0, na, (uint32_t)(t == 0 ? c0 : c1));
+  __syncthreads();
+  const uint32_t j0 = jj[0], m = jj[1] - j0;
+  const bool inl = m <= (uint32_t)kMergeTile;
+  if (inl)
+    for (uint32_t k = t; k < m; k += blockDim.x) lk[k] = sk[j0 + k];
+  __syncthreads();
+  for (int64_t c = c0 + t; c < c1; c += blockDim.x) {
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((inl ? lk[mid] : sk[j0 + mid]) < (uint32_t)c)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const uint32_t os = old_start[c];
+    const uint32_t r = (int64_t)os < n0 ? rank[os] : n0p;
+    new_start[c] = r + j0 + lo;
+  }
+}
+__global__ void k_merge_pts(const float4* __restrict__ pts, const uint8_t* __restrict__ keep,
+                            const uint32_t* __restrict__ rank, const uint32_t* __restrict__ old_start,
+                            const uint32_t* __restrict__ new_start, int64_t n0, GridGeom g,
+                            float4* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n0 || !keep[p]) return;
+  const float4 v = pts[p];
+  const int cx = min(max(cell_coord(v.x, g.ox, g.inv_h), 0), g.dx - 1);
+  const int cy = min(max(cell_coord(v.y, g.oy, g.inv_h), 0), g.dy - 1);
+  const int cz = min(max(cell_coord(v.z, g.oz, g.inv_h), 0), g.dz - 1);
+  const uint32_t c = ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx + (uint32_t)cx;
+  const uint32_t os = old_start[c];  // <= p < n0
+  out[new_start[c] + rank[p] - rank[os]] = v;
+}
+__global__ void k_merge_adds(const float4* __restrict__ adds, const uint32_t* __restrict__ sk,
+                             const uint32_t* __restrict__ sv, uint32_t na, const uint32_t* __restrict__ new_start,
+                             float4* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= na) return;
+  const uint32_t c = sk[j];
+  const uint32_t e = lower_bound_u32(sk, j, na, c + 1);
+  out[new_start[c + 1] - (e - j)] = adds[sv[j]];
+}
+
+// The merge rebuild (see k_merge_start) of m: *handled = false when the
+// additions do not all lie at least one cell inside the grid (then the caller
+// rebuilds by sorting, with a new grid).  Stream-ordered; synchronises twice
+// (the counts, the additions' box) and once at the end.
+static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
+  *handled = false;
+  const int64_t n0 = m.n, n1 = m.nadd;
+  const GridGeom g = m.g;
+  hipError_t e;
+  auto fail = [&](const char* what, hipError_t err) {
+    set_error(std::string("slio map merge: ") + what + ": " + hipGetErrorString(err));
+    return err == hipErrorOutOfMemory ? SLIO_ENOMEM : SLIO_EDEVICE;
+  };
+  const int64_t na_cap = std::max<int64_t>(n1, 1);
+  if ((e = m.take(m.b_ref[1], 4 * n0)) || (e = m.take(m.b_ref[2], 4 * n0)) || (e = m.take(m.b_ref[3], 32)) ||
+      (e = m.take(m.b_ref[4], 4 * na_cap)) || (e = m.take(m.b_ref[5], 4 * na_cap)) ||
+      (e = m.take(m.b_tmp[0], 16 * na_cap)) || (e = m.take(m.b_tmp[1], 4 * na_cap)) ||
+      (e = m.take(m.b_tmp[2], 4 * na_cap)) || (e = m.take(m.b_tmp[3], 4 * na_cap)) ||
+      (e = m.take(m.b_tmp[4], 4 * na_cap)))
+    return fail("hipMalloc", e);
+  uint32_t* flag = (uint32_t*)m.b_ref[1].p;
+  uint32_t* rank = (uint32_t*)m.b_ref[2].p;
+  int32_t* bb = (int32_t*)m.b_ref[3].p;
+  uint32_t* aflag = (uint32_t*)m.b_ref[4].p;
+  uint32_t* arank = (uint32_t*)m.b_ref[5].p;
+  float4* acomp = (float4*)m.b_tmp[0].p;
+  uint32_t* ak = (uint32_t*)m.b_tmp[1].p;
+  uint32_t* sk = (uint32_t*)m.b_tmp[2].p;
+  uint32_t* av = (uint32_t*)m.b_tmp[3].p;
+  uint32_t* sv = (uint32_t*)m.b_tmp[4].p;
+  // survivor ranks and the live additions' ranks, one readback
+  k_widen_flags<<<grid_blocks(n0), 256, 0, st>>>(m.keep, n0, flag);
+  if (n1) k_widen_flags<<<grid_blocks(n1), 256, 0, st>>>(m.akeep, n1, aflag);
+  if (int rc = scan_launch(flag, rank, n0, st)) return rc;
+  if (n1)
+    if (int rc = scan_launch(aflag, arank, n1, st)) return rc;
+  uint32_t last[4] = {0, 0, 0, 0};
+  if ((e = hipMemcpyAsync(&last[0], rank + n0 - 1, 4, hipMemcpyDeviceToHost, st)) ||
+      (e = hipMemcpyAsync(&last[1], flag + n0 - 1, 4, hipMemcpyDeviceToHost, st)) ||
+      (n1 && (e = hipMemcpyAsync(&last[2], arank + n1 - 1, 4, hipMemcpyDeviceToHost, st))) ||
+      (n1 && (e = hipMemcpyAsync(&last[3], aflag + n1 - 1, 4, hipMemcpyDeviceToHost, st))))
+    return fail("counts", e);
+  if (n1) k_compact4<<<grid_blocks(n1), 256, 0, st>>>(m.add4, aflag, arank, n1, acomp);
+  if ((e = hipStreamSynchronize(st))) return fail("counts", e);
+  const uint32_t n0p = last[0] + last[1], na = last[2] + last[3];
+  if (na) {
+    // the live additions' box: they must lie a cell inside the kept grid
+    const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
+    int32_t got[8];
+    if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) return fail("box", e);
+    k_bbox4<<<std::min(grid_blocks(na), 512), 256, 0, st>>>(acomp, na, bb);
+    if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      return fail("box", e);
+    if (got[6]) return SLIO_OK;  // non-finite: the sorting rebuild reports it
+    const float o[3] = {g.ox, g.oy, g.oz};
+    const int d[3] = {g.dx, g.dy, g.dz};
+    for (int a = 0; a < 3; ++a)
+      if (!(fkey_inv(got[a]) >= o[a] + g.h && fkey_inv(got[3 + a]) <= o[a] + (float)(d[a] - 1) * g.h))
+        return SLIO_OK;  // an addition near or past the grid's edge: re-grid by sorting
+  }
+  *handled = true;
+  const int64_t n = (int64_t)n0p + na;
+  if ((e = m.take(m.b_ref[0], 16 * std::max<int64_t>(n, 1))) ||
+      (e = m.take(m.b_start2, sizeof(uint32_t) * (m.ncells + 1))))
+    return fail("hipMalloc", e);
+  float4* out = (float4*)m.b_ref[0].p;
+  uint32_t* new_start = (uint32_t*)m.b_start2.p;
+  int cbits = 1;
+  while (cbits < 32 && ((int64_t)1 << cbits) < m.ncells) ++cbits;
+  if (na) {
+    k_coarse_keys<<<grid_blocks(na), 256, 0, st>>>(acomp, na, g, ak, av);  // fine cell keys (same formula)
+    size_t tb = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ak, sk, av, sv, (int)na, 0, cbits, st)) ||
+        (e = m.take(m.b_tmp[7], tb)))
+      return fail("sort size", e);
+    tb = m.b_tmp[7].cap;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(m.b_tmp[7].p, tb, ak, sk, av, sv, (int)na, 0, cbits, st)))
+      return fail("sort", e);
+  }
+  const int64_t nc1 = m.ncells + 1;
+  k_merge_start<<<(unsigned)((nc1 + kMergeTile - 1) / kMergeTile), 256, 0, st>>>(m.start, rank, n0, n0p, sk,
+                                                                                 na, nc1, new_start);
+  k_merge_pts<<<grid_blocks(n0), 256, 0, st>>>(m.pts, m.keep, rank, m.start, new_start, n0, g, out);
+  if (na) k_merge_adds<<<grid_blocks(na), 256, 0, st>>>(acomp, sk, sv, na, new_start, out);
+  if ((e = hipGetLastError())) return fail("merge kernels", e);
+  // new views: points and cell table swap buffers with their temporaries
+  std::swap(m.b_pts, m.b_ref[0]);
+  std::swap(m.b_start, m.b_start2);
+  m.pts = (float4*)m.b_pts.p;
+  m.start = (uint32_t*)m.b_start.p;
+  m.n = n;
+  if ((e = m.take(m.b_keep, std::max<int64_t>(n, 1))) || (e = m.take(m.b_cpts, sizeof(float4) * std::max<int64_t>(n, 1))))
+    return fail("hipMalloc", e);
+  m.keep = (uint8_t*)m.b_keep.p;
+  m.cpts = (float4*)m.b_cpts.p;
+  k_fill_u8<<<grid_blocks(n), 256, 0, st>>>(m.keep, n, 1);
+  // coarse level from the new cell table (as build_index)
+  if ((e = m.take(m.b_tmp[6], 4 * (m.nccells + 1)))) return fail("hipMalloc", e);
+  uint32_t* cnt = (uint32_t*)m.b_tmp[6].p;
+  size_t t3 = 0;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, t3, cnt, m.cstart, (int)(m.nccells + 1), st)) ||
+      (e = m.take(m.b_tmp[7], t3)))
+    return fail("coarse scan size", e);
+  t3 = m.b_tmp[7].cap;
+  k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, m.cg, m.nccells, cnt);
+  if ((e = hipcub::DeviceScan::ExclusiveSum(m.b_tmp[7].p, t3, cnt, m.cstart, (int)(m.nccells + 1), st)))
+    return fail("coarse scan", e);
+  k_coarse_fill<<<grid_blocks(m.nccells * 64), 256, 0, st>>>(m.pts, m.start, g, m.cg, m.cstart, m.nccells, m.cpts,
+                                                               m.clo, m.chi);
+  if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) return fail("coarse kernels", e);
+  m.blk = nullptr;
+  m.bstart = nullptr;
+  m.nblk = 0;
+  m.blk_deferred = block_rows_wanted(m);
+  m.stable_passes = 0;
+#ifdef SLIO_BOUNDS_CHECK
+  {
+    const int64_t nc = m.ncells;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_npts), &n, sizeof(n));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dbg_ncells), &nc, sizeof(nc));
+  }
+#endif
+  if (std::getenv("SLIO_DEBUG_REBUILD"))
+    std::fprintf(stderr, "slio rebuild: merge n %lld (survivors %u of %lld, additions %u of %lld)\n", (long long)n,
+                 n0p, (long long)n0, na, (long long)n1);
+  return SLIO_OK;
 }
 
 // Rebuild the index from the surviving points and the pending additions
@@ -4611,6 +4998,25 @@ static int map_refresh_locked(Ctx& c, bool adds_only) {
   if (int rc = nbr_settle(c)) return rc;  // the rebuild moves the points
   hipStream_t st = c.stream;
   const int64_t n0 = m.n, n1 = m.nadd, nt = n0 + n1;
+  {
+    // a grid that still holds every point: merge instead of sorting
+    // (SLIO_NO_MERGE=1: always sort)
+    const char* nm = std::getenv("SLIO_NO_MERGE");
+    if (n0 > 0 && m.start && m.cstart && !(nm && nm[0] && nm[0] != '0')) {
+      bool handled = false;
+      const int rc = merge_rebuild(m, st, &handled);
+      if (handled || rc) {
+        if (rc) {
+          m.broken = true;
+          m.free_index();
+        }
+        m.nadd = 0;
+        m.version++;
+        m.dirty = false;
+        return rc;
+      }
+    }
+  }
   hipError_t e;
   // survivors: stored points (cell order) and additions (id order) compacted
   // into in4; the sort in build_index orders them by (cell, id) anyway
@@ -4913,18 +5319,26 @@ int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_
     int rc = SLIO_OK;
     do {
       hipError_t e;
-      if ((e = hipMalloc(&w4, 16 * n)) || (e = hipMalloc(&l1, 16 * n)) || (e = hipMalloc(&l2, 16 * n)) ||
-          (e = hipMalloc(&fa, 4 * n)) || (e = hipMalloc(&fn, 4 * n)) || (e = hipMalloc(&ra, 4 * n)) ||
-          (e = hipMalloc(&rn, 4 * n))) {
+      auto& B = c.inc;  // kept across scans (hipFree would synchronise the device)
+      if ((e = MapDev::take(B[0], 16 * n)) || (e = MapDev::take(B[1], 16 * n)) ||
+          (e = MapDev::take(B[2], 16 * n)) || (e = MapDev::take(B[3], 4 * n)) ||
+          (e = MapDev::take(B[4], 4 * n)) || (e = MapDev::take(B[5], 4 * n)) || (e = MapDev::take(B[6], 4 * n))) {
         set_error(std::string("slio_map_incremental: hipMalloc: ") + hipGetErrorString(e));
         rc = SLIO_ENOMEM;
         break;
       }
+      w4 = (float4*)B[0].p;
+      l1 = (float4*)B[1].p;
+      l2 = (float4*)B[2].p;
+      fa = (uint32_t*)B[3].p;
+      fn = (uint32_t*)B[4].p;
+      ra = (uint32_t*)B[5].p;
+      rn = (uint32_t*)B[6].p;
       const int nb = grid_blocks(n);
       k_map_classify<<<nb, 256, 0, c.stream>>>(c.bx, c.by, c.bz, n, W, c.nbr_pos, c.map->pts,
                                                filter_size_map_min, ekf_inited, w4, fa, fn);
       uint32_t na = 0, nn = 0;
-      if ((rc = scan_flags(fa, ra, n, c.stream, &na)) || (rc = scan_flags(fn, rn, n, c.stream, &nn))) break;
+      if ((rc = scan_flags2(fa, ra, fn, rn, n, c.stream, &na, &nn))) break;
       k_compact4<<<nb, 256, 0, c.stream>>>(w4, fa, ra, n, l1);
       k_compact4<<<nb, 256, 0, c.stream>>>(w4, fn, rn, n, l2);
       out[0] = na;
@@ -4935,8 +5349,6 @@ int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_
       out[2] = cnt;
       SLIO_HIP(hipStreamSynchronize(c.stream));
     } while (0);
-    for (void* q : {(void*)w4, (void*)l1, (void*)l2, (void*)fa, (void*)fn, (void*)ra, (void*)rn})
-      if (q) (void)hipFree(q);
     if (int rc2 = map_write_end(c); rc2 && !rc) rc = rc2;
     if (rc) return rc;
   }
@@ -4979,6 +5391,24 @@ int slio_map_download(slio_handle h, float* x, float* y, float* z, uint32_t* ids
     y[k] = p.y;
     z[k] = p.z;
     ids[k] = order[k].first;
+  }
+  return SLIO_OK;
+}
+
+// test support (not in include/slio.h): the index's points in their stored
+// (cell, id) order, x, y, z, bits(id) per point, after the pending rebuild
+int slio_dbg_map_raw(slio_handle h, float* xyzw, int64_t cap, int64_t* n) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!c.map || !n) return SLIO_ESTATE;
+  if (int rc = map_refresh(c)) return rc;
+  std::shared_lock<std::shared_mutex> lk(c.map->mu);
+  if (int rc = map_read_sync(c)) return rc;
+  *n = c.map->n;
+  if (cap < c.map->n || (c.map->n > 0 && !xyzw)) return SLIO_ECAPACITY;
+  if (c.map->n) {
+    SLIO_HIP(hipMemcpyAsync(xyzw, c.map->pts, 16 * c.map->n, hipMemcpyDeviceToHost, c.stream));
+    SLIO_HIP(hipStreamSynchronize(c.stream));
   }
   return SLIO_OK;
 }
@@ -5912,9 +6342,24 @@ struct UpdateRun {
     const SolveArgs sa = args(i);
     // pass 0 always searches (converge starts true, esekfom.hpp:282)
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
-    if (!p0 && fusable()) {
-      const FuseArgs fa{c.d_seg, c.d_super, c.ctl, c.d_hctl, c.count, R, i, maxit, num_chunks(c.n)};
-      int rc = enqueue_pass(c, nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
+    if (fusable() && !(p0 && getenv_on("SLIO_NO_FUSE0"))) {
+      // one launch: search + sums + filter step.  The first pass reads the
+      // mapped host block, filled below while the launch runs and then
+      // released by its sequence number
+      // The first pass's filter step reads the mapped host block in the same
+      // launch: fill it first (measured: launching first and handing the
+      // block over by a polled sequence word cost more than it hid)
+      if (p0) {
+        // the previous update has published: nothing on the device still
+        // reads or writes the block
+        fill_block();
+        if (!info_constants(P, dim, c.h_ctl->P11i, c.h_ctl->G)) {
+          set_error("slio_ikf_update_device: singular covariance block P[:D, :D]");
+          return SLIO_EINVAL;
+        }
+      }
+      const FuseArgs fa{c.ctl, c.d_seg, c.d_super, sa.src, c.d_hctl, c.count, R, i, maxit, num_chunks(c.n)};
+      int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
       if (rc) return rc;
       SLIO_HIP(hipGetLastError());
       return SLIO_OK;
@@ -5942,9 +6387,12 @@ struct UpdateRun {
   // search every pass), no extrinsic estimation, 2 lanes per query without
   // the sphere-first search, and at least 8 chunks per super-chunk (every
   // segment row has a chunk).  SLIO_NO_FUSE=1 keeps two launches per pass.
+  static bool getenv_on(const char* name) {
+    const char* e = std::getenv(name);
+    return e && e[0] && e[0] != '0';
+  }
   bool fusable() const {
-    const char* e = std::getenv("SLIO_NO_FUSE");
-    const bool off = e && e[0] && e[0] != '0';
+    const bool off = getenv_on("SLIO_NO_FUSE");
     const int lpq = c.prm.lanes_per_query;
     return !off && !multi && mode == SLIO_MODE_FIXED && dim == 6 && c.prm.nranks == 1 &&
            (lpq != 1 && lpq != 4 && lpq != 8) && !(c.prm.search_radius > 0.0f) &&

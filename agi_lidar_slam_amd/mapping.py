@@ -17,6 +17,7 @@ device-resident one.  This module only sequences the calls, like the ROS node.
 from __future__ import annotations
 
 import ctypes as C
+import time
 
 import numpy as np
 
@@ -51,6 +52,56 @@ def point_body_to_world(x: StateIkfom, body: np.ndarray) -> np.ndarray:
     a = _mv(quat_matrix(x.offset_R_L_I), pb) + np.asarray(x.offset_T_L_I, dtype=np.float64)[:, None]
     w = _mv(quat_matrix(x.rot), a) + np.asarray(x.pos, dtype=np.float64)[:, None]
     return w.T.astype(np.float32)
+
+
+class _LazyNearest(dict):
+    """Nearest_Points of the scan's last search pass, read from the device on
+    first use: map_incremental runs on the device from the pass's neighbour
+    positions, so the live loop never copies 100k x 5 ids to the host (the
+    ids stay derivable until the handle's scan or map changes; valid until
+    the next process())."""
+
+    def __init__(self, kf):
+        super().__init__()
+        self._kf = kf
+        self._loaded = False
+
+    def _load(self):
+        if not self._loaded:
+            self._loaded = True
+            super().update(self._kf.nearest_points())
+
+    def __getitem__(self, k):
+        self._load()
+        return super().__getitem__(k)
+
+    def __contains__(self, k):
+        self._load()
+        return super().__contains__(k)
+
+    def __iter__(self):
+        self._load()
+        return super().__iter__()
+
+    def __len__(self):
+        self._load()
+        return super().__len__()
+
+    def get(self, k, default=None):
+        self._load()
+        return super().get(k, default)
+
+    def keys(self):
+        self._load()
+        return super().keys()
+
+    def items(self):
+        self._load()
+        return super().items()
+
+    def values(self):
+        self._load()
+        return super().values()
 
 
 class LaserMapping:
@@ -98,7 +149,9 @@ class LaserMapping:
         pos_lid = np.asarray(x.pos, dtype=np.float64) + _mv(
             quat_matrix(x.rot), np.asarray(x.offset_T_L_I, dtype=np.float64)[:, None])[:, 0]
         flg_ekf_inited = (float(lidar_beg_time) - self.first_lidar_time) >= INIT_TIME
+        t0 = time.perf_counter()
         self.last["deleted"] = self.lasermap_fov_segment(pos_lid)
+        t1 = time.perf_counter()
         body = np.ascontiguousarray(np.asarray(feats_down_body, dtype=np.float32)[:, :3])
         if body.shape[0] < 5:
             return False
@@ -107,9 +160,14 @@ class LaserMapping:
             self.ikdtree.Build(point_body_to_world(x, body))
             self.built = True
             return False
-        self.Nearest_Points = {}
-        self.kf.update_iterated_dyn_share_modified(LASER_POINT_COV, body, self.ikdtree, self.Nearest_Points,
+        self.kf.update_iterated_dyn_share_modified(LASER_POINT_COV, body, self.ikdtree, None,
                                                    self.maximum_iter, self.extrinsic_est)
+        self.Nearest_Points = _LazyNearest(self.kf)
+        t2 = time.perf_counter()
         self.last["map_incremental"] = self.kf.map_incremental(self.ikdtree, self.filter_size_map_min,
                                                                flg_ekf_inited)
+        t3 = time.perf_counter()
+        # host wall clock of the three steps (ms): fov segment + deletions,
+        # scan upload + IKF update, map_incremental
+        self.last["t_ms"] = (1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2))
         return True

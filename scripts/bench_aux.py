@@ -44,6 +44,7 @@ def mapping(n_map, n_scan, frames_n=6):
     lm.kf.change_x(x)
     lib = L.load()
     rows = []
+    steps, search = [], []
     for k, fr in enumerate(frames):
         x = lm.kf.get_x()
         if k:
@@ -51,12 +52,21 @@ def mapping(n_map, n_scan, frames_n=6):
         lm.kf.change_x(x)
         lm.kf.change_P(np.eye(24) * 1e-2)
         body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
+        # HIP events on this scan's search launches (diagnostic: ~5 us per launch)
+        lib.slio_profile(lm.kf.h, 1 << (L.SLIO_KERNEL_SEARCH + 1))
         t0 = time.perf_counter()
         lm.process(body, lidar_beg_time=0.1 * (k + 1))
         t_total = (time.perf_counter() - t0) * 1e3
+        ms, nl = C.c_double(), C.c_int64()
+        lib.slio_profile_read(lm.kf.h, L.SLIO_KERNEL_SEARCH, C.byref(ms), C.byref(nl))
+        lib.slio_profile(lm.kf.h, 0)
+        nfar = C.c_int64()
+        lib.slio_far_queries(lm.kf.h, C.byref(nfar))
         n = C.c_int64()
         t_rebuild, _ = t_ms(lambda: lib.slio_map_info(lm.ikdtree.h, None, None, C.byref(n)))
         rows.append((t_total, t_rebuild, int(n.value), [int(v) for v in lm.last["map_incremental"]]))
+        steps.append([round(v, 3) for v in lm.last.get("t_ms", (0, 0, 0))])
+        search.append((round(ms.value, 3), int(nl.value), int(nfar.value)))
     # first scan pays one-time allocations; report the median of the rest
     tt = np.median([r[0] for r in rows[1:]])
     tr = np.median([r[1] for r in rows[1:]])
@@ -64,7 +74,9 @@ def mapping(n_map, n_scan, frames_n=6):
                       "ms_fov_ikf4_map_incremental": tt, "ms_index_rebuild": tr,
                       "ms_per_scan": tt + tr, "ms_index_rebuild_each": [round(r[1], 3) for r in rows],
                       "map_size_after": rows[-1][2],
-                      "map_incremental_counts_last": rows[-1][3]}), flush=True)
+                      "map_incremental_counts_last": rows[-1][3],
+                      "ms_fov_update_mapinc_each": steps,
+                      "search_ms_launches_farq_each": search}), flush=True)
 
 
 def preproc(n_raw):

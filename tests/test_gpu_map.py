@@ -401,3 +401,63 @@ def test_exact_distance_tie_and_map_incremental(L, oracle_mod):
         assert_same_map(L, h, om)
     finally:
         L.load().slio_destroy(h)
+
+
+def _raw(L, h):
+    lib = L.load()
+    n = C.c_int64()
+    lib.slio_dbg_map_raw.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+    L.check(lib.slio_map_info(h, None, None, C.byref(n)), "map_info")   # (rebuilds when pending)
+    out = np.zeros((max(n.value, 1), 4), np.float32)
+    L.check(lib.slio_dbg_map_raw(h, out.ctypes.data, out.shape[0], C.byref(n)), "raw")
+    return out[:n.value].view(np.uint32)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_merge_rebuild_equals_sort(L, oracle_mod, seed, monkeypatch):
+    """The merge rebuild (kept grid: survivors in place, additions merged in
+    by cell) gives the sorting rebuild's index bit for bit -- the same points
+    in the same (cell, id) order -- after Add_Points with and without
+    downsampling, box deletions, and an addition past the grid's edge (the
+    merge declines and the index is re-gridded by sorting); both equal the
+    oracle's point set."""
+    rng = np.random.default_rng(seed)
+    base = rng.uniform(-20, 20, (60000, 3)).astype(np.float32)
+    base[:, 2] *= 0.2
+    hm = mk(L, n_max=1000, cell=1.0)
+    hs = mk(L, n_max=1000, cell=1.0)
+    om = oracle_mod.Map(base)
+    try:
+        upload_map(L, hm, base)
+        upload_map(L, hs, base)
+
+        def both(fn):
+            monkeypatch.delenv("SLIO_NO_MERGE", raising=False)
+            a = fn(hm)
+            monkeypatch.setenv("SLIO_NO_MERGE", "1")
+            b = fn(hs)
+            monkeypatch.delenv("SLIO_NO_MERGE", raising=False)
+            return a, b
+
+        for rep in range(6):
+            new = np.concatenate([
+                rng.uniform(-19, 19, (4000, 3)) * [1, 1, 0.2],
+                base[rng.choice(base.shape[0], 800)] + rng.normal(0, 0.05, (800, 3)),
+                base[rng.choice(base.shape[0], 100)],
+            ]).astype(np.float32)
+            if rep == 4:   # past the grid's edge: the merge declines, the index re-grids
+                new = np.concatenate([new, [[40.0, 1.0, 0.5]]]).astype(np.float32)
+            new = new[rng.permutation(new.shape[0])]
+            ds = rep % 2 == 0
+            ca, cb = both(lambda h: add(L, h, new, ds))
+            assert ca == cb == om.add_points(new, ds, 0.5)
+            if rep % 3 == 1:
+                boxes = np.array([[-5, -5, -2, 2.5, 3.5, 2]], np.float32) + rep
+                da, db = both(lambda h: delete(L, h, boxes))
+                assert da == db == om.delete_boxes(boxes)
+            ra, rb = both(lambda h: _raw(L, h))
+            np.testing.assert_array_equal(ra, rb)
+            assert_same_map(L, hm, om)
+    finally:
+        L.load().slio_destroy(hm)
+        L.load().slio_destroy(hs)
