@@ -422,77 +422,96 @@ __global__ void k_coarse_count(const uint32_t* __restrict__ start, GridGeom g, G
   }
   cnt[c] = sum;
 }
-// one wavefront per coarse cell: copy its rows (.w = fine position) and form
-// its tight box (count in lo.w)
+// one wavefront per 64 coarse cells: each lane reads its cell's size (empty
+// cells -- most of a surface map's -- are written by their lane at once),
+// then 16-lane groups copy the non-empty cells' rows (.w = fine position),
+// four cells at a time, and form their tight boxes (count in lo.w).  (One
+// wavefront per cell: ~240 us of a 10M map's rebuild.)
 __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __restrict__ start, GridGeom g,
                               GridGeom cg, const uint32_t* __restrict__ cstart, int64_t nc,
                               float4* __restrict__ cpts, float4* __restrict__ lo, float4* __restrict__ hi) {
-  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t c_base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) << 6;
   const int lane = threadIdx.x & 63;
-  if (c >= nc) return;
-  const uint32_t base = cstart[c], total = cstart[c + 1] - base;
   const float INF = __int_as_float(0x7f800000);
-  if (total == 0) {  // most coarse cells of a surface map: no row bounds needed
-    if (lane == 0) {
-      lo[c] = make_float4(INF, INF, INF, __uint_as_float(0u));
-      hi[c] = make_float4(-INF, -INF, -INF, 0.0f);
-    }
-    return;
-  }
-  int cx, cy, cz;
-  coarse_decode(cg, c, cx, cy, cz);
-  const int x0 = 4 * cx, x1 = min(4 * cx + 4, g.dx);
-  uint32_t rs = 0, len = 0;
-  if (lane < 16) {
-    const int fy = 4 * cy + (lane & 3), fz = 4 * cz + (lane >> 2);
-    if (fy < g.dy && fz < g.dz) {
-      const int64_t rb = ((int64_t)fz * g.dy + fy) * g.dx;
-      rs = start[rb + x0];
-      len = start[rb + x1] - rs;
+  const int64_t mc = c_base + lane;
+  uint32_t mb = 0, mt = 0;
+  if (mc < nc) {
+    mb = cstart[mc];
+    mt = cstart[mc + 1] - mb;
+    if (mt == 0) {
+      lo[mc] = make_float4(INF, INF, INF, __uint_as_float(0u));
+      hi[mc] = make_float4(-INF, -INF, -INF, 0.0f);
     }
   }
-  uint32_t inc = len;
+  // the non-empty cells, four at a time: 16 lanes per cell (lane r of a
+  // group fetches row r's bounds), most cells hold a few dozen points
+  const uint64_t busy = __ballot(mc < nc && mt != 0);
+  const int nbusy = __popcll(busy);
+  const int gi = lane >> 4, sl = lane & 15;
+  for (int k0 = 0; k0 < nbusy; k0 += 4) {
+    const int kk = k0 + gi;
+    const bool act = kk < nbusy;
+    uint64_t bm = busy;
+    for (int q = 0; q < kk && bm; ++q) bm &= bm - 1;  // the kk-th set bit
+    const int l = (act && bm) ? __ffsll((unsigned long long)bm) - 1 : 0;
+    const int64_t c = c_base + l;
+    // (every lane shuffles: a cross-lane read inside a condition would read
+    // lanes the condition turned off)
+    const uint32_t base = __shfl(mb, l, 64), tsrc = __shfl(mt, l, 64);
+    const uint32_t total = act ? tsrc : 0u;
+    int cx, cy, cz;
+    coarse_decode(cg, c, cx, cy, cz);
+    const int x0 = 4 * cx, x1 = min(4 * cx + 4, g.dx);
+    uint32_t rs = 0, len = 0;
+    {
+      const int fy = 4 * cy + (sl & 3), fz = 4 * cz + (sl >> 2);
+      if (act && fy < g.dy && fz < g.dz) {
+        const int64_t rb = ((int64_t)fz * g.dy + fy) * g.dx;
+        rs = start[rb + x0];
+        len = start[rb + x1] - rs;
+      }
+    }
+    uint32_t inc = len;
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    const uint32_t v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  const uint32_t excl = inc - len;
-  float l[3] = {INF, INF, INF}, u[3] = {-INF, -INF, -INF};
-  {
-    // the cell's points as one flat list over its rows: lane j takes list
-    // entries j, j + 64, ... (row r = the last row starting at or before the
-    // entry), so one round trip serves 64 points whatever the rows
+    for (int o = 1; o < 16; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o, 16);
+      if (sl >= o) inc += v;
+    }
+    const uint32_t excl = inc - len;
+    float l3[3] = {INF, INF, INF}, u3[3] = {-INF, -INF, -INF};
+    // the cell's points as one flat list over its rows: lane j of the group
+    // takes list entries j, j + 16, ... (row r = the last row starting at or
+    // before the entry)
     uint32_t E[16], S[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      E[r] = __shfl(excl, r, 64);
-      S[r] = __shfl(rs, r, 64) - E[r];  // list entry j of row r is pts[S[r] + j]
+      E[r] = __shfl(excl, r, 16);
+      S[r] = __shfl(rs, r, 16) - E[r];  // list entry j of row r is pts[S[r] + j]
     }
-    for (uint32_t j = lane; j < total; j += 64) {
+    for (uint32_t j = sl; j < total; j += 16) {
       uint32_t src = S[0] + j;
 #pragma unroll
       for (int r = 1; r < 16; ++r) src = (j >= E[r]) ? S[r] + j : src;
       const float4 v = pts[src];
       cpts[base + j] = make_float4(v.x, v.y, v.z, __uint_as_float(src));
-      l[0] = fminf(l[0], v.x);
-      l[1] = fminf(l[1], v.y);
-      l[2] = fminf(l[2], v.z);
-      u[0] = fmaxf(u[0], v.x);
-      u[1] = fmaxf(u[1], v.y);
-      u[2] = fmaxf(u[2], v.z);
+      l3[0] = fminf(l3[0], v.x);
+      l3[1] = fminf(l3[1], v.y);
+      l3[2] = fminf(l3[2], v.z);
+      u3[0] = fmaxf(u3[0], v.x);
+      u3[1] = fmaxf(u3[1], v.y);
+      u3[2] = fmaxf(u3[2], v.z);
     }
 #pragma unroll
     for (int a = 0; a < 3; ++a)
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        l[a] = fminf(l[a], __shfl_xor(l[a], o, 64));
-        u[a] = fmaxf(u[a], __shfl_xor(u[a], o, 64));
+      for (int o = 8; o >= 1; o >>= 1) {
+        l3[a] = fminf(l3[a], __shfl_xor(l3[a], o, 16));
+        u3[a] = fmaxf(u3[a], __shfl_xor(u3[a], o, 16));
       }
-  }
-  if (lane == 0) {
-    lo[c] = make_float4(l[0], l[1], l[2], __uint_as_float(total));
-    hi[c] = make_float4(u[0], u[1], u[2], 0.0f);
+    if (sl == 0 && act) {
+      lo[c] = make_float4(l3[0], l3[1], l3[2], __uint_as_float(total));
+      hi[c] = make_float4(u3[0], u3[1], u3[2], 0.0f);
+    }
   }
 }
 
@@ -739,57 +758,6 @@ __device__ __forceinline__ void group_merge_rolled(Top5& t, int width) {
   }
 }
 
-// Top5 with a payload per entry: the block-row index of the candidate, so the
-// fit phase reloads the winners from the block rows the kNN has just read
-// (L2-resident) instead of from pts.  Same keys and order as Top5.
-struct Top5B {
-  uint64_t k[5];
-  uint32_t b[5];
-};
-
-__device__ __forceinline__ void top5b_clear(Top5B& t) {
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    t.k[j] = kInfKey;
-    t.b[j] = 0xFFFFFFFFu;
-  }
-}
-
-__device__ __forceinline__ void top5b_insert(Top5B& t, uint64_t key, uint32_t bi) {
-  bool c[5];
-#pragma unroll
-  for (int j = 0; j < 5; ++j) c[j] = key < t.k[j];
-#pragma unroll
-  for (int j = 4; j > 0; --j) {
-    t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
-    t.b[j] = c[j - 1] ? t.b[j - 1] : (c[j] ? bi : t.b[j]);
-  }
-  t.k[0] = c[0] ? key : t.k[0];
-  t.b[0] = c[0] ? bi : t.b[0];
-}
-
-template <int CTRL>
-__device__ __forceinline__ void merge_round_dpp_b(Top5B& t) {
-  uint64_t ok[5];
-  uint32_t ob[5];
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    ok[j] = dpp64<CTRL>(t.k[j]);
-    ob[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t.b[j], CTRL, 0xF, 0xF, false);
-  }
-#pragma unroll
-  for (int j = 0; j < 5; ++j) top5b_insert(t, ok[j], ob[j]);
-}
-
-template <int LPQ>
-__device__ __forceinline__ void group_merge_b(Top5B& t) {
-  static_assert(LPQ <= 16, "group_merge_b: up to 16 lanes (DPP)");
-  if (LPQ >= 2) merge_round_dpp_b<0xB1>(t);
-  if (LPQ >= 4) merge_round_dpp_b<0x4E>(t);
-  if (LPQ >= 8) merge_round_dpp_b<0x141>(t);
-  if (LPQ >= 16) merge_round_dpp_b<0x140>(t);
-}
-
 // Conservative lower bound of the distance from coordinate q to the points
 // assigned to grid cell i along one axis (cell edges are known to +-tol).
 __device__ __forceinline__ float axis_gap(float q, int i, float o, float h, float tol) {
@@ -1007,10 +975,10 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
 // The 3x3x3 block from the block rows: one contiguous range, so a flat
 // position is an address (no run lookup); keys carry the pts position (.w),
 // identical to the keys of the 9-run scan.  Same pipeline as scan_flat.
-template <int LPQ, int U, typename TOP>
+template <int LPQ, int U>
 __device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, uint32_t s,
                                                 uint32_t T, int sub, float qx, float qy, float qz,
-                                                TOP& t) {
+                                                Top5& t) {
   uint32_t t0 = sub;
   if (t0 >= T) return;
   constexpr uint32_t kStep = U * LPQ;
@@ -1025,10 +993,7 @@ __device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, 
       const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
       const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
       const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c[u].w);
-      if constexpr (std::is_same<TOP, Top5B>::value)
-        top5b_insert(t, (tb + u * LPQ < T) ? key : kInfKey, s + tb + u * LPQ);
-      else
-        top5_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
+      top5_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
     }
   };
   for (;;) {
@@ -2314,7 +2279,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     alignas(16) uint32_t nb_pos[SLIO_CHUNK][5];
     alignas(16) float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
     alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
-    uint32_t nb_blk[SLIO_CHUNK][5];  // block-row index of each winner of the 3x3x3 fast path (FITB), else ~0
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];
     // deferred (far) queries of this chunk and the far workers' scratch
@@ -2337,14 +2301,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& nb_pos = lds.s.nb_pos;
   auto& nb_sqd = lds.s.nb_sqd;
   auto& nb_idx = lds.s.nb_idx;
-  auto& nb_blk = lds.s.nb_blk;
-  // the fast path's winners carry their block-row index, and the fit phase
-  // reloads them from the block rows (just read by the kNN: L2-resident)
-#ifdef SLIO_NO_FITB
-  constexpr bool FITB = false;
-#else
-  constexpr bool FITB = LPQ == 2 && !SPHERE;
-#endif
   auto& nb_d5 = lds.s.nb_d5;
   auto& qw = lds.s.qw;
   auto& far_cnt = lds.s.far_cnt;
@@ -2390,7 +2346,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     }
     Top5 t;
     top5_clear(t);
-    uint32_t bw[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     const bool finite = live && isfinite(qx) && isfinite(qy) && isfinite(qz) && map.n > 0 &&
                         !far_outside(g, cfg.far_sq, qx, qy, qz);
     int cx = 0, cy = 0, cz = 0, r = 1;
@@ -2420,26 +2375,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           if (b1 < b0 || (int64_t)b1 > map.nblk)
             printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
 #endif
-          if constexpr (FITB) {
-            Top5B tb;
-            top5b_clear(tb);
-            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, tb);
-            group_merge_b<LPQ>(tb);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-              t.k[j] = tb.k[j];
-              bw[j] = tb.b[j];
-            }
-          } else {
-            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
-            group_merge<LPQ>(t);
-          }
+          scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
           if (sub == 0 && out.chunk_cost) atomicAdd(&lds.s.cost, b1 - b0);
         } else {
           RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
           scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
-          group_merge<LPQ>(t);
         }
+        group_merge<LPQ>(t);
         bool covers;
         const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
         const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
@@ -2539,7 +2481,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb_sqd[slot][j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                  : __uint_as_float((uint32_t)(mk >> 32));
         nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
-        if constexpr (FITB) nb_blk[slot][j] = bw[j];
       }
     }
     if (sub == 0) {
@@ -2617,7 +2558,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
               nb_sqd[slot][j] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                        : __uint_as_float((uint32_t)(mk >> 32));
               nb_pos[slot][j] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
-              if constexpr (FITB) nb_blk[slot][j] = 0xFFFFFFFFu;
             }
             nb_d5[slot] = (tr.k[4] != kInfKey) ? d5n : __int_as_float(0x7f800000);
           } else {
@@ -2665,7 +2605,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb_sqd[slot][lane] = (mk == kInfKey) ? __int_as_float(0x7f800000)
                                                     : __uint_as_float((uint32_t)(mk >> 32));
         nb_pos[slot][lane] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
-        if constexpr (FITB) nb_blk[slot][lane] = 0xFFFFFFFFu;
       }
       if (lane == 0)
         nb_d5[slot] = (tf.k[4] != kInfKey) ? __uint_as_float((uint32_t)(tf.k[4] >> 32))
@@ -2706,11 +2645,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           continue;
         }
 #endif
-        if (ps != 0xFFFFFFFFu) {
-          // (kNN-only passes read the map index in .w: from pts)
-          const uint32_t bi = (FITB && !cfg.knn_only) ? nb_blk[slot][j] : 0xFFFFFFFFu;
-          c = bi != 0xFFFFFFFFu ? map.blk[bi] : pts[ps];
-        }
+        if (ps != 0xFFFFFFFFu) c = pts[ps];
         nb[j][0] = c.x;
         nb[j][1] = c.y;
         nb[j][2] = c.z;
@@ -3993,7 +3928,7 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
       rc = fail("coarse scan", e);
       break;
     }
-    k_coarse_fill<<<grid_blocks(m.nccells * 64), 256, 0, st>>>(m.pts, m.start, g, cg, m.cstart, m.nccells,
+    k_coarse_fill<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, cg, m.cstart, m.nccells,
                                                                   m.cpts, m.clo, m.chi);
     if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
       rc = fail("build kernels", e);
@@ -4733,7 +4668,14 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
       rc = SLIO_EDEVICE;
       break;
     }
-    k_ds_conflicts<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, dcount + 1);
+    // Boxes interact only through float rounding: for a power-of-two size
+    // <= 1 (0.5, the reference default) p / ds, floor * ds and + ds are all
+    // exact (|key| < 2^20), every box is exactly [k ds, (k + 1) ds), and no
+    // point can lie outside its own box or in two -- nothing to detect
+    int ds_exp = 0;
+    const bool exact_boxes = std::frexp(ds, &ds_exp) == 0.5f && ds <= 1.0f;
+    if (!exact_boxes)
+      k_ds_conflicts<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, dcount + 1);
     k_ds_groups<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, surv, dcount);
     uint32_t total = 0;
     if ((rc = scan_flags(surv, rank, n, st, &total))) break;
@@ -4781,7 +4723,7 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
 //   addition j, cell c -> new_start[c + 1] - (lb(c + 1) - j)
 // (rank(n0) = the survivor count).  Bit-identical to the sort: same points,
 // same order, same cell table.
-constexpr int kMergeTile = 1024;  // cells per workgroup of k_merge_start
+constexpr int kMergeTile = 4096;  // cells per workgroup of k_merge_start (256 threads x 16)
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t lo, uint32_t hi,
                                                     uint32_t v) {
   while (lo < hi) {
@@ -4793,23 +4735,44 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__
   }
   return lo;
 }
+// jt[t] = lb(t * kMergeTile), t <= ntiles: every tile's first addition, one
+// thread per tile (a per-workgroup search at the head of k_merge_start put
+// ~15 dependent loads in front of every tile: 294 us for the 10M map's grid)
+__global__ void k_merge_tiles(const uint32_t* __restrict__ sk, uint32_t na, int64_t ntiles, int64_t ncells1,
+                              uint32_t* __restrict__ jt) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  jt[t] = lower_bound_u32(sk, 0, na, (uint32_t)min(t * (int64_t)kMergeTile, ncells1));
+}
 __global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict__ old_start,
                                                      const uint32_t* __restrict__ rank, int64_t n0, uint32_t n0p,
-                                                     const uint32_t* __restrict__ sk, uint32_t na,
+                                                     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ jt,
                                                      int64_t ncells1, uint32_t* __restrict__ new_start) {
   __shared__ uint32_t lk[kMergeTile];
-  __shared__ uint32_t jj[2];
   const int64_t c0 = (int64_t)blockIdx.x * kMergeTile;
   const int64_t c1 = min(c0 + (int64_t)kMergeTile, ncells1);
   const int t = threadIdx.x;
-  if (t < 2) jj[t] = lower_bound_u32(sk, 0, na, (uint32_t)(t == 0 ? c0 : c1));
-  __syncthreads();
-  const uint32_t j0 = jj[0], m = jj[1] - j0;
+  const uint32_t j0 = jt[blockIdx.x], m = jt[blockIdx.x + 1] - j0;
   const bool inl = m <= (uint32_t)kMergeTile;
   if (inl)
     for (uint32_t k = t; k < m; k += blockDim.x) lk[k] = sk[j0 + k];
+  // every load of the thread's 16 cells in flight before any use (one round
+  // trip for the cell table, one for the ranks: a load-use chain per cell
+  // made this kernel latency-bound)
+  constexpr int kPer = kMergeTile / 256;
+  uint32_t os[kPer], r[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t c = c0 + t + 256 * u;
+    os[u] = c < c1 ? old_start[c] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) r[u] = (int64_t)os[u] < n0 ? rank[os[u]] : n0p;
   __syncthreads();
-  for (int64_t c = c0 + t; c < c1; c += blockDim.x) {
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t c = c0 + t + 256 * u;
+    if (c >= c1) continue;
     uint32_t lo = 0, hi = m;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -4818,9 +4781,7 @@ __global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict_
       else
         hi = mid;
     }
-    const uint32_t os = old_start[c];
-    const uint32_t r = (int64_t)os < n0 ? rank[os] : n0p;
-    new_start[c] = r + j0 + lo;
+    new_start[c] = r[u] + j0 + lo;
   }
 }
 __global__ void k_merge_pts(const float4* __restrict__ pts, const uint8_t* __restrict__ keep,
@@ -4926,9 +4887,11 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
     if ((e = hipcub::DeviceRadixSort::SortPairs(m.b_tmp[7].p, tb, ak, sk, av, sv, (int)na, 0, cbits, st)))
       return fail("sort", e);
   }
-  const int64_t nc1 = m.ncells + 1;
-  k_merge_start<<<(unsigned)((nc1 + kMergeTile - 1) / kMergeTile), 256, 0, st>>>(m.start, rank, n0, n0p, sk,
-                                                                                 na, nc1, new_start);
+  const int64_t nc1 = m.ncells + 1, ntiles = (nc1 + kMergeTile - 1) / kMergeTile;
+  if ((e = m.take(m.b_tmp[5], 4 * (ntiles + 1)))) return fail("hipMalloc", e);
+  uint32_t* jt = (uint32_t*)m.b_tmp[5].p;
+  k_merge_tiles<<<grid_blocks(ntiles + 1), 256, 0, st>>>(sk, na, ntiles, nc1, jt);
+  k_merge_start<<<(unsigned)ntiles, 256, 0, st>>>(m.start, rank, n0, n0p, sk, jt, nc1, new_start);
   k_merge_pts<<<grid_blocks(n0), 256, 0, st>>>(m.pts, m.keep, rank, m.start, new_start, n0, g, out);
   if (na) k_merge_adds<<<grid_blocks(na), 256, 0, st>>>(acomp, sk, sv, na, new_start, out);
   if ((e = hipGetLastError())) return fail("merge kernels", e);
@@ -4954,7 +4917,7 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, m.cg, m.nccells, cnt);
   if ((e = hipcub::DeviceScan::ExclusiveSum(m.b_tmp[7].p, t3, cnt, m.cstart, (int)(m.nccells + 1), st)))
     return fail("coarse scan", e);
-  k_coarse_fill<<<grid_blocks(m.nccells * 64), 256, 0, st>>>(m.pts, m.start, g, m.cg, m.cstart, m.nccells, m.cpts,
+  k_coarse_fill<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, m.cg, m.cstart, m.nccells, m.cpts,
                                                                m.clo, m.chi);
   if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) return fail("coarse kernels", e);
   m.blk = nullptr;
