@@ -1,5 +1,5 @@
 # usage: bash scripts/gpu_round.sh <tag> <step>...   (one GPU box, steps chained, each under its own limit)
-# steps: tests smoke bench benchc3 benchc5 prof timeline solve ustamps pmc
+# steps: tests smoke bench benchc3 benchc5 prof profc3 timeline solve ustamps pmc
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 tag=$1; shift
@@ -25,6 +25,9 @@ for step in "$@"; do
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 5; }
       for f in $(find gpurun_out/${tag}_prof -name "*kernel_stats.csv"); do head -8 $f; done ;;
+    profc3)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profc3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 300 --warmup 10 --no-cpu-baseline > gpurun_out/${tag}_profc3.log 2>&1 || { echo "profc3 failed"; tail -20 gpurun_out/${tag}_profc3.log; exit 5; }
+      for f in $(find gpurun_out/${tag}_profc3 -name "*kernel_stats.csv"); do head -12 $f | cut -c1-150; done ;;
     timeline)
       timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/${tag}_tl -o run --output-format csv -- python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-kernel-timing > gpurun_out/${tag}_tl.log 2>&1 || { echo "timeline failed"; tail -20 gpurun_out/${tag}_tl.log; exit 5; }
       python scripts/timeline.py gpurun_out/${tag}_tl 320 | tee gpurun_out/${tag}_timeline.txt ;;

@@ -1,5 +1,7 @@
 """Drive the C2 search pass REPS times (for rocprofv3 PMC / ablation runs).
-Env: SLIO_LIB (library path), LPQ, CELL, REPS."""
+Env: SLIO_LIB (library path), LPQ, CELL, REPS, MODE (pass: slio_iterate at the
+initial pose; update: bench.py's step, slio_ikf_update_device in fixed mode,
+4 fused passes)."""
 import ctypes as C
 import json
 import os
@@ -37,6 +39,31 @@ def main():
     bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
     L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]), "scan")
     HTH = np.zeros(78); HTh = np.zeros(12); m = C.c_int64()
+    if os.environ.get("MODE", "pass") == "update":
+        st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9), [0, 0, -9.81]])
+        stats = L.SlioIkfStats()
+        cb = L.ALLREDUCE_FN()
+
+        def upd():
+            xs = L.SlioState()
+            xs.pos[:] = list(st0[0:3]); xs.rot[:] = list(st0[3:7]); xs.rli[:] = list(st0[7:11])
+            xs.tli[:] = list(st0[11:14]); xs.grav[:] = list(st0[23:26])
+            P = np.eye(24) * 1e-2
+            L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, 4, 0, L.SLIO_MODE_FIXED, cb, None,
+                                               C.byref(stats)), "ikf")
+        for _ in range(3):
+            upd()
+        lib.slio_profile(h, 1)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            upd()
+        el = (time.perf_counter() - t0) / reps
+        ms = C.c_double(); n = C.c_int64()
+        lib.slio_profile_read(h, 0, C.byref(ms), C.byref(n))
+        print(json.dumps({"mode": "update", "search_us": ms.value / n.value * 1e3, "update_wall_us": el * 1e6,
+                          "m": stats.last_m}), flush=True)
+        lib.slio_destroy(h)
+        return
     for _ in range(3):
         L.check(lib.slio_iterate(h, C.byref(pose), 1, 0, L.dptr(HTH), L.dptr(HTh), C.byref(m)), "it")
     lib.slio_profile(h, 1)
