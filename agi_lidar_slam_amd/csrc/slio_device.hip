@@ -3256,7 +3256,8 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   // later passes of a device-resident update take their chunks in the order
   // the previous pass's costs call for (chunk_order; pass 0 in index order)
   static const bool no_order = std::getenv("SLIO_NO_CHUNK_ORDER") != nullptr;
-  cfg.perm = (devpose && c.cus_per_xcd > 0 && !no_order) ? c.chunk_perm : nullptr;
+  // (fused passes compute no order: c.chunk_perm may be another scan's)
+  cfg.perm = (devpose && !fuse && c.cus_per_xcd > 0 && !no_order) ? c.chunk_perm : nullptr;
   if (int rc = map_refresh(c); rc) return rc;
   if (which != 0 && c.map->blk_deferred) {
     std::unique_lock<std::shared_mutex> lk(c.map->mu);

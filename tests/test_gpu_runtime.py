@@ -405,3 +405,29 @@ def test_c5_50M_map_exact_and_replay(L, oracle_mod):
             rp.close()
         if base is not None:
             lib.slio_destroy(base)
+
+
+def test_fused_after_reference_other_scan(L, c2):
+    """A fused update after a two-launch update of a LARGER scan on the same
+    handle (whose chunk order is left behind) equals the fused update on a
+    fresh handle, bit for bit."""
+    mp, fr, _ = c2
+    st = state_of(fr)
+    lib = L.load()
+    big = np.ascontiguousarray(fr.body)
+    small = np.ascontiguousarray(fr.body[:30_011])
+    ha, hb = mk(L, cell=C2_CELL), mk(L, cell=C2_CELL)
+    try:
+        upload_map(L, ha, mp)
+        L.check(lib.slio_map_share(hb, ha), "share")
+        assert upload_scan(L, ha, big) == 0
+        _update_once(L, ha, st, mode=0)          # reference control flow: two launches, chunk order
+        assert upload_scan(L, ha, small) == 0
+        assert upload_scan(L, hb, small) == 0
+        one = _update_once(L, ha, st)
+        two = _update_once(L, hb, st)
+        for a, b in zip(one, two):
+            np.testing.assert_array_equal(a, b)
+    finally:
+        lib.slio_destroy(hb)
+        lib.slio_destroy(ha)
