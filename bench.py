@@ -117,34 +117,49 @@ def bench_c3(args, rank, world, dev, dist):
     if world > 1:
         dist.barrier()
     L.load()
-    sc = synth.make_ouster_scan(seed=20261015 + rank)
-    tb = imu_deskew_table(sc["imu_stamps"], sc["imu_gyro"], sc["time_scan_cur"], sc["time_scan_end"])
-    fe = LioSamFrontEnd(LioSamParams(N_SCAN=64, Horizon_SCAN=2048), device=dev)
-    fe.set_deskew(*tb[:4], sc["time_scan_cur"], tb[4])
-    fe.upload(sc["x"], sc["y"], sc["z"], sc["intensity"], sc["ring"], sc["time"])
+    S = max(1, args.c3_streams)
+    fes, scs = [], []
+    for j in range(S):
+        # stream j: its own handle, stream and scan (distinct seeds)
+        sc_j = synth.make_ouster_scan(seed=20261015 + rank + 7919 * j)
+        tb_j = imu_deskew_table(sc_j["imu_stamps"], sc_j["imu_gyro"], sc_j["time_scan_cur"],
+                                sc_j["time_scan_end"])
+        fe_j = LioSamFrontEnd(LioSamParams(N_SCAN=64, Horizon_SCAN=2048), device=dev)
+        fe_j.set_deskew(*tb_j[:4], sc_j["time_scan_cur"], tb_j[4])
+        fe_j.upload(sc_j["x"], sc_j["y"], sc_j["z"], sc_j["intensity"], sc_j["ring"], sc_j["time"])
+        fes.append(fe_j)
+        scs.append((sc_j, tb_j))
+    fe = fes[0]
+    sc, tb = scs[0]
     lib, h = fe.lib, fe.h
     for _ in range(args.warmup):
-        fe.run()
+        for f in fes:
+            f.run()
     counts = L.SlioLioCounts()
     lib.slio_lio_profile(h, 0)
-    every = max(1, args.timing_every)
     if world > 1:
         dist.barrier()
-    L.check(lib.slio_lio_get_counts(h, C.byref(counts)), "counts")
+    for f in fes:
+        L.check(lib.slio_lio_get_counts(f.h, C.byref(counts)), "counts")
     t0 = time.perf_counter()
     for k in range(args.steps):
-        timed = not args.no_kernel_timing and k % every == 0
-        if timed:
-            lib.slio_lio_profile(h, 1 | L.SLIO_LIO_PROFILE_KEEP)
-        rc = lib.slio_lio_run_async(h)
-        if rc:
-            L.check(rc, "slio_lio_run_async")
-        if timed:
-            lib.slio_lio_profile(h, L.SLIO_LIO_PROFILE_KEEP)
-    L.check(lib.slio_lio_get_counts(h, C.byref(counts)), "counts")  # waits for the stream
+        for f in fes:  # S scans in flight, one per stream
+            rc = lib.slio_lio_run_async(f.h)
+            if rc:
+                L.check(rc, "slio_lio_run_async")
+    for f in fes:
+        L.check(lib.slio_lio_get_counts(f.h, C.byref(counts)), "counts")  # waits for each stream
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # the feature stage's kernel time: HIP events on further scans of stream
+    # 0 alone, after the timed region (events cost idle time per launch)
+    if not args.no_kernel_timing:
+        lib.slio_lio_profile(h, 1)
+        for k in range(max(1, args.timing_steps)):
+            L.check(lib.slio_lio_run_async(h), "slio_lio_run_async")
+        lib.slio_lio_profile(h, 1 | L.SLIO_LIO_PROFILE_KEEP)
+    L.check(lib.slio_lio_get_counts(h, C.byref(counts)), "counts")
     ms, nl = C.c_double(), C.c_int64()
     lib.slio_lio_profile_read(h, C.byref(ms), C.byref(nl))
     if world > 1:
@@ -152,7 +167,7 @@ def bench_c3(args, rank, world, dev, dist):
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    value = args.steps * world / el
+    value = args.steps * S * world / el
     avg_s = (ms.value / max(nl.value, 1)) * 1e-3
     n_ext, nc, ns = counts.n_extracted, counts.n_corner, counts.n_surface
     # feature stage (k_fe_pick .. k_fe_voxel) compulsory bytes: per extracted point curvature 4 + column 4
@@ -191,6 +206,7 @@ def bench_c3(args, rank, world, dev, dist):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (points, ranges, curvature) + f64 (deskew interpolation, trig)",
+        "streams": S,
         "data": "synthetic (seeded urban scene, OS1-64-like 64 x 2048 sweep with IMU deskew)",
         "config": {
             "workload": ("C3: LIO-SAM ImageProjection::projectPointCloud/cloudExtraction + "
@@ -200,8 +216,10 @@ def bench_c3(args, rank, world, dev, dist):
             "points_extracted": int(n_ext),
             "corners": int(nc),
             "surface": int(ns),
-            "parallelism": (f"replicas x{world}: one scan stream per GPU, no collective"
-                            if world > 1 else "single GPU"),
+            "parallelism": ((f"replicas x{world}: one scan stream per GPU, no collective"
+                             if world > 1 else "single GPU")
+                            + (f"; {S} independent scans in flight per GPU (own handle and stream each)"
+                               if S > 1 else "")),
         },
         "roofline": {
             "bound": "hbm",
@@ -214,13 +232,15 @@ def bench_c3(args, rank, world, dev, dist):
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_us": avg_s * 1e6,
             "launches": int(nl.value),
-            "timing": f"HIP events in the dispatch packet, 1 in {every} timed steps",
+            "timing": (f"HIP events in the dispatch packet, {args.timing_steps} further scans of one "
+                       "stream after the timed region"),
         },
         "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    fe.close()
+    for f in fes:
+        f.close()
 
 
 def bench_c5(args, rank, world, dev, dist):
@@ -349,8 +369,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP events on the search kernel (roofline fields null)")
-    ap.add_argument("--timing-every", type=int, default=5,
-                    help="c3: time the feature stage (HIP events) on every k-th timed step")
     ap.add_argument("--timing-steps", type=int, default=40,
                     help="c2: steps after the timed region whose search launches carry HIP events "
                          "(roofline.avg_launch_us)")
@@ -369,6 +387,9 @@ def main():
                          "instead of the library's own RCCL communicator (slio_comm_init); implied by "
                          "--dist-backend gloo (RCCL refuses two ranks on one device)")
     ap.add_argument("--cpu-scans-c3", type=int, default=300)
+    ap.add_argument("--c3-streams", type=int, default=1,
+                    help="c3: independent scans in flight per GPU, each on its own handle and stream "
+                         "(1: one scan stream, the latency-bound rate)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path with several ranks on one GPU)")
