@@ -3177,13 +3177,20 @@ static hipError_t wait_stream(Ctx& c) {
 // (ctl->done) and touch neither the mapped block nor the caller's buffers.
 static hipError_t wait_published(Ctx& c) {
   hipError_t e;
-  if (!c.done_ev && (e = hipEventCreateWithFlags(&c.done_ev, hipEventDisableTiming))) return e;
-  if ((e = hipEventRecord(c.done_ev, c.stream))) return e;
+  // the stream itself is queried now and then (a failed or early-exiting
+  // launch still ends the wait): no completion-event packet behind the
+  // update's kernels (SLIO_EVENT_WAIT=1: the round-2 event record + query)
+  const char* ev_env = std::getenv("SLIO_EVENT_WAIT");
+  const bool use_event = ev_env && ev_env[0] && ev_env[0] != '0';
+  if (use_event) {
+    if (!c.done_ev && (e = hipEventCreateWithFlags(&c.done_ev, hipEventDisableTiming))) return e;
+    if ((e = hipEventRecord(c.done_ev, c.stream))) return e;
+  }
   volatile int32_t* pub = &c.h_ctl->published;
   for (uint32_t it = 1;; ++it) {
     if (*pub) break;
     if ((it & 255) == 0) {
-      e = hipEventQuery(c.done_ev);
+      e = use_event ? hipEventQuery(c.done_ev) : hipStreamQuery(c.stream);
       if (e != hipErrorNotReady) {
         if (e != hipSuccess) return e;
         break;  // all work done: the flags tell whether it published
@@ -4016,6 +4023,49 @@ __device__ __forceinline__ uint64_t ds_key(int64_t kx, int64_t ky, int64_t kz) {
          (uint64_t)((kz + (1 << 20)) & 0x1FFFFF);
 }
 
+// the call's voxel-key range per axis (atomic min / max of floor(p / ds),
+// reduced per wavefront first)
+__global__ void k_ds_range(const float4* __restrict__ in, int64_t n, float ds, int32_t* __restrict__ rg) {
+  int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 p = in[i];
+    const int32_t k[3] = {(int32_t)floorf(p.x / ds), (int32_t)floorf(p.y / ds), (int32_t)floorf(p.z / ds)};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = min(lo[a], k[a]);
+      hi[a] = max(hi[a], k[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int d = 32; d > 0; d >>= 1) {
+      lo[a] = min(lo[a], __shfl_xor(lo[a], d, 64));
+      hi[a] = max(hi[a], __shfl_xor(hi[a], d, 64));
+    }
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(&rg[a], lo[a]);
+      atomicMax(&rg[3 + a], hi[a]);
+    }
+}
+// keys packed relative to the call's range (groups by equality only)
+struct DsPack {
+  int32_t mx, my, mz;
+  int sy, sz;  // shifts of the x and y fields
+};
+__global__ void k_ds_keys_packed(const float4* __restrict__ in, int64_t n, float ds, DsPack pk,
+                                 uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  const uint64_t kx = (uint64_t)((int64_t)(int32_t)floorf(p.x / ds) - pk.mx);
+  const uint64_t ky = (uint64_t)((int64_t)(int32_t)floorf(p.y / ds) - pk.my);
+  const uint64_t kz = (uint64_t)((int64_t)(int32_t)floorf(p.z / ds) - pk.mz);
+  keys[i] = (kx << pk.sy) | (ky << pk.sz) | kz;
+  vals[i] = (uint32_t)i;
+}
+
 __global__ void k_ds_keys(const float4* __restrict__ in, int64_t n, float ds, uint64_t* __restrict__ keys,
                           uint32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4640,7 +4690,7 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     auto& B = m.b_add;
     if ((e = m.take(B[0], 8 * n)) || (e = m.take(B[1], 8 * n)) || (e = m.take(B[2], 4 * n)) ||
         (e = m.take(B[3], 4 * n)) || (e = m.take(B[4], 4 * n)) || (e = m.take(B[5], 4 * n)) ||
-        (e = m.take(B[6], 16))) {
+        (e = m.take(B[6], 64))) {
       set_error(std::string("slio map: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
       break;
@@ -4662,19 +4712,51 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     tmp = B[7].p;
     tb = B[7].cap;
     const int nb = grid_blocks(n);
-    k_ds_keys<<<nb, 256, 0, st>>>(in, n, ds, k0, v0);
-    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 63, st)) ||
-        (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 16, st))) {
-      set_error(std::string("slio map: sort: ") + hipGetErrorString(e));
-      rc = SLIO_EDEVICE;
-      break;
-    }
     // Boxes interact only through float rounding: for a power-of-two size
     // <= 1 (0.5, the reference default) p / ds, floor * ds and + ds are all
     // exact (|key| < 2^20), every box is exactly [k ds, (k + 1) ds), and no
     // point can lie outside its own box or in two -- nothing to detect
     int ds_exp = 0;
     const bool exact_boxes = std::frexp(ds, &ds_exp) == 0.5f && ds <= 1.0f;
+    // Then only key equality matters (k_ds_groups; k_ds_conflicts and
+    // k_ds_sequential, which look keys up by value, do not run): the keys are
+    // packed relative to the call's voxel range, so the radix sort covers a
+    // few dozen bits instead of 63 (8 onesweep passes: ~100 us for ~20k keys)
+    int sort_bits = 63;
+    if (exact_boxes) {
+      int32_t* rg = (int32_t*)((char*)B[6].p + 16);  // after dcount (B[6]: 64 bytes)
+      const int32_t init[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
+      int32_t got[6];
+      if ((e = hipMemcpyAsync(rg, init, 24, hipMemcpyHostToDevice, st))) {
+        set_error(std::string("slio map: range: ") + hipGetErrorString(e));
+        rc = SLIO_EDEVICE;
+        break;
+      }
+      k_ds_range<<<std::min(nb, 256), 256, 0, st>>>(in, n, ds, rg);
+      if ((e = hipMemcpyAsync(got, rg, 24, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+        set_error(std::string("slio map: range: ") + hipGetErrorString(e));
+        rc = SLIO_EDEVICE;
+        break;
+      }
+      int bits[3];
+      for (int a = 0; a < 3; ++a) {
+        const int64_t span = (int64_t)got[3 + a] - (int64_t)got[a] + 1;
+        bits[a] = 0;
+        while (bits[a] < 40 && ((int64_t)1 << bits[a]) < span) ++bits[a];
+      }
+      if (bits[0] + bits[1] + bits[2] <= 48) {
+        sort_bits = std::max(1, bits[0] + bits[1] + bits[2]);
+        const DsPack pk{got[0], got[1], got[2], bits[1] + bits[2], bits[2]};
+        k_ds_keys_packed<<<nb, 256, 0, st>>>(in, n, ds, pk, k0, v0);
+      }
+    }
+    if (sort_bits == 63) k_ds_keys<<<nb, 256, 0, st>>>(in, n, ds, k0, v0);
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, sort_bits, st)) ||
+        (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 16, st))) {
+      set_error(std::string("slio map: sort: ") + hipGetErrorString(e));
+      rc = SLIO_EDEVICE;
+      break;
+    }
     if (!exact_boxes)
       k_ds_conflicts<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, dcount + 1);
     k_ds_groups<<<nb, 256, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, surv, dcount);
