@@ -29,7 +29,7 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profc3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 300 --warmup 10 --no-cpu-baseline > gpurun_out/${tag}_profc3.log 2>&1 || { echo "profc3 failed"; tail -20 gpurun_out/${tag}_profc3.log; exit 5; }
       for f in $(find gpurun_out/${tag}_profc3 -name "*kernel_stats.csv"); do head -12 $f | cut -c1-150; done ;;
     timeline)
-      timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/${tag}_tl -o run --output-format csv -- python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-kernel-timing > gpurun_out/${tag}_tl.log 2>&1 || { echo "timeline failed"; tail -20 gpurun_out/${tag}_tl.log; exit 5; }
+      timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/${tag}_tl -o run --output-format csv -- python3 bench.py --steps 150 --warmup 3 --no-cpu-baseline --no-kernel-timing > gpurun_out/${tag}_tl.log 2>&1 || { echo "timeline failed"; tail -20 gpurun_out/${tag}_tl.log; exit 5; }
       python scripts/timeline.py gpurun_out/${tag}_tl 320 | tee gpurun_out/${tag}_timeline.txt ;;
     solve)
       SLIO_LIB=agi_lidar_slam_amd/_abl/libslio_SOLVE.so timeout -k 10 200 python scripts/solve_stamps.py > gpurun_out/${tag}_solve.log 2>&1 || { echo "solve failed"; tail gpurun_out/${tag}_solve.log; exit 6; }
