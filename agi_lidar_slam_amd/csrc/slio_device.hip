@@ -2068,9 +2068,10 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
 // written by other workgroups of this launch) and adds them in registers (8
 // super rows, then their ordered total -- the tree step_totals uses); the
 // other 165 threads load the control block meanwhile (one round trip, no LDS
-// staging of the rows).  DXN_SC1: dx_new was written in this launch (by
-// block 0 of a fused search pass), so it is read past the L2 as well.
-template <int NT, int D, bool DXN_SC1>
+// staging of the rows).  CTL_SC1: parts of the block were written in this
+// launch (dx_new by block 0 of a fused pass; the whole block by the first
+// fused pass's prefetch), so every control load goes past the L2 (sc1).
+template <int NT, int D, bool CTL_SC1>
 __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, double* super_out, IkfCtl* ctl,
                                            const IkfCtl* src, IkfCtl* hblk, double R, int iter, int maxit) {
   const int t = threadIdx.x;
@@ -2098,7 +2099,6 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
     for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
   } else {
     constexpr int NC = NT - SLIO_NPROD, nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
-    constexpr int kDxn = nC - CtlList<D>::nD;  // dx_new: the list's last 24 entries
     const int tt = t - SLIO_NPROD;
     const bool first = src != ctl;
     const gdouble* gc = (const gdouble*)(const double*)src;
@@ -2106,13 +2106,16 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       const int e = tt + u * NC;
-      if (DXN_SC1 && e >= kDxn)
+      if (CTL_SC1)
         cv[u] = e < nC ? ld_sc1(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : 0.0;
       else
         cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
     }
     typedef __attribute__((address_space(1))) int32_t gint;
-    const int32_t fl = tt < 8 ? ((const gint*)(const int32_t*)&src->converge)[tt] : 0;
+    int32_t fl = 0;
+    if (tt < 8)
+      fl = CTL_SC1 ? (int32_t)ld_sc1_u32(reinterpret_cast<const uint32_t*>(&src->converge) + tt)
+                   : ((const gint*)(const int32_t*)&src->converge)[tt];
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       const int e = tt + u * NC;
@@ -2170,6 +2173,9 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
 // completes the 64th row runs final_step.
 struct FuseArgs {
   IkfCtl* ctl;        // the update's control block in HBM
+  const IkfCtl* pre;  // first pass: the mapped host block, copied into ctl by block 0 at
+                      // the launch's start (its PCIe round trip hidden behind the search),
+                      // so the filter step reads HBM (src == ctl); else null
   double* seg_out;    // 64 segment rows
   double* super_out;  // 8 super rows (slio_super_download)
   const IkfCtl* src;  // control block source (ctl: passes after the first)
@@ -2193,6 +2199,26 @@ __device__ __forceinline__ int seg_of_chunk(int64_t C, int64_t c, int64_t& lim) 
   return s * kSuperSeg + g;
 }
 
+// The first fused pass: block 0 copies the control list (x, x_prop, P,
+// P_DD^-1, G, dx_new) and the flags from the caller's mapped host block into
+// the HBM block, write-through, at the start of the launch; its stores drain
+// before its chunk's arrival, so the filter step (after every arrival) reads
+// them from HBM (sc1) instead of over PCIe (measured: the staging step of the
+// first pass took 5.7 us against 2.4 us for the later passes).
+__device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, IkfCtl* __restrict__ ctl) {
+  constexpr int nC = CtlList<6>::total;
+  const double* hs = reinterpret_cast<const double*>(hsrc);
+  double* cd = reinterpret_cast<double*>(ctl);
+  for (int e = threadIdx.x; e < nC; e += blockDim.x) {
+    const int o = ctl_src<6>(e);
+    st_sc1(cd + o, hs[o]);
+  }
+  if (threadIdx.x < 8)
+    st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->converge) + threadIdx.x,
+               reinterpret_cast<const uint32_t*>(&hsrc->converge)[threadIdx.x]);
+  if (threadIdx.x == 8) st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->singular), 0u);
+}
+
 // After the chunk partial is stored (sc1): arrival on the chunk's segment row;
 // the last arrival sums the row, and the last row runs the filter step.
 // Every thread of the workgroup calls it.
@@ -2202,10 +2228,19 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
   const int t = threadIdx.x;
   int64_t lim;
   const int b = seg_of_chunk(fa.C, chunk, lim);
+#ifdef SLIO_SOLVE_STAMP
+  // the final workgroup's tail: partial issued, segment arrival, row stored,
+  // row arrival (g_sstamp[16..19]); the launch's first block start is [20]
+  unsigned long long ts[4] = {0, 0, 0, 0};
+  if (t == 0) ts[0] = wall_clock64();
+#endif
   drain_stores();
   __syncthreads();
   if (t == 0) bcast = (int)arrive(fa.cnt + kSegCnt + b);
   __syncthreads();
+#ifdef SLIO_SOLVE_STAMP
+  if (t == 0) ts[1] = wall_clock64();
+#endif
   if (bcast != (int)lim - 1) return;
   if (t < SLIO_NPROD) {
     const int s = b / kSuperSeg, g = b - s * kSuperSeg;
@@ -2224,9 +2259,18 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
   if (t == 0) reset_counter(fa.cnt + kSegCnt + b);
   drain_stores();
   __syncthreads();
+#ifdef SLIO_SOLVE_STAMP
+  if (t == 0) ts[2] = wall_clock64();
+#endif
   if (t == 0) bcast = (int)arrive(fa.cnt);
   __syncthreads();
   if (bcast != kNSeg - 1) return;
+#ifdef SLIO_SOLVE_STAMP
+  if (t == 0) {
+    ts[3] = wall_clock64();
+    for (int k = 0; k < 4; ++k) g_sstamp[16 + k] = ts[k];
+  }
+#endif
   if (t == 0) {
     reset_counter(fa.cnt);
     // the pass's number of far queries (slio_far_queries); queue reset
@@ -2252,6 +2296,11 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
     const PassOut out, const FuseArgs fa) {
   static_assert(!FUSE || search_block<LPQ>() == kSolveThreads, "fused pass: 256 threads");
+#ifdef SLIO_SOLVE_STAMP
+  if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) g_sstamp[20] = wall_clock64();
+#endif
+  if constexpr (FUSE && !DEVPOSE)
+    if (blockIdx.x == 0 && fa.pre) prefetch_ctl(fa.pre, fa.ctl);
   // DEVPOSE: pose and pass selection come from the device-resident update
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
@@ -6404,7 +6453,8 @@ struct UpdateRun {
           return SLIO_EINVAL;
         }
       }
-      const FuseArgs fa{c.ctl, c.d_seg, c.d_super, sa.src, c.d_hctl, c.count, R, i, maxit, num_chunks(c.n)};
+      const FuseArgs fa{c.ctl, p0 ? (const IkfCtl*)c.d_hctl : nullptr, c.d_seg, c.d_super, c.ctl, c.d_hctl,
+                        c.count, R, i, maxit, num_chunks(c.n)};
       int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
       if (rc) return rc;
       SLIO_HIP(hipGetLastError());

@@ -1,7 +1,12 @@
+# round-3 session check: fused-pass GPU tests, tail stamps, same-box in-process A/B vs the previous tree
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_chain.py tests/test_gpu_runtime.py -x -v --timeout 120 --timeout-method thread -m gpu > gpurun_out/r03i_tests.log 2>&1; rc=$?; tail -3 gpurun_out/r03i_tests.log; grep -E "FAILED|Error" gpurun_out/r03i_tests.log | head -5
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python scripts/bench_aux.py mapping > gpurun_out/r03i_mapping.jsonl 2>&1 || { echo "mapping failed"; tail gpurun_out/r03i_mapping.jsonl; exit 6; }
-cut -c1-400 gpurun_out/r03i_mapping.jsonl
-timeout -k 10 400 python scripts/ab_inproc.py - SLIO_EVENT_WAIT=1 --rounds 7 > gpurun_out/r03i_ab.log 2>&1 || { echo "ab failed"; tail gpurun_out/r03i_ab.log; exit 5; }
-cat gpurun_out/r03i_ab.log
+tag=${1:-r03n}
+timeout -k 10 300 python -u -m pytest tests/test_gpu_runtime.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/${tag}_tests.log 2>&1 || { tail -20 gpurun_out/${tag}_tests.log; exit 3; }
+tail -1 gpurun_out/${tag}_tests.log
+SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so timeout -k 10 200 python scripts/tail_stamps.py > gpurun_out/${tag}_tail.log 2>&1 || { tail gpurun_out/${tag}_tail.log; exit 4; }
+grep maxit gpurun_out/${tag}_tail.log
+for k in 1 2; do
+  timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/main /" || exit 5
+  SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_prev.so timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/prev /" || exit 5
+done > gpurun_out/${tag}_ab.log 2>&1
+cat gpurun_out/${tag}_ab.log
