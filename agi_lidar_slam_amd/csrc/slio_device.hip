@@ -1860,10 +1860,15 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
       hblk->last_m = m;
       hblk->singular = 0;
     }
-    // every thread's stores, then one release store the host polls for
-    __threadfence_system();
+    // every thread's stores complete, then ONE system-scope release (the L2
+    // write-back of the fence covers the whole workgroup's stores) and the
+    // word the host polls for (a fence in each of the 256 threads cost ~2 us)
+    drain_stores();
     __syncthreads();
-    if (t == 0) __hip_atomic_store(&hblk->published, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) {
+      __threadfence_system();
+      __hip_atomic_store(&hblk->published, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   SSTAMP(8);
 }
