@@ -163,6 +163,8 @@ class SlioImuPose(C.Structure):
 
 
 SLIO_COMM_ID_BYTES = 128
+SLIO_GROUP_RCCL = 1
+SLIO_GROUP_DEVICE = 2
 
 SIGNATURES = {
     "slio_params_default": (C.c_int, [C.POINTER(SlioParams)]),
@@ -176,6 +178,7 @@ SIGNATURES = {
     "slio_create_group": (C.c_int, [C.POINTER(_P), C.c_int, _IP, C.POINTER(SlioParams)]),
     "slio_group_ikf_update": (C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(SlioState), _DP, C.c_double, C.c_int,
                                         C.c_int, C.c_int, C.POINTER(SlioIkfStats)]),
+    "slio_group_reduce_kind": (C.c_int, [_P]),
     "slio_comm_unique_id": (C.c_int, [_U8P]),
     "slio_comm_init": (C.c_int, [_P, _U8P]),
     "slio_map_info": (C.c_int, [_P, _IP, _FP, _I64P]),

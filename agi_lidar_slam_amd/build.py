@@ -64,14 +64,28 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every source to an object in parallel (the two HIP files take
+    most of the time), then link the shared library."""
     if not force and not _stale():
         return LIB
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    cmd = [HIPCC, *FLAGS, f'-DSLIO_SOURCE_HASH="{source_hash()}"', "-I", os.path.join(ROOT, "include"),
-           *srcs, "-o", LIB + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    tag = source_hash()
+    compile_flags = [f for f in FLAGS if f != "-shared" and not f.startswith(("-L", "-l", "-Wl"))]
+    objs, procs = [], []
+    for src in srcs:
+        obj = os.path.join(PKG, "_obj", os.path.basename(src) + ".o")
+        os.makedirs(os.path.dirname(obj), exist_ok=True)
+        cmd = [HIPCC, *compile_flags, f'-DSLIO_SOURCE_HASH="{tag}"', "-I", os.path.join(ROOT, "include"),
+               "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    link = [HIPCC, *FLAGS, *objs, "-o", LIB + ".tmp"]
+    subprocess.run(link, check=True)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

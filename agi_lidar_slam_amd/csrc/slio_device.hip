@@ -2141,6 +2141,49 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
 template <int LPQ>
 constexpr int search_block() { return LPQ == 1 ? SLIO_CHUNK : kBlock; }
 
+// One point of a non-search pass (esekfom.hpp:138-150 with converge ==
+// false): the cached plane and selection of the last search pass, the
+// residual gate re-evaluated at this pass's pose (:157-173), the Jacobian row
+// (:197-226) into row[kRow] (zeros when not selected).  Shared by k_reuse_pass
+// and the reuse branch of a fused pass, so both give the same rows.
+__device__ __forceinline__ void reuse_row(const ScanDev& scan, const PoseDev& pose, const PassCfg& cfg,
+                                          const PassOut& out, int64_t i, double (&row)[kRow]) {
+#pragma unroll
+  for (int j = 0; j < kRow; ++j) row[j] = 0.0;
+  if (i >= scan.n) return;
+  bool sel = out.sel[i] != 0;
+  float pd2 = __int_as_float(0x7fc00000);
+  if (sel) {
+    const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
+    float qx, qy, qz;
+    body_to_world(pose, bx, by, bz, qx, qy, qz);
+    const float4 pl = out.plane[i];
+    const float abcd[4] = {pl.x, pl.y, pl.z, pl.w};
+    sel = residual_gate(abcd, qx, qy, qz, bx, by, bz, pd2);
+    if (sel) {
+      double h[12];
+      jacobian_row(pose, bx, by, bz, abcd[0], abcd[1], abcd[2], cfg.extrinsic != 0, h);
+#pragma unroll
+      for (int j = 0; j < 12; ++j) row[j] = h[j];
+      row[12] = -(double)pd2;
+      row[13] = 1.0;
+    }
+    out.sel[i] = sel ? 1 : 0;
+  }
+  out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
+}
+
+// The chunk's 91 products of the rows in LDS (256 threads): on the matrix
+// cores, or the VALU form under SLIO_NO_MFMA.  sc1: the partial is read by
+// another workgroup of the same launch (fused pass).
+__device__ __forceinline__ void chunk_sums_256(double (*rows)[kRow], double (*part)[SLIO_NPROD],
+                                               double* out, bool mfma, bool sc1) {
+  if (mfma)
+    chunk_products_mfma<256>(rows, out, sc1);
+  else
+    chunk_products<256>(rows, part, out, sc1);
+}
+
 // dx_new = x [-] x_propagated (esekfom.hpp:236-258) of the iterate a
 // device-resident pass runs at, for that pass's filter step: formed by block
 // 0 of the pass kernel (lanes 0..23 the vector blocks, lanes 32 / 64 the
@@ -2210,12 +2253,13 @@ __device__ __forceinline__ int seg_of_chunk(int64_t C, int64_t c, int64_t& lim) 
 // before its chunk's arrival, so the filter step (after every arrival) reads
 // them from HBM (sc1) instead of over PCIe (measured: the staging step of the
 // first pass took 5.7 us against 2.4 us for the later passes).
+template <int D>
 __device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, IkfCtl* __restrict__ ctl) {
-  constexpr int nC = CtlList<6>::total;
+  constexpr int nC = CtlList<D>::total;
   const double* hs = reinterpret_cast<const double*>(hsrc);
   double* cd = reinterpret_cast<double*>(ctl);
   for (int e = threadIdx.x; e < nC; e += blockDim.x) {
-    const int o = ctl_src<6>(e);
+    const int o = ctl_src<D>(e);
     st_sc1(cd + o, hs[o]);
   }
   if (threadIdx.x < 8)
@@ -2227,7 +2271,7 @@ __device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, Ik
 // After the chunk partial is stored (sc1): arrival on the chunk's segment row;
 // the last arrival sums the row, and the last row runs the filter step.
 // Every thread of the workgroup calls it.
-template <int NT>
+template <int NT, int D>
 __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl,
                                            const double* chunk_part, int64_t chunk) {
   const int t = threadIdx.x;
@@ -2283,7 +2327,7 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     st_sc1_u32(fa.cnt + 4, 0u);
     st_sc1_u32(fa.cnt + 5, 0u);
   }
-  final_step<NT, 6, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+  final_step<NT, D, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
 }
 
 // One h_share_model search pass over one 128-point chunk.
@@ -2296,7 +2340,7 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
 #ifndef SLIO_RL8_MAX
 #define SLIO_RL8_MAX 8
 #endif
-template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE = false>
+template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE = false, int FD = 6>
 __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
     const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
     const PassOut out, const FuseArgs fa) {
@@ -2305,10 +2349,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) g_sstamp[20] = wall_clock64();
 #endif
   if constexpr (FUSE && !DEVPOSE)
-    if (blockIdx.x == 0 && fa.pre) prefetch_ctl(fa.pre, fa.ctl);
-  // DEVPOSE: pose and pass selection come from the device-resident update
+    if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
+  // DEVPOSE: pose and pass selection come from the device-resident update.
+  // A fused pass runs whichever pass the update wants (search or reuse,
+  // ctl->search_now = converge, esekfom.hpp:138): one launch per pass in the
+  // reference control flow too.
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
-                  cfg.ctl->search_now != cfg.want_search))
+                  (!FUSE && cfg.ctl->search_now != cfg.want_search)))
     return;
   const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
   constexpr int NT = search_block<LPQ>();
@@ -2366,6 +2413,21 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& far_pre = lds.s.far_pre;
   auto& far_beg = lds.s.far_beg;
   int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
+  if constexpr (FUSE && DEVPOSE) {
+    if (!cfg.ctl->search_now) {
+      // reuse pass (k_reuse_pass's rows and products), then the fused tail
+      if (threadIdx.x < SLIO_CHUNK) {
+        double row[kRow];
+        reuse_row(scan, pose, cfg, out, chunk * SLIO_CHUNK + threadIdx.x, row);
+#pragma unroll
+        for (int j = 0; j < kRow; ++j) lds.s.rr.rows[threadIdx.x][j] = row[j];
+      }
+      __syncthreads();
+      chunk_sums_256(lds.s.rr.rows, lds.s.part, out.chunk_part + chunk * SLIO_NPROD, cfg.mfma, true);
+      fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
+      return;
+    }
+  }
   if (cfg.perm) {
     // (a permutation of [0, nblk) by construction; the range check only
     // keeps a corrupt order from writing outside the chunk arrays)
@@ -2768,12 +2830,12 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
-  if (NT == 256 && cfg.mfma)
-    chunk_products_mfma<256>(rows, out.chunk_part + chunk * SLIO_NPROD, FUSE);
+  if constexpr (NT == 256)
+    chunk_sums_256(rows, part, out.chunk_part + chunk * SLIO_NPROD, cfg.mfma, FUSE);
   else
     chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, FUSE);
   if (tid == 0) STAMP(3);
-  if constexpr (FUSE) fused_tail<NT>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
+  if constexpr (FUSE) fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
 }
 
 // Nearest_Points ids and pointSearchSqDis of the last search pass, derived
@@ -2806,50 +2868,30 @@ __global__ __launch_bounds__(256) void k_nbr_derive(const ScanDev scan, const fl
 }
 
 // Non-search pass: reuse neighbours/plane/selection (esekfom.hpp:138-150 with
-// converge == false), one lane per point.
+// converge == false), one lane per point (threads < 128 of 256), the chunk's
+// products as in the search pass (chunk_sums_256) -- the same rows and sums
+// as the reuse branch of a fused pass.
 template <bool DEVPOSE>
-__global__ __launch_bounds__(SLIO_CHUNK) void k_reuse_pass(const ScanDev scan,
-                                                           const PoseDev pose_arg,
-                                                           const PassCfg cfg, const PassOut out) {
+__global__ __launch_bounds__(256) void k_reuse_pass(const ScanDev scan,
+                                                    const PoseDev pose_arg,
+                                                    const PassCfg cfg, const PassOut out) {
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
     return;
   const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
   if (DEVPOSE) ikf_dx_new(cfg.ctl);
   __shared__ double rows[SLIO_CHUNK][kRow];
-  __shared__ double part[1][SLIO_NPROD];
+  __shared__ double part[2][SLIO_NPROD];
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
   const int t = threadIdx.x;
-  const int64_t i = chunk * SLIO_CHUNK + t;
-  double row[kRow];
+  if (t < SLIO_CHUNK) {
+    double row[kRow];
+    reuse_row(scan, pose, cfg, out, chunk * SLIO_CHUNK + t, row);
 #pragma unroll
-  for (int j = 0; j < kRow; ++j) row[j] = 0.0;
-  if (i < scan.n) {
-    bool sel = out.sel[i] != 0;
-    float pd2 = __int_as_float(0x7fc00000);
-    if (sel) {
-      const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
-      float qx, qy, qz;
-      body_to_world(pose, bx, by, bz, qx, qy, qz);
-      const float4 pl = out.plane[i];
-      const float abcd[4] = {pl.x, pl.y, pl.z, pl.w};
-      sel = residual_gate(abcd, qx, qy, qz, bx, by, bz, pd2);
-      if (sel) {
-        double h[12];
-        jacobian_row(pose, bx, by, bz, abcd[0], abcd[1], abcd[2], cfg.extrinsic != 0, h);
-#pragma unroll
-        for (int j = 0; j < 12; ++j) row[j] = h[j];
-        row[12] = -(double)pd2;
-        row[13] = 1.0;
-      }
-      out.sel[i] = sel ? 1 : 0;
-    }
-    out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
+    for (int j = 0; j < kRow; ++j) rows[t][j] = row[j];
   }
-#pragma unroll
-  for (int j = 0; j < kRow; ++j) rows[t][j] = row[j];
   __syncthreads();
-  chunk_products<SLIO_CHUNK>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
+  chunk_sums_256(rows, part, out.chunk_part + chunk * SLIO_NPROD, cfg.mfma, false);
 }
 
 // chunk_order: the order in which the next search pass's workgroups take
@@ -3040,6 +3082,8 @@ struct Ctx {
   double* d_super_own = nullptr;
   double* d_seg = nullptr;    // the pass's 64 segment rows (k_super_sums hand-off)
   void* comm = nullptr;        // RCCL communicator of the rank group (slio_comm_init / slio_create_group)
+  int group_reduce = 0;        // slio_create_group: 1 RCCL communicator, 2 in-device reduce (k_group_reduce)
+  hipEvent_t grp_ev = nullptr; // in-device reduce: end of this rank's pass / of the reduce (rank 0)
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
   MapDev::Buf inc[7];         // map_incremental temporaries, kept across scans
                               // (zero between launches)
@@ -3338,7 +3382,9 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
   if (c.prof && (c.pending[0].size() + c.pending[1].size()) > 256) prof_drain(c);
-  const bool run_search = which != 0, run_reuse = which != 1;
+  // (a fused pass is one launch of the search kernel, which also runs the
+  // reuse pass when the update asks for one)
+  const bool run_search = which != 0, run_reuse = which != 1 && !fuse;
   // Profiled launches carry their start/stop events inside the dispatch
   // packet (hipExtLaunchKernelGGL): no separate marker packets, so timing
   // does not open gaps between the dependent kernels.
@@ -3369,13 +3415,24 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   } while (0)
     if (fuse) {
       // fused pass (fusable() checked the configuration): the filter step
-      // runs in this launch, no k_super_sums
-      if (devpose)
-        hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, true, true>, nb, dim3(kSolveThreads), 0,
-                              c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse);
-      else
-        hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, false, true>, nb, dim3(kSolveThreads), 0,
-                              c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse);
+      // (D = 6, or 12 with extrinsic estimation) runs in this launch, no
+      // k_super_sums; a later pass is a search or a reuse pass as the update
+      // decides on the device
+#define SLIO_LAUNCH_FUSED(DEV, D)                                                                           \
+  hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, DEV, true, D>, nb, dim3(kSolveThreads), 0, \
+                        c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse)
+      if (sa && sa->dim == 12) {
+        if (devpose)
+          SLIO_LAUNCH_FUSED(true, 12);
+        else
+          SLIO_LAUNCH_FUSED(false, 12);
+      } else {
+        if (devpose)
+          SLIO_LAUNCH_FUSED(true, 6);
+        else
+          SLIO_LAUNCH_FUSED(false, 6);
+      }
+#undef SLIO_LAUNCH_FUSED
     } else
     switch (c.prm.lanes_per_query * 2 + (sph ? 1 : 0)) {
       case 2: SLIO_LAUNCH2(1, false); break;
@@ -3396,7 +3453,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
     const auto ev = timing(SLIO_KERNEL_REUSE);
     PassCfg rcfg = cfg;
     rcfg.want_search = 0;
-    const dim3 nb((unsigned)nblk), bs(SLIO_CHUNK);
+    const dim3 nb((unsigned)nblk), bs(256);
     if (devpose)
       hipExtLaunchKernelGGL(k_reuse_pass<true>, nb, bs, 0, c.stream, ev.first, ev.second, 0, s, P,
                             rcfg, o);
@@ -3615,6 +3672,7 @@ int slio_destroy(slio_handle h) {
   for (auto& b : h->c.inc)
     if (b.p) (void)hipFree(b.p);
   if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
+  if (h->c.grp_ev) (void)hipEventDestroy(h->c.grp_ev);
   (void)hipFree(h->c.ctl);
   (void)hipHostFree(h->c.h_ctl);
   if (h->c.done_ev) (void)hipEventDestroy(h->c.done_ev);
@@ -4768,10 +4826,11 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     const int nb = grid_blocks(n);
     // Boxes interact only through float rounding: for a power-of-two size
     // <= 1 (0.5, the reference default) p / ds, floor * ds and + ds are all
-    // exact (|key| < 2^20), every box is exactly [k ds, (k + 1) ds), and no
-    // point can lie outside its own box or in two -- nothing to detect
+    // exact while |key| + 1 < 2^24 (checked below on the call's key range),
+    // every box is exactly [k ds, (k + 1) ds), and no point can lie outside
+    // its own box or in two -- nothing to detect
     int ds_exp = 0;
-    const bool exact_boxes = std::frexp(ds, &ds_exp) == 0.5f && ds <= 1.0f;
+    bool exact_boxes = std::frexp(ds, &ds_exp) == 0.5f && ds <= 1.0f;
     // Then only key equality matters (k_ds_groups; k_ds_conflicts and
     // k_ds_sequential, which look keys up by value, do not run): the keys are
     // packed relative to the call's voxel range, so the radix sort covers a
@@ -4792,13 +4851,15 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
         rc = SLIO_EDEVICE;
         break;
       }
+      for (int a = 0; a < 6; ++a)
+        if (std::llabs((long long)got[a]) >= (1ll << 24) - 1) exact_boxes = false;  // (k + 1) ds inexact
       int bits[3];
       for (int a = 0; a < 3; ++a) {
         const int64_t span = (int64_t)got[3 + a] - (int64_t)got[a] + 1;
         bits[a] = 0;
         while (bits[a] < 40 && ((int64_t)1 << bits[a]) < span) ++bits[a];
       }
-      if (bits[0] + bits[1] + bits[2] <= 48) {
+      if (exact_boxes && bits[0] + bits[1] + bits[2] <= 48) {
         sort_bits = std::max(1, bits[0] + bits[1] + bits[2]);
         const DsPack pk{got[0], got[1], got[2], bits[1] + bits[2], bits[2]};
         k_ds_keys_packed<<<nb, 256, 0, st>>>(in, n, ds, pk, k0, v0);
@@ -5497,6 +5558,22 @@ int slio_map_download(slio_handle h, float* x, float* y, float* z, uint32_t* ids
 
 // test support (not in include/slio.h): the index's points in their stored
 // (cell, id) order, x, y, z, bits(id) per point, after the pending rebuild
+// Test hook (not in the header): the last pass's per-chunk partials,
+// num_chunks(n) x 91 doubles (global chunk index; other ranks' chunks are
+// stale), so tests can rebuild the segment / super tree from them.
+int slio_dbg_chunk_partials(slio_handle h, double* out, int64_t cap, int64_t* nchunks) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!nchunks) return SLIO_EINVAL;
+  const int64_t C = num_chunks(c.n);
+  *nchunks = C;
+  if (!c.chunk_part || C == 0) return SLIO_ESTATE;
+  if (cap < C * SLIO_NPROD || !out) return SLIO_ECAPACITY;
+  SLIO_HIP(hipMemcpyAsync(out, c.chunk_part, sizeof(double) * SLIO_NPROD * C, hipMemcpyDeviceToHost, c.stream));
+  SLIO_HIP(hipStreamSynchronize(c.stream));
+  return SLIO_OK;
+}
+
 int slio_dbg_map_raw(slio_handle h, float* xyzw, int64_t cap, int64_t* n) {
   SLIO_CHECK_H(h);
   Ctx& c = h->c;
@@ -6408,10 +6485,12 @@ struct UpdateRun {
   // The control block comes in and goes out through the mapped host block:
   // pass 0 takes its pose by value and its filter step reads the block over
   // the bus (then keeps it in HBM); the step that ends the update writes x,
-  // P and the flags back.  No copy-engine work on the path.  The block is
-  // filled while pass 0's search runs (launched first): the previous
-  // update has published, and its kernels still queued exit at once (done
-  // in the HBM copy), so nothing reads or writes the host block meanwhile.
+  // P and the flags back.  No copy-engine work on the path.  When the block
+  // is written: before pass 0's launch on the fused path (that launch copies
+  // it at its start), after pass 0's launch on the two-launch path (its
+  // filter step, in the next launch, is the first reader).  Either way the
+  // previous update has published, and its kernels still queued exit at
+  // once (done in the HBM copy), so nothing else reads or writes the block.
   void fill_block() {
     IkfCtl& hc = *c.h_ctl;
     hc.x = *x;
@@ -6443,12 +6522,11 @@ struct UpdateRun {
     // pass 0 always searches (converge starts true, esekfom.hpp:282)
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
     if (fusable() && !(p0 && getenv_on("SLIO_NO_FUSE0"))) {
-      // one launch: search + sums + filter step.  The first pass reads the
-      // mapped host block, filled below while the launch runs and then
-      // released by its sequence number
-      // The first pass's filter step reads the mapped host block in the same
-      // launch: fill it first (measured: launching first and handing the
-      // block over by a polled sequence word cost more than it hid)
+      // one launch: search (or reuse) pass + sums + filter step.  The first
+      // pass's launch copies the mapped host block into HBM, so the host
+      // fills the block BEFORE that launch (measured: launching first and
+      // handing the block over by a polled sequence word cost more than it
+      // hid)
       if (p0) {
         // the previous update has published: nothing on the device still
         // reads or writes the block
@@ -6483,11 +6561,12 @@ struct UpdateRun {
     return SLIO_OK;
   }
 
-  // A later pass runs as one fused launch (search + sums + filter step,
-  // fused_tail) in the bench's configuration: single rank, fixed mode (a
-  // search every pass), no extrinsic estimation, 2 lanes per query without
-  // the sphere-first search, and at least 8 chunks per super-chunk (every
-  // segment row has a chunk).  SLIO_NO_FUSE=1 keeps two launches per pass.
+  // Every pass runs as one fused launch (search or reuse pass + sums +
+  // filter step, fused_tail) on a single rank with 2 lanes per query and no
+  // sphere-first search, in either control flow (FIXED, or REFERENCE with
+  // its reuse passes) and with or without extrinsic estimation (D = 12 / 6),
+  // given at least 8 chunks per super-chunk (every segment row has a chunk).
+  // SLIO_NO_FUSE=1 keeps two launches per pass.
   static bool getenv_on(const char* name) {
     const char* e = std::getenv(name);
     return e && e[0] && e[0] != '0';
@@ -6495,7 +6574,7 @@ struct UpdateRun {
   bool fusable() const {
     const bool off = getenv_on("SLIO_NO_FUSE");
     const int lpq = c.prm.lanes_per_query;
-    return !off && !multi && mode == SLIO_MODE_FIXED && dim == 6 && c.prm.nranks == 1 &&
+    return !off && !multi && c.prm.nranks == 1 &&
            (lpq != 1 && lpq != 4 && lpq != 8) && !(c.prm.search_radius > 0.0f) &&
            num_chunks(c.n) >= (int64_t)kNSeg;
   }
@@ -6535,6 +6614,24 @@ struct UpdateRun {
     return SLIO_OK;
   }
 };
+
+// The group's in-device all-reduce (slio_create_group's reduce backend when
+// ranks share a device, or on request across peer-accessible devices): one
+// workgroup on rank 0's stream sums the ranks' 8 x 91 super rows in rank
+// order and writes the total back into every rank's buffer.  Each super row
+// has exactly one non-zero contributor (the rank owning that super-chunk), so
+// the sum is an exact gather: the same bits as RCCL's SUM or one rank alone.
+struct GroupSupers {
+  double* sup[SLIO_NSUPER];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_group_reduce(GroupSupers g) {
+  for (int e = threadIdx.x; e < SLIO_NSUPER * SLIO_NPROD; e += blockDim.x) {
+    double v = g.sup[0][e];
+    for (int r = 1; r < g.n; ++r) v = v + g.sup[r][e];
+    for (int r = 0; r < g.n; ++r) g.sup[r][e] = v;
+  }
+}
 
 // the in-library all-reduce of a handle's super rows (RCCL), on its stream
 static int comm_allreduce(Ctx& c) {
@@ -6627,7 +6724,25 @@ int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio
     set_error("slio_create_group: bad arguments (ndev must divide 8)");
     return SLIO_EINVAL;
   }
+  int caller_dev = 0;
+  SLIO_HIP(hipGetDevice(&caller_dev));
   for (int r = 0; r < ndev; ++r) out[r] = nullptr;
+  // reduce backend: RCCL (ncclCommInitAll) when every rank has its own GPU;
+  // the in-device reduce when ranks share a device (RCCL refuses that), or
+  // when SLIO_GROUP_REDUCE=device asks for it across peer-accessible GPUs
+  bool shared = false;
+  for (int r = 0; r < ndev; ++r)
+    for (int q = 0; q < r; ++q) shared = shared || devices[q] == devices[r];
+  const char* env = std::getenv("SLIO_GROUP_REDUCE");
+  int kind = shared ? 2 : 1;
+  if (env && std::strcmp(env, "device") == 0) kind = 2;
+  if (env && std::strcmp(env, "rccl") == 0) {
+    if (shared) {
+      set_error("slio_create_group: SLIO_GROUP_REDUCE=rccl needs one device per rank");
+      return SLIO_EINVAL;
+    }
+    kind = 1;
+  }
   int rc = SLIO_OK;
   for (int r = 0; r < ndev && !rc; ++r) {
     slio_params q = *p;
@@ -6636,12 +6751,40 @@ int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio
     q.nranks = ndev;
     rc = slio_create(&out[r], &q);
   }
-  std::vector<ncclComm_t> comms((size_t)ndev, nullptr);
-  if (!rc) {
+  if (!rc && kind == 1) {
+    std::vector<ncclComm_t> comms((size_t)ndev, nullptr);
     const ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devices);
     if (r != ncclSuccess) {
       set_error(std::string("slio_create_group: ncclCommInitAll: ") + ncclGetErrorString(r));
       rc = SLIO_EDEVICE;
+    } else {
+      for (int q = 0; q < ndev; ++q) out[q]->c.comm = comms[q];
+    }
+  }
+  if (!rc && kind == 2) {
+    // rank 0's device reads and writes every rank's super rows
+    for (int r = 1; r < ndev && !rc; ++r) {
+      if (devices[r] == devices[0]) continue;
+      int ok = 0;
+      if (hipDeviceCanAccessPeer(&ok, devices[0], devices[r]) != hipSuccess || !ok) {
+        set_error("slio_create_group: in-device reduce needs peer access from rank 0's GPU");
+        rc = SLIO_EDEVICE;
+        break;
+      }
+      (void)hipSetDevice(devices[0]);
+      const hipError_t e = hipDeviceEnablePeerAccess(devices[r], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        set_error(std::string("slio_create_group: hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+        rc = SLIO_EDEVICE;
+      }
+      (void)hipGetLastError();
+    }
+    for (int r = 0; r < ndev && !rc; ++r) {
+      (void)hipSetDevice(devices[r]);
+      if (hipEventCreateWithFlags(&out[r]->c.grp_ev, hipEventDisableTiming) != hipSuccess) {
+        set_error("slio_create_group: hipEventCreate failed");
+        rc = SLIO_EDEVICE;
+      }
     }
   }
   if (rc) {
@@ -6649,24 +6792,25 @@ int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio
       slio_destroy(out[r]);
       out[r] = nullptr;
     }
-    return rc;
+  } else {
+    for (int r = 0; r < ndev; ++r) out[r]->c.group_reduce = kind;
   }
-  for (int r = 0; r < ndev; ++r) out[r]->c.comm = comms[r];
-  return SLIO_OK;
+  (void)hipSetDevice(caller_dev);
+  return rc;
 }
 
-int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], double R, int maximum_iter,
-                          int extrinsic_est, int mode, slio_ikf_stats* stats) {
-  if (!hs || n < 1 || !x || !P || !(R > 0.0) || maximum_iter < 1 ||
-      (mode != SLIO_MODE_REFERENCE && mode != SLIO_MODE_FIXED)) {
-    set_error("slio_group_ikf_update: bad arguments");
-    return SLIO_EINVAL;
-  }
-  for (int r = 0; r < n; ++r)
-    if (!hs[r] || hs[r]->c.prm.nranks != n || hs[r]->c.prm.rank != r || !hs[r]->c.comm) {
-      set_error("slio_group_ikf_update: handles must be ranks 0..n-1 of one group (slio_create_group)");
-      return SLIO_EINVAL;
-    }
+int slio_group_reduce_kind(slio_handle h) {
+  if (!h) return SLIO_EINVAL;
+  return h->c.group_reduce;
+}
+
+namespace slio {
+
+// slio_group_ikf_update's body; the caller restores the device and, after an
+// error, drains every rank's stream
+static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], double R, int maximum_iter,
+                        int extrinsic_est, int mode, slio_ikf_stats* stats) {
+  const int kind = hs[0]->c.group_reduce;
   // every rank starts from the caller's x and P and ends with the same bits
   std::vector<slio_state> xs((size_t)n, *x);
   std::vector<std::vector<double>> Ps((size_t)n, std::vector<double>(P, P + 576));
@@ -6678,12 +6822,17 @@ int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], 
     SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
     if (int rc = runs[r].begin()) return rc;
   }
+  GroupSupers gs{};
+  gs.n = n;
+  for (int r = 0; r < n; ++r) gs.sup[r] = hs[r]->c.d_super;
+  Ctx& c0 = hs[0]->c;
   for (int i = runs[0].first; i < maximum_iter; ++i) {
     for (int r = 0; r < n; ++r) {
       SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
       if (int rc = runs[r].pass(i)) return rc;
+      if (kind == 2 && r > 0) SLIO_HIP(hipEventRecord(hs[r]->c.grp_ev, hs[r]->c.stream));
     }
-    {
+    if (kind == 1) {
       // one RCCL all-reduce of the 8 x 91 super rows per pass, all ranks
       // enqueued by this thread as one group (each on its own stream)
       if (ncclGroupStart() != ncclSuccess) {
@@ -6697,10 +6846,22 @@ int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], 
         rc = SLIO_EDEVICE;
       }
       if (rc) return rc;
-      for (int r = 0; r < n; ++r) {
+    } else {
+      // in-device reduce on rank 0's stream after every rank's pass; every
+      // rank's filter step after the reduce
+      SLIO_HIP(hipSetDevice(c0.prm.device));
+      for (int r = 1; r < n; ++r) SLIO_HIP(hipStreamWaitEvent(c0.stream, hs[r]->c.grp_ev, 0));
+      k_group_reduce<<<1, 256, 0, c0.stream>>>(gs);
+      SLIO_HIP(hipGetLastError());
+      SLIO_HIP(hipEventRecord(c0.grp_ev, c0.stream));
+      for (int r = 1; r < n; ++r) {
         SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
-        if (int rc2 = runs[r].solve(i)) return rc2;
+        SLIO_HIP(hipStreamWaitEvent(hs[r]->c.stream, c0.grp_ev, 0));
       }
+    }
+    for (int r = 0; r < n; ++r) {
+      SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
+      if (int rc2 = runs[r].solve(i)) return rc2;
     }
   }
   slio_ikf_stats st0{};
@@ -6720,6 +6881,36 @@ int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], 
   std::memcpy(P, Ps[0].data(), sizeof(double) * 576);
   if (stats) *stats = st0;
   return SLIO_OK;
+}
+
+}  // namespace slio
+
+int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], double R, int maximum_iter,
+                          int extrinsic_est, int mode, slio_ikf_stats* stats) {
+  if (!hs || n < 1 || !x || !P || !(R > 0.0) || maximum_iter < 1 ||
+      (mode != SLIO_MODE_REFERENCE && mode != SLIO_MODE_FIXED)) {
+    set_error("slio_group_ikf_update: bad arguments");
+    return SLIO_EINVAL;
+  }
+  for (int r = 0; r < n; ++r)
+    if (!hs[r] || hs[r]->c.prm.nranks != n || hs[r]->c.prm.rank != r || !hs[r]->c.group_reduce ||
+        hs[r]->c.group_reduce != hs[0]->c.group_reduce) {
+      set_error("slio_group_ikf_update: handles must be ranks 0..n-1 of one group (slio_create_group)");
+      return SLIO_EINVAL;
+    }
+  int caller_dev = 0;
+  SLIO_HIP(hipGetDevice(&caller_dev));
+  const int rc = group_update(hs, n, x, P, R, maximum_iter, extrinsic_est, mode, stats);
+  if (rc) {
+    // work already queued on the other ranks must not outlive the call (the
+    // next update refills their control blocks)
+    for (int r = 0; r < n; ++r) {
+      (void)hipSetDevice(hs[r]->c.prm.device);
+      (void)hipStreamSynchronize(hs[r]->c.stream);
+    }
+  }
+  (void)hipSetDevice(caller_dev);
+  return rc;
 }
 
 int slio_set_super_buffer(slio_handle h, double* dev_buf) {

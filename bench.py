@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BYTES_PER_SEARCH_PT = 109   # SURVEY.md §8d compulsory bytes, search pass
+BYTES_PER_REUSE_PT = 30     # SURVEY.md §8d compulsory bytes, non-search (reuse) pass
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -354,7 +355,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=4,
+                    help="maximum_iter of each update (C2: 4; the Avia launch file's is 3)")
+    ap.add_argument("--mode", choices=["fixed", "reference"], default="fixed",
+                    help="fixed: exactly --iters passes, kNN every pass (the C2 throughput line); "
+                         "reference: the esekfom.hpp:292-345 control flow (passes i = -1 .. iters-1, "
+                         "a kNN only after converged passes, reuse passes between), what the drop-in "
+                         "runs (mapping_avia.launch:11: --iters 3)")
     ap.add_argument("--map-points", type=int, default=None,
                     help="default: 10M (c2), 50M (c5)")
     ap.add_argument("--scan-points", type=int, default=100_000)
@@ -500,12 +507,13 @@ def main():
     P = np.empty_like(P0)
     P_ptr, xs_ref, st_ref = L.dptr(P), C.byref(xs), C.byref(stats)
     fn = lib.slio_ikf_update if args.host_loop else lib.slio_ikf_update_device
+    mode = L.SLIO_MODE_REFERENCE if args.mode == "reference" else L.SLIO_MODE_FIXED
 
     def step():
         # every step restarts from the same prior (same work per step)
         C.memmove(C.addressof(xs), C.addressof(xs0), C.sizeof(xs))
         P[...] = P0
-        rc = fn(h, xs_ref, P_ptr, 0.001, args.iters, 0, L.SLIO_MODE_FIXED, reduce_cb, None, st_ref)
+        rc = fn(h, xs_ref, P_ptr, 0.001, args.iters, 0, mode, reduce_cb, None, st_ref)
         if rc:
             L.check(rc, "ikf")
         return xs
@@ -542,16 +550,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    iters_total = args.steps * args.iters
+    # passes per update: --iters in fixed mode; in the reference flow what the
+    # control flow ran (the same every step: same inputs)
+    passes, searches = int(stats.passes), int(stats.searches)
+    iters_total = args.steps * passes
     value = iters_total / el
     avg_kernel_s = (ms.value / max(nl.value, 1)) * 1e-3
-    alg_bytes = BYTES_PER_SEARCH_PT * shard_pts
+    # algorithmic bytes per launch: every launch of the fused kernel is one
+    # pass, a search (109 B/pt) or, in the reference flow, a reuse (30 B/pt)
+    alg_bytes = (searches * BYTES_PER_SEARCH_PT + (passes - searches) * BYTES_PER_REUSE_PT) * shard_pts / passes
     achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else None
+    # x and P of the last update (every rank holds the same bits): lets a
+    # multi-rank run be compared with a single-rank one
+    import hashlib
+    digest = hashlib.sha256(C.string_at(C.addressof(xs), C.sizeof(xs)) + P.tobytes()).hexdigest()[:16]
     # HBM bytes per launch from the committed PMC summary (rocprofv3 --pmc
     # cannot run inside this process): only for the same workload, one rank
     # holding the whole scan, and the library built from the same sources
     traffic = None
-    if os.path.exists(args.traffic_json) and world == 1 and shard_pts == args.scan_points:
+    if (os.path.exists(args.traffic_json) and world == 1 and shard_pts == args.scan_points
+            and args.mode == "fixed"):
         try:
             tj = json.load(open(args.traffic_json))
             if (tj.get("scan_points") == args.scan_points and tj.get("map_points") == args.map_points
@@ -561,7 +579,7 @@ def main():
             traffic = None
 
     l2 = None
-    if rank == 0 and avg_kernel_s > 0:
+    if rank == 0 and avg_kernel_s > 0 and args.mode == "fixed":
         dem = l2_demand_bytes(mp, fr.body[b.value:e.value], st0, cell_m)
         l2 = {"demand_bytes_per_launch": dem, "achieved": dem / avg_kernel_s / 1e9,
               "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": dem / avg_kernel_s / 1e9 / L2_PEAK_GBS,
@@ -577,31 +595,38 @@ def main():
         log(f"[cpu] oracle kd-tree built in {time.time() - t0:.1f}s")
         t0 = time.perf_counter()
         for _ in range(args.cpu_scans):
-            O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=1,
-                         reference_gain=1, threads=args.cpu_threads)
+            _, _, cst, *_ = O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=mode,
+                                         reference_gain=1, threads=args.cpu_threads)
         cel = time.perf_counter() - t0
+        cpu_passes = int(cst[0])
         # the same sample on every core this process may use (the reference's
         # MP_PROC_NUM is 3; SURVEY.md 8(d) asks for both)
         all_cores, cores_why = usable_cores()
         t0 = time.perf_counter()
         for _ in range(args.cpu_scans):
-            O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=1,
+            O.ikf_update(T, fr.body, st0, P0, maximum_iter=args.iters, mode=mode,
                          reference_gain=1, threads=all_cores)
         cel_all = time.perf_counter() - t0
         cpu = {
-            "value": args.cpu_scans * args.iters / cel,
+            "value": args.cpu_scans * cpu_passes / cel,
             "unit": "IKF iterations/s",
-            "all_cores": {"value": args.cpu_scans * args.iters / cel_all, "cores": all_cores},
+            "all_cores": {"value": args.cpu_scans * cpu_passes / cel_all, "cores": all_cores},
             "cores": args.cpu_threads,
             "kind": "port",
-            "sample": (f"{args.cpu_scans} scan updates x {args.iters} IKF iterations (kNN every "
-                       f"iteration, 24 x m gain formed as esekfom.hpp:314), "
+            "sample": (f"{args.cpu_scans} scan updates x {cpu_passes} IKF iterations ("
+                       + ("kNN every iteration" if args.mode == "fixed" else
+                          f"reference control flow, maximum_iter {args.iters}, {int(cst[1])} kNN passes")
+                       + ", 24 x m gain formed as esekfom.hpp:314), "
                        f"{args.scan_points}-pt scan vs {args.map_points}-pt map, "
                        f"{args.cpu_threads} OpenMP threads (MP_PROC_NUM), and all_cores = every "
                        f"core this process may use ({cores_why}); host {cpu_model()}, "
                        f"nproc {os.cpu_count()}"),
         }
 
+    flow = (f"{args.iters} IKF iterations per step with the 5-NN search every iteration"
+            if args.mode == "fixed" else
+            f"reference control flow (esekfom.hpp:292-345, maximum_iter {args.iters}): {passes} IKF "
+            f"iterations per step, {searches} with the 5-NN search")
     out = {
         "metric": "IKF iterations/sec, 100k-pt scan vs 10M-pt map",
         "value": value,
@@ -617,12 +642,13 @@ def main():
         "data": "synthetic (seeded urban scene, Avia-like rosette scan)",
         "config": {
             "workload": ("C2: S-FAST_LIO update_iterated_dyn_share_modified, "
-                         f"{args.scan_points}-pt Avia scan vs {args.map_points}-pt map, "
-                         f"{args.iters} IKF iterations per step with the 5-NN search every "
-                         "iteration"),
+                         f"{args.scan_points}-pt Avia scan vs {args.map_points}-pt map, " + flow),
             "map_points": args.map_points,
             "scan_points": args.scan_points,
-            "iterations_per_step": args.iters,
+            "iterations_per_step": passes,
+            "control_flow": args.mode,
+            "maximum_iter": args.iters,
+            "searches_per_step": searches,
             "ikf_loop": "host" if args.host_loop else "device-resident",
             "grid_cell_m": cell_m,
             "parallelism": (f"scan points sharded x{world}, map replicated, one all-reduce of 8x91 fp64 "
@@ -631,7 +657,9 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_search_pass (fused: each launch also sums the pass and runs its filter step)",
+            "kernel": ("k_search_pass (fused: each launch also sums the pass and runs its filter step"
+                       + ("" if args.mode == "fixed" else "; search or reuse pass as the update decides")
+                       + ")"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -645,6 +673,7 @@ def main():
         },
         "roofline_l2": l2,
         "cpu_baseline": cpu,
+        "result_digest": digest,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

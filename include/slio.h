@@ -300,10 +300,15 @@ int slio_ikf_update(slio_handle h, slio_state* x, double P[576], double R,
                     slio_ikf_stats* stats);
 
 /* Same update, device-resident: state, covariance and the control flags of
- * esekfom.hpp:292-345 live in HBM and a one-wavefront kernel performs the
- * 24x24 step after each pass (same operation order as slio_ikf_update), so
- * the passes are enqueued back to back with no host round trip; the host
- * synchronises once at the end.  `reduce` (if any) is called once per pass at
+ * esekfom.hpp:292-345 live in HBM and the filter step runs on the device
+ * after each pass, so the passes are enqueued back to back with no host round
+ * trip; the host synchronises once at the end.  The device filter step is the
+ * information form on the D columns H can have non-zero -- D = 6 without
+ * extrinsic estimation (H's columns 6..11 are zero, esekfom.hpp:218-220), 12
+ * with it -- while slio_ikf_update's host step always works on 12: the same
+ * algebra, different operation order, so the two agree to rounding (not
+ * bitwise).  In the single-rank configuration each pass after the first is
+ * one launch (search or reuse pass, its sums and the filter step).  `reduce` (if any) is called once per pass at
  * enqueue time and must enqueue a stream-ordered SUM all-reduce; with NULL
  * and nranks > 1 the handle's communicator is used (slio_comm_init). */
 int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R,
@@ -320,17 +325,35 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
  * runs on one CPU process). */
 #define SLIO_COMM_ID_BYTES 128
 /* One process, ndev GPUs (the reference's single-process laserMapping node):
- * out[r] = a handle of rank r on devices[r], all sharing one communicator
- * (ncclCommInitAll).  p gives the other parameters (rank / nranks / device
- * are set here); ndev divides 8.  Each handle then takes the map
- * (slio_map_upload: a replica per GPU) and the whole scan (slio_scan_upload),
- * and slio_group_ikf_update runs the update on all of them. */
+ * out[r] = a handle of rank r on devices[r].  p gives the other parameters
+ * (rank / nranks / device are set here); ndev divides 8.  Each handle then
+ * takes the map (slio_map_upload: a replica per GPU, or slio_map_share between
+ * ranks on one device) and the whole scan (slio_scan_upload), and
+ * slio_group_ikf_update runs the update on all of them.  The group's reduce
+ * backend (slio_group_reduce_kind):
+ *   SLIO_GROUP_RCCL   (1) one communicator over all ranks (ncclCommInitAll),
+ *                         when every rank has its own GPU;
+ *   SLIO_GROUP_DEVICE (2) an in-device fixed-order sum of the ranks' super
+ *                         rows by one kernel on rank 0's stream (ordered by
+ *                         HIP events), when ranks share a device (RCCL
+ *                         refuses that), or across peer-accessible GPUs when
+ *                         the environment sets SLIO_GROUP_REDUCE=device.
+ * SLIO_GROUP_REDUCE=rccl forces RCCL (an error when ranks share a device).
+ * Both give the same bits as one rank. */
+#define SLIO_GROUP_RCCL 1
+#define SLIO_GROUP_DEVICE 2
 int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio_params* p);
+/* The reduce backend of a group handle (SLIO_GROUP_*), 0 for a handle made by
+ * slio_create, < 0 for a null handle. */
+int slio_group_reduce_kind(slio_handle h);
 /* slio_ikf_update_device on every rank of a group, enqueued from the calling
- * thread: per pass, each rank's search pass, the ranks' all-reduces as one
- * ncclGroup, each rank's filter step -- no host round trip until the end.
- * x and P (in / out) and stats come back from rank 0; the call fails
- * (SLIO_EDEVICE) if any rank's x or P differs from rank 0's. */
+ * thread: per pass, each rank's search pass, the all-reduce of the ranks'
+ * super rows (RCCL: one ncclGroup; in-device: k_group_reduce), each rank's
+ * filter step -- no host round trip until the end.  x and P (in / out) and
+ * stats come back from rank 0; the call fails (SLIO_EDEVICE) if any rank's x
+ * or P differs from rank 0's.  On any error every rank's stream is drained
+ * before the call returns, and the calling thread's current device is
+ * restored in every case. */
 int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], double R,
                           int maximum_iter, int extrinsic_est, int mode, slio_ikf_stats* stats);
 /* One process per GPU (e.g. torchrun): rank 0 makes an id (ncclGetUniqueId),

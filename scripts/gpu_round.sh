@@ -10,6 +10,15 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
       rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/${tag}_tests.log; grep -E "FAILED|SKIPPED" gpurun_out/${tag}_tests.log | head
       [ $rc -eq 0 ] || exit $rc ;;
+    t:*)
+      # selected test files / node ids, comma-separated: t:tests/test_gpu_comm.py,tests/test_x.py::test_y
+      sel=${step#t:}; sel=${sel//,/ }
+      timeout -k 10 900 python -u -m pytest $sel -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${tag}_tsel.log 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/${tag}_tsel.log; grep -E "FAILED|SKIPPED|Error" gpurun_out/${tag}_tsel.log | head
+      [ $rc -eq 0 ] || exit $rc ;;
+    benchref)
+      timeout -k 10 600 python bench.py --steps 200 --warmup 5 --mode reference --iters 3 > gpurun_out/${tag}_benchref.json 2> gpurun_out/${tag}_benchref.err || { echo "benchref failed"; tail -20 gpurun_out/${tag}_benchref.err; exit 4; }
+      cat gpurun_out/${tag}_benchref.json ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/${tag}_smoke.log; exit 6; }
       tail -1 gpurun_out/${tag}_smoke.log ;;

@@ -6,7 +6,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from agi_lidar_slam_amd import _lib as L, shard, synth  # noqa: E402
+from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
 lib = L.load(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
 lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
@@ -29,7 +29,7 @@ for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
         HTH = np.zeros(78); HTh = np.zeros(12); m = C.c_int64()
         for _ in range(5):
             L.check(lib.slio_iterate(h, C.byref(pose), 1, 0, L.dptr(HTH), L.dptr(HTh), C.byref(m)), "it")
-        nb = shard.num_chunks(nscan)
+        nb = (nscan + 127) // 128
         buf = (C.c_ulonglong * (8 * nb))()
         assert lib.slio_debug_stamps(buf, nb) == 0
         a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)

@@ -10,7 +10,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from agi_lidar_slam_amd import _lib as L, shard, synth  # noqa: E402
+from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
 lib = L.load(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
 lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
@@ -23,7 +23,7 @@ L.check(lib.slio_map_upload(h, L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "m
 bx, by, bz = (np.ascontiguousarray(body[:, k]) for k in range(3))
 L.check(lib.slio_scan_upload(h, L.fptr(bx), L.fptr(by), L.fptr(bz), body.shape[0]), "scan")
 st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9), [0, 0, -9.81]])
-nb = shard.num_chunks(body.shape[0])
+nb = (body.shape[0] + 127) // 128
 for it in (1, 4):
     for rep in range(3):
         xs = L.SlioState()

@@ -8,6 +8,9 @@ import re
 import numpy as np
 import pytest
 
+import sys
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -97,7 +100,8 @@ def test_bad_arguments_fail_loudly(lib):
 
 
 def test_reduce_super_matches_python_tree(lib):
-    from agi_lidar_slam_amd import _lib as L, shard
+    from agi_lidar_slam_amd import _lib as L
+    import tree_model as shard
     rng = np.random.default_rng(0)
     sup = rng.normal(size=(8, 91))
     sup[:, 90] = rng.integers(0, 1000, 8)

@@ -3,7 +3,8 @@ all-reduce of the 8 x 91 super-chunk sums per IKF iteration through the
 library's reduce hook) run end to end with torch.distributed: 2 ranks on the
 box's one GPU over gloo (RCCL refuses two ranks on one device; the hook, the
 shared stream and the device-resident update are the same).  The sharded run
-must select the same effective points as the single-rank run."""
+must end with the single-rank x and P bit for bit (result_digest: SHA-256 of
+the last update's x and P) and select the same effective points."""
 import json
 import os
 import subprocess
@@ -33,3 +34,14 @@ def test_bench_two_ranks_gloo_matches_single():
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["value"] > 0
     assert two["config"]["effective_points"] == one["config"]["effective_points"]
+    assert two["result_digest"] == one["result_digest"]
+
+
+def test_bench_reference_flow_line():
+    """--mode reference --iters 3 (the drop-in's control flow, mapping_avia.launch:11):
+    a bench line whose passes include reuse passes, with a roofline."""
+    ref = _run([sys.executable, "bench.py", *SMALL, "--mode", "reference", "--iters", "3"])
+    cfg = ref["config"]
+    assert cfg["control_flow"] == "reference" and cfg["maximum_iter"] == 3
+    assert 1 <= cfg["searches_per_step"] <= cfg["iterations_per_step"] <= 4
+    assert ref["value"] > 0 and ref["roofline"]["achieved"] > 0

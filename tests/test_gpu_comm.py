@@ -1,17 +1,18 @@
-"""GPU tests of the in-library multi-GPU path (include/slio.h, RCCL).
+"""GPU tests of the in-library multi-GPU path (include/slio.h).
 
 The reference updates on one CPU process (laserMapping.cpp:772-774); the
 drop-in shards the scan over ranks and all-reduces each pass's 8 x 91 fp64
-super rows inside the library:
+super rows inside the library (esekfom.hpp:306-319 summed over the shards):
 
-* slio_create_group / slio_group_ikf_update (one process, ndev GPUs, one
-  ncclCommInitAll communicator, the ranks' all-reduces as one ncclGroup):
-  a group of ONE rank goes through the same path (super rows -> ncclAllReduce
-  on the handle's stream -> k_ikf_solve) and must give x and P bit for bit
+* slio_create_group / slio_group_ikf_update (one process, one handle per
+  rank).  On this one-GPU box the ranks share the device, so the group takes
+  the in-device reduce backend (SLIO_GROUP_DEVICE: k_group_reduce on rank 0's
+  stream between every rank's pass and every rank's filter step, ordered by
+  HIP events) -- the same enqueue -> all-reduce -> k_ikf_solve -> bitwise
+  agreement sequence as with RCCL.  N = 1, 2, 4, 8 ranks at C2 size, both
+  control flows and extrinsic estimation: x, P and the stats bit for bit
   equal to the plain single-rank update, and within the north_star tolerance
-  of the oracle.  A group of two ranks on this one GPU is run where RCCL
-  accepts it (it refuses two ranks on one device on some builds: then the
-  test says so and skips; the 2..8-GPU runs are the driver's).
+  of the oracle.  A group of one rank takes the RCCL backend.
 * slio_comm_unique_id / slio_comm_init (one process per GPU, torchrun):
   one rank, reduce == NULL, bitwise equal to the single-rank update.
 """
@@ -29,7 +30,7 @@ from test_gpu_runtime import C2_CELL, TOL_POS, TOL_ROT, c2, slio_state, state_ar
 pytestmark = pytest.mark.gpu
 
 
-def single_update(L, mp, fr, st, maxit=4, mode=None):
+def single_update(L, mp, fr, st, maxit=4, mode=None, ext=0):
     lib = L.load()
     mode = L.SLIO_MODE_FIXED if mode is None else mode
     h = mk(L, cell=C2_CELL)
@@ -39,14 +40,17 @@ def single_update(L, mp, fr, st, maxit=4, mode=None):
         xs = slio_state(st)
         P = np.eye(24) * 1e-2
         stt = L.SlioIkfStats()
-        L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, maxit, 0, mode,
+        L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, maxit, ext, mode,
                                            L.ALLREDUCE_FN(), None, C.byref(stt)), "single")
         return state_array(xs), P, (stt.passes, stt.searches, stt.valid_passes, stt.last_m)
     finally:
         lib.slio_destroy(h)
 
 
-def group_update(L, mp, fr, st, devices, maxit=4, mode=None):
+def group_update(L, mp, fr, st, devices, maxit=4, mode=None, ext=0, kinds=None, updates=1):
+    """One group of len(devices) ranks: rank 0 takes the map, ranks on the
+    same device share it, every rank takes the whole scan; `updates`
+    back-to-back group updates from the same prior (the last one returned)."""
     lib = L.load()
     mode = L.SLIO_MODE_FIXED if mode is None else mode
     n = len(devices)
@@ -59,15 +63,24 @@ def group_update(L, mp, fr, st, devices, maxit=4, mode=None):
     if rc:
         return rc, lib.slio_last_error().decode(), None
     try:
+        if kinds is not None:
+            kinds.extend(lib.slio_group_reduce_kind(hs[r]) for r in range(n))
+        upload_map(L, hs[0], mp)
+        for r in range(1, n):
+            if devices[r] == devices[0]:
+                L.check(lib.slio_map_share(hs[r], hs[0]), "share")
+            else:
+                upload_map(L, hs[r], mp)
         for r in range(n):
-            upload_map(L, hs[r], mp)
             assert upload_scan(L, hs[r], fr.body) == 0
-        xs = slio_state(st)
-        P = np.eye(24) * 1e-2
-        stt = L.SlioIkfStats()
-        rc = lib.slio_group_ikf_update(hs, n, C.byref(xs), L.dptr(P), 0.001, maxit, 0, mode, C.byref(stt))
-        if rc:
-            return rc, lib.slio_last_error().decode(), None
+        for _ in range(updates):
+            xs = slio_state(st)
+            P = np.eye(24) * 1e-2
+            stt = L.SlioIkfStats()
+            rc = lib.slio_group_ikf_update(hs, n, C.byref(xs), L.dptr(P), 0.001, maxit, ext, mode,
+                                           C.byref(stt))
+            if rc:
+                return rc, lib.slio_last_error().decode(), None
         return 0, "", (state_array(xs), P, (stt.passes, stt.searches, stt.valid_passes, stt.last_m))
     finally:
         for r in range(n):
@@ -91,17 +104,37 @@ def test_group_one_rank_bitwise(L, oracle_mod, c2, mode):
     assert rot_err(xg[3:7], s_ref[3:7]) < TOL_ROT
 
 
-def test_group_two_ranks_one_device(L, c2):
-    mp, fr, _ = c2
+@pytest.mark.parametrize("mode,ext", [(1, 0), (0, 0), (0, 1)])
+def test_group_ranks_one_device_bitwise(L, oracle_mod, c2, mode, ext):
+    """C4's in-library sequence at N = 2, 4, 8 ranks on this one GPU (the
+    in-device reduce backend): bitwise equal to one rank, in the FIXED and the
+    REFERENCE control flow, with and without extrinsic estimation; the group
+    is updated twice (its counters and events are reused)."""
+    mp, fr, T = c2
     st = state_of(fr)
-    x1, P1, s1 = single_update(L, mp, fr, st)
-    rc, msg, out = group_update(L, mp, fr, st, [0, 0])
-    if rc:
-        pytest.skip(f"RCCL refused two ranks on one device here: {msg}")
-    xg, Pg, sg = out
-    np.testing.assert_array_equal(xg, x1)
-    np.testing.assert_array_equal(Pg, P1)
-    assert sg == s1
+    x1, P1, s1 = single_update(L, mp, fr, st, mode=mode, ext=ext)
+    s_ref, *_ = oracle_mod.ikf_update(T, fr.body, st, np.eye(24) * 1e-2, maximum_iter=4, mode=mode,
+                                      reference_gain=0, extrinsic=bool(ext))
+    assert np.abs(x1[0:3] - s_ref[0:3]).max() < TOL_POS
+    assert rot_err(x1[3:7], s_ref[3:7]) < TOL_ROT
+    for n in (2, 4, 8):
+        kinds = []
+        rc, msg, out = group_update(L, mp, fr, st, [0] * n, mode=mode, ext=ext, kinds=kinds, updates=2)
+        assert rc == 0, msg
+        assert kinds == [L.SLIO_GROUP_DEVICE] * n
+        xg, Pg, sg = out
+        np.testing.assert_array_equal(xg, x1)
+        np.testing.assert_array_equal(Pg, P1)
+        assert sg == s1
+
+
+def test_group_rccl_refused_on_shared_device(L, c2, monkeypatch):
+    """SLIO_GROUP_REDUCE=rccl cannot put two ranks on one device: a clear
+    error, no handles left behind."""
+    mp, fr, _ = c2
+    monkeypatch.setenv("SLIO_GROUP_REDUCE", "rccl")
+    rc, msg, _ = group_update(L, mp, fr, state_of(fr), [0, 0])
+    assert rc == -1 and "one device per rank" in msg
 
 
 def test_comm_init_one_rank_bitwise(L, c2):

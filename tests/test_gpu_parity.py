@@ -342,7 +342,9 @@ def test_edge_cases(L, far):
 
 
 def test_sharded_handles_bitwise_equal(L, c1):
-    """nranks = 1, 2, 4, 8 handles (all on this GPU) give identical sums."""
+    """nranks = 1, 2, 4, 8 handles (all on this GPU) give identical sums, and
+    tests/tree_model.py rebuilds every rank's super rows from its chunk
+    partials bit for bit (the model the gloo tests use)."""
     lib = L.load()
     mp, fr, _ = c1["avia"]
     st = state_of(fr)
@@ -353,6 +355,18 @@ def test_sharded_handles_bitwise_equal(L, c1):
     ref = np.zeros(8 * 91)
     L.check(lib.slio_iterate_async(base, C.byref(pose), 1, 0, None), "it")
     L.check(lib.slio_super_download(base, L.dptr(ref)), "dl")
+    import tree_model as TM
+    lib.slio_dbg_chunk_partials.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+    nch = C.c_int64()
+
+    def partials(h):
+        out = np.zeros((TM.num_chunks(fr.body.shape[0]), 91))
+        L.check(lib.slio_dbg_chunk_partials(h, out.ctypes.data, out.size, C.byref(nch)), "partials")
+        return out
+    # the test model of the tree (tests/tree_model.py, used by the gloo
+    # tests) rebuilds the device's super rows from its chunk partials
+    part_all = partials(base)
+    np.testing.assert_array_equal(TM.super_rows(part_all).reshape(-1), ref)
     try:
         for nr in (2, 4, 8):
             acc = np.zeros(8 * 91)
@@ -365,8 +379,8 @@ def test_sharded_handles_bitwise_equal(L, c1):
                 L.check(lib.slio_super_download(h, L.dptr(part)), "dl")
                 b, e = C.c_int64(), C.c_int64()
                 lib.slio_shard_range(h, C.byref(b), C.byref(e))
-                from agi_lidar_slam_amd import shard
-                assert (b.value, e.value) == shard.shard_range(fr.body.shape[0], r, nr)
+                assert (b.value, e.value) == TM.shard_range(fr.body.shape[0], r, nr)
+                np.testing.assert_array_equal(TM.super_rows(partials(h), r, nr).reshape(-1), part)
                 acc = acc + part   # exact: each slot has one non-zero contributor
                 lib.slio_destroy(h)
             np.testing.assert_array_equal(acc, ref)

@@ -228,13 +228,13 @@ def test_c2_full_size_pinned(L, oracle_mod, c2, mode):
         kd.close()
 
 
-def _update_once(L, h, st, maxit=4, mode=1):
+def _update_once(L, h, st, maxit=4, mode=1, ext=0):
     lib = L.load()
     xs = slio_state(st)
     P = np.eye(24) * 1e-2
     stt = L.SlioIkfStats()
-    L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, maxit, 0, mode, L.ALLREDUCE_FN(), None,
-                                       C.byref(stt)), "ikf")
+    L.check(lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, maxit, ext, mode, L.ALLREDUCE_FN(),
+                                       None, C.byref(stt)), "ikf")
     n = lib.slio_get_neighbors
     b, e = C.c_int64(), C.c_int64()
     lib.slio_shard_range(h, C.byref(b), C.byref(e))
@@ -248,15 +248,20 @@ def _update_once(L, h, st, maxit=4, mode=1):
             ii, sq, se, sup)
 
 
-@pytest.mark.parametrize("npts", [100_000, 8_191, 8_320, 20_013])
-def test_fused_pass_bitwise(L, c2, npts, monkeypatch):
-    """Passes after the first run as ONE launch (search + segment sums + the
-    filter step in the search kernel's tail, fused_tail) in the bench's
-    configuration; the two-launch path (SLIO_NO_FUSE=1: k_search_pass then
-    k_super_sums) sums in the same order and runs the same filter step, so
-    x, P, the flags, the super rows and Nearest_Points are bit-for-bit
-    equal.  Scan sizes: C2, 64 chunks exactly (the smallest fused scan),
-    65 chunks, and uneven super-chunks."""
+@pytest.mark.parametrize("npts,mode,ext,maxit", [
+    (100_000, 1, 0, 4), (8_191, 1, 0, 4), (8_320, 1, 0, 4), (20_013, 1, 0, 4),
+    (100_000, 0, 0, 3), (100_000, 0, 0, 4), (20_013, 0, 0, 4),
+    (100_000, 0, 1, 4), (100_000, 1, 1, 4), (8_320, 0, 1, 3)])
+def test_fused_pass_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
+    """Every pass runs as ONE launch (search or reuse pass + segment sums +
+    the filter step in the kernel's tail, fused_tail) on a single rank; the
+    two-launch path (SLIO_NO_FUSE=1: k_search_pass / k_reuse_pass then
+    k_super_sums) sums in the same order and runs the same filter step, so x,
+    P, the flags, the super rows and Nearest_Points are bit-for-bit equal.
+    Both control flows (FIXED; REFERENCE with its reuse passes, maximum_iter
+    3 as mapping_avia.launch:11 and 4) and extrinsic estimation (D = 12).
+    Scan sizes: C2, 64 chunks exactly (the smallest fused scan), 65 chunks,
+    and uneven super-chunks."""
     mp, fr, _ = c2
     st = state_of(fr)
     body = np.ascontiguousarray(fr.body[:npts])
@@ -266,13 +271,18 @@ def test_fused_pass_bitwise(L, c2, npts, monkeypatch):
         upload_map(L, h, mp)
         assert upload_scan(L, h, body) == 0
         monkeypatch.setenv("SLIO_NO_FUSE", "1")
-        two = _update_once(L, h, st)
+        two = _update_once(L, h, st, maxit=maxit, mode=mode, ext=ext)
         monkeypatch.delenv("SLIO_NO_FUSE")
         for rep in range(3):   # repeated: counters are reset by each pass
-            one = _update_once(L, h, st)
+            one = _update_once(L, h, st, maxit=maxit, mode=mode, ext=ext)
             for a, b in zip(one, two):
                 np.testing.assert_array_equal(a, b)
-        assert two[2][0] == 4 and two[2][2] == 4
+        if mode == 1:
+            assert two[2][0] == maxit and two[2][2] == maxit
+        else:
+            # the perturbed prior does not converge on pass -1: a reuse pass follows
+            print(f"reference flow: passes {two[2][0]} searches {two[2][1]}")
+            assert two[2][1] < two[2][0]
     finally:
         lib.slio_destroy(h)
 
