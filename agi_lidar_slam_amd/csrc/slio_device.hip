@@ -1425,6 +1425,7 @@ struct StepLds {
     double K[288];  // 24 x D: G S^-1 M = K H[:, :D]
   } zk;
   double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums
+  double seg[kSuperSeg][SLIO_NPROD];    // a fused pass's last super-chunk: its segment rows
   double tot[SLIO_NPROD];               // H^T H (78, upper triangle), H^T h (12), m
   double Mt[SLIO_NHTH];                 // H^T H / R (upper triangle)
   double hR[12];                        // H^T h / R
@@ -1878,8 +1879,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
 // accumulators (rows r = 0,1,2,3 mod 4) to break the dependent fp64 add chain;
 // the accumulators and halves are then combined in a fixed order.
 template <int NT>
-__device__ __forceinline__ void chunk_products(const double (*rows)[kRow], double (*part)[SLIO_NPROD],
-                                               double* __restrict__ out, bool sc1 = false) {
+__device__ __forceinline__ double chunk_products_v(const double (*rows)[kRow], double (*part)[SLIO_NPROD]) {
   constexpr int kSplit = NT / 128;                 // row halves handled in parallel
   constexpr int kRowsPer = SLIO_CHUNK / kSplit;
   const int t = threadIdx.x;
@@ -1898,10 +1898,20 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
     part[half][kk] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
+  double s = 0.0;
   if (t < SLIO_NPROD) {
-    double s = part[0][t];
+    s = part[0][t];
 #pragma unroll
     for (int h = 1; h < kSplit; ++h) s = s + part[h][t];
+  }
+  return s;
+}
+template <int NT>
+__device__ __forceinline__ void chunk_products(const double (*rows)[kRow], double (*part)[SLIO_NPROD],
+                                               double* __restrict__ out, bool sc1 = false) {
+  const double s = chunk_products_v<NT>(rows, part);
+  const int t = threadIdx.x;
+  if (t < SLIO_NPROD) {
     if (sc1)
       st_sc1(out + t, s);  // read by another workgroup of this launch
     else
@@ -1922,8 +1932,7 @@ __device__ __forceinline__ void chunk_products(const double (*rows)[kRow], doubl
 // chunk_products (rtol ~1e-16 of the sums).
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 template <int NT>
-__device__ __forceinline__ void chunk_products_mfma(double (*rows)[kRow], double* __restrict__ out,
-                                                    bool sc1 = false) {
+__device__ __forceinline__ double chunk_products_mfma_v(double (*rows)[kRow]) {
   static_assert(NT == 256 && SLIO_CHUNK == 128 && kRow <= 16, "4 waves x 32 rows, 16 columns");
   const int t = threadIdx.x, w = t >> 6, l = t & 63;
   const int col = l & 15, kq = l >> 4;
@@ -1938,11 +1947,21 @@ __device__ __forceinline__ void chunk_products_mfma(double (*rows)[kRow], double
 #pragma unroll
   for (int r = 0; r < 4; ++r) tile[(kq + 4 * r) * 16 + col] = acc[r];
   __syncthreads();
+  double s2 = 0.0;
   if (t < SLIO_NPROD) {
     const int e = (int)c_pa[t] * 16 + (int)c_pb[t];
     const double* r0 = &rows[0][0];
     constexpr int kW = 32 * kRow;  // doubles between the waves' tiles
-    const double s2 = (r0[e] + r0[kW + e]) + (r0[2 * kW + e] + r0[3 * kW + e]);
+    s2 = (r0[e] + r0[kW + e]) + (r0[2 * kW + e] + r0[3 * kW + e]);
+  }
+  return s2;
+}
+template <int NT>
+__device__ __forceinline__ void chunk_products_mfma(double (*rows)[kRow], double* __restrict__ out,
+                                                    bool sc1 = false) {
+  const double s2 = chunk_products_mfma_v<NT>(rows);
+  const int t = threadIdx.x;
+  if (t < SLIO_NPROD) {
     if (sc1)
       st_sc1(out + t, s2);
     else
@@ -2174,14 +2193,10 @@ __device__ __forceinline__ void reuse_row(const ScanDev& scan, const PoseDev& po
 }
 
 // The chunk's 91 products of the rows in LDS (256 threads): on the matrix
-// cores, or the VALU form under SLIO_NO_MFMA.  sc1: the partial is read by
-// another workgroup of the same launch (fused pass).
-__device__ __forceinline__ void chunk_sums_256(double (*rows)[kRow], double (*part)[SLIO_NPROD],
-                                               double* out, bool mfma, bool sc1) {
-  if (mfma)
-    chunk_products_mfma<256>(rows, out, sc1);
-  else
-    chunk_products<256>(rows, part, out, sc1);
+// cores, or the VALU form under SLIO_NO_MFMA; product t in thread t < 91.
+__device__ __forceinline__ double chunk_sums_256(double (*rows)[kRow], double (*part)[SLIO_NPROD],
+                                                 bool mfma) {
+  return mfma ? chunk_products_mfma_v<256>(rows) : chunk_products_v<256>(rows, part);
 }
 
 // dx_new = x [-] x_propagated (esekfom.hpp:236-258) of the iterate a
@@ -2214,27 +2229,69 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
 }
 
 // Fused pass (single rank, device-resident update, the filter step in the
-// pass's own launch): what the search workgroups need to finish the pass's
-// sums and run its filter step.  Segment row b = 8 s + g of super-chunk s
-// sums chunks c0 + g, c0 + g + 8, ... (k_super_sums' order); the workgroup
-// that completes a segment's last chunk sums the row, and the one that
-// completes the 64th row runs final_step.
+// pass's own launch).  The pass's sums follow the fixed tree of k_super_sums
+// (segment row b = 8 s + g of super-chunk s sums chunks c0 + g, c0 + g + 8,
+// ... in order; super row s = segment rows 8 s .. 8 s + 7 in order; the
+// total = super rows 0 .. 7 in order), handed between workgroups as TAGGED
+// values instead of fenced stores and counter chains:
+//   * every value crosses as two 8-byte granules {32 bits of the double, the
+//     pass's epoch}, stored and loaded write-through (sc1); an 8-byte access
+//     is single-copy atomic, so a reader that sees the epoch in both granules
+//     has the value, and one that does not re-polls -- no drain before an
+//     arrival, no second load round trip after a flag;
+//   * a chunk's workgroup stores its tagged partial and arrives, in one round
+//     trip, on its segment row's counter and on the pass's chunk counter; the
+//     last chunk of a row sums the row (its own partial from registers) and
+//     stores it tagged, then arrives on its super-chunk's counter, whose last
+//     arrival sums and stores the super row; the last chunk of the pass runs
+//     the filter step: its own row, the 7 other rows of its super-chunk and
+//     the 7 other super rows in ONE batch of loads with the control block.
+//     Every workgroup it waits for has already arrived (is running), so
+//     every wait ends; a wait is still bounded (kHandoffTicks) and a timeout
+//     ends the update with an error rather than a hang.
+// The counters are banked by the epoch's parity and never reset in the pass
+// that uses them: block 0 of each launch zeroes the NEXT launch's bank (the
+// previous launch, which used it, has completed).  The sums are bit for bit
+// those of k_super_sums (same tree, same order).
+constexpr int kBankWords = 80;  // [0, 64) segment rows, [64, 72) super rows, [72] chunks
+constexpr int kBankSup = 64, kBankChunks = 72;
+constexpr long long kHandoffTicks = 5000000;  // 50 ms at the 100 MHz wall clock
 struct FuseArgs {
   IkfCtl* ctl;        // the update's control block in HBM
   const IkfCtl* pre;  // first pass: the mapped host block, copied into ctl by block 0 at
                       // the launch's start (its PCIe round trip hidden behind the search),
                       // so the filter step reads HBM (src == ctl); else null
-  double* seg_out;    // 64 segment rows
   double* super_out;  // 8 super rows (slio_super_download)
   const IkfCtl* src;  // control block source (ctl: passes after the first)
   IkfCtl* hblk;       // mapped host block
-  uint32_t* cnt;      // [0] row arrivals, [4..6] far queue, [kSegCnt + b] chunk arrivals of row b
+  uint32_t* cnt;      // [4..6] far queue words
+  uint32_t* bank;     // this launch's arrival counters (kBankWords)
+  uint32_t* bank_next;  // the next launch's, zeroed here
+  uint64_t* tpart;    // tagged chunk partials [C][91][2]
+  uint64_t* tseg;     // tagged segment rows [64][91][2]
+  uint64_t* tsup;     // tagged super rows [8][91][2]
+  uint32_t epoch;     // this launch's tag (never 0)
   double R;
   int iter, maxit;
   int64_t C;          // chunks of the scan
 };
 constexpr int kSegCnt = 16;
 constexpr int kCountWords = kSegCnt + kNSeg;
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ void st_tag(uint64_t* p, double v, uint32_t tag) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v), tg = (uint64_t)tag << 32;
+  __hip_atomic_store((gu64*)p, (b & 0xFFFFFFFFull) | tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64*)(p + 1), (b >> 32) | tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_g(const uint64_t* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the value of a granule pair, and whether both carry the tag
+__device__ __forceinline__ double untag(uint64_t g0, uint64_t g1, uint32_t tag, bool& ok) {
+  ok = ok && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag;
+  return __longlong_as_double((long long)((g1 << 32) | (g0 & 0xFFFFFFFFull)));
+}
 
 // the segment row of chunk c (single rank) and its number of chunks
 __device__ __forceinline__ int seg_of_chunk(int64_t C, int64_t c, int64_t& lim) {
@@ -2268,66 +2325,263 @@ __device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, Ik
   if (threadIdx.x == 8) st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->singular), 0u);
 }
 
-// After the chunk partial is stored (sc1): arrival on the chunk's segment row;
-// the last arrival sums the row, and the last row runs the filter step.
-// Every thread of the workgroup calls it.
+// A hand-off wait that ran past kHandoffTicks: the update ends (done, error
+// 2 in `singular`, published) instead of hanging; the host reports it.
+__device__ __forceinline__ void handoff_abort(const FuseArgs& fa) {
+  if (threadIdx.x == 0) {
+    st_sc1_u32(reinterpret_cast<uint32_t*>(&fa.ctl->singular), 2u);
+    st_sc1_u32(reinterpret_cast<uint32_t*>(&fa.ctl->done), 1u);
+    fa.hblk->singular = 2;
+    fa.hblk->done = 1;
+    __threadfence_system();
+    __hip_atomic_store(&fa.hblk->published, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Whether a hand-off wait that started at t0 (0: this is its first miss;
+// thread 0's clock) has run past kHandoffTicks -- the same answer in every
+// thread of the workgroup (a barrier inside).  Every thread calls it.
+__device__ __forceinline__ bool handoff_late(long long& t0) {
+  bool late = false;
+  if (threadIdx.x == 0) {
+    const long long now = wall_clock64();
+    if (t0 == 0) t0 = now;
+    late = now - t0 > kHandoffTicks;
+  }
+  return __syncthreads_or(late) != 0;
+}
+
+// Sum of rows q = 0..7 of a tagged [8][91] block for product t, in order,
+// with row `own` taken from `ownv` (already in registers); false if a row is
+// not yet there (caller re-polls).
+__device__ __forceinline__ bool sum8_tagged(const uint64_t* rows, int own, double ownv, uint32_t tag,
+                                           int t, double& out) {
+  uint64_t g[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint64_t* p = rows + ((size_t)q * SLIO_NPROD + t) * 2;
+    g[2 * q] = q == own ? 0 : ld_g(p);
+    g[2 * q + 1] = q == own ? 0 : ld_g(p + 1);
+  }
+  bool ok = true;
+  double a = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bool okq = true;
+    const double v = q == own ? ownv : untag(g[2 * q], g[2 * q + 1], tag, okq);
+    ok = ok && okq;
+    a = q == 0 ? v : a + v;
+  }
+  out = a;
+  return ok;
+}
+
+// After the chunk's products: the tagged partial, the arrivals and the levels
+// of the tree above it; the pass's last chunk runs the filter step.  `part`
+// is product t of this chunk in thread t < 91.  Every thread calls it.
 template <int NT, int D>
-__device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl,
-                                           const double* chunk_part, int64_t chunk) {
+__device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl, double part,
+                                           int64_t chunk) {
   const int t = threadIdx.x;
+  const uint32_t tag = fa.epoch;
   int64_t lim;
   const int b = seg_of_chunk(fa.C, chunk, lim);
+  const int s = b / kSuperSeg, g = b - s * kSuperSeg;
+  const int64_t c0 = super_lo(fa.C, s);
+  const int jown = (int)((chunk - c0 - g) / kSuperSeg);
 #ifdef SLIO_SOLVE_STAMP
-  // the final workgroup's tail: partial issued, segment arrival, row stored,
-  // row arrival (g_sstamp[16..19]); the launch's first block start is [20]
+  // the final workgroup's tail: partial issued, arrivals back, own row summed,
+  // batch loaded (g_sstamp[16..19]); the launch's first block start is [20]
   unsigned long long ts[4] = {0, 0, 0, 0};
   if (t == 0) ts[0] = wall_clock64();
 #endif
-  drain_stores();
+  if (t < SLIO_NPROD) st_tag(fa.tpart + ((size_t)chunk * SLIO_NPROD + t) * 2, part, tag);
+  // block 0's stores that the filter step reads (the prefetched control
+  // block, dx_new) complete before its arrival
+  if (blockIdx.x == 0) drain_stores();
   __syncthreads();
-  if (t == 0) bcast = (int)arrive(fa.cnt + kSegCnt + b);
+  if (t == 0) {
+    const uint32_t r_row = arrive(fa.bank + b);
+    const uint32_t r_all = arrive(fa.bank + kBankChunks);
+    bcast = (r_row == (uint32_t)lim - 1 ? 1 : 0) | (r_all == (uint32_t)fa.C - 1 ? 2 : 0);
+  }
   __syncthreads();
+  const int role = bcast;
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) ts[1] = wall_clock64();
 #endif
-  if (bcast != (int)lim - 1) return;
-  if (t < SLIO_NPROD) {
-    const int s = b / kSuperSeg, g = b - s * kSuperSeg;
-    const double* p = chunk_part + (super_lo(fa.C, s) + g) * SLIO_NPROD + t;
-    constexpr int kJ = 16;  // C2's 100k-point scan has <= 13 chunks per segment: one round trip
-    double acc = 0.0;
-    for (int64_t j0 = 0; j0 < lim; j0 += kJ) {
-      double v[kJ];
+  if (!(role & 1)) return;  // not the last chunk of its segment row
+  const bool final = (role & 2) != 0;
+  // the segment row: chunks c0 + g + 8 j, j < lim, in order (thread t < 91)
+  double row = 0.0;
+  long long t0 = 0;
+  for (;;) {
+    bool ok = true;
+    if (t < SLIO_NPROD) {
+      const uint64_t* p = fa.tpart + ((size_t)(c0 + g) * SLIO_NPROD + t) * 2;
+      constexpr int kJ = 16;  // C2's 100k-point scan has <= 13 chunks per segment: one round trip
+      double acc = 0.0;
+      for (int64_t j0 = 0; j0 < lim; j0 += kJ) {
+        uint64_t gr[2 * kJ];
 #pragma unroll
-      for (int j = 0; j < kJ; ++j) v[j] = (j0 + j < lim) ? ld_sc1(p + (j0 + j) * (kSuperSeg * SLIO_NPROD)) : 0.0;
+        for (int j = 0; j < kJ; ++j) {
+          const bool ld = j0 + j < lim && j0 + j != jown;
+          const uint64_t* q = p + (size_t)(j0 + j) * (kSuperSeg * SLIO_NPROD * 2);
+          gr[2 * j] = ld ? ld_g(q) : 0;
+          gr[2 * j + 1] = ld ? ld_g(q + 1) : 0;
+        }
 #pragma unroll
-      for (int j = 0; j < kJ; ++j) acc = acc + v[j];
+        for (int j = 0; j < kJ; ++j) {
+          if (j0 + j < lim) {
+            bool okj = true;
+            const double v = j0 + j == jown ? part : untag(gr[2 * j], gr[2 * j + 1], tag, okj);
+            ok = ok && okj;
+            acc = acc + v;
+          }
+        }
+      }
+      row = acc;
     }
-    st_sc1(fa.seg_out + b * SLIO_NPROD + t, acc);
+    if (__syncthreads_and(ok)) break;
+    if (handoff_late(t0)) {
+      handoff_abort(fa);
+      return;
+    }
   }
-  if (t == 0) reset_counter(fa.cnt + kSegCnt + b);
-  drain_stores();
-  __syncthreads();
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) ts[2] = wall_clock64();
 #endif
-  if (t == 0) bcast = (int)arrive(fa.cnt);
-  __syncthreads();
-  if (bcast != kNSeg - 1) return;
+  if (!final) {
+    if (t < SLIO_NPROD) st_tag(fa.tseg + ((size_t)b * SLIO_NPROD + t) * 2, row, tag);
+    __syncthreads();
+    if (t == 0) bcast = arrive(fa.bank + kBankSup + s) == kSuperSeg - 1 ? 1 : 0;
+    __syncthreads();
+    if (!bcast) return;
+    // the super row of s: its 8 segment rows in order (this row from registers)
+    t0 = 0;
+    for (;;) {
+      double sv = 0.0;
+      const bool ok = t < SLIO_NPROD ? sum8_tagged(fa.tseg + (size_t)s * kSuperSeg * SLIO_NPROD * 2, g, row, tag,
+                                                    t, sv)
+                                     : true;
+      if (__syncthreads_and(ok)) {
+        if (t < SLIO_NPROD) st_tag(fa.tsup + ((size_t)s * SLIO_NPROD + t) * 2, sv, tag);
+        return;
+      }
+      if (handoff_late(t0)) {
+        handoff_abort(fa);
+        return;
+      }
+    }
+  }
+  // ---- the pass's last chunk: its super row from the other 7 segment rows,
+  // the total from the other 7 super rows, and the control block, in one
+  // batch (threads >= 91 load the rows' granules into LDS and the control
+  // block; threads < 91 then sum)
+  if (t == 0) {
+    // the pass's number of far queries (slio_far_queries); queue reset (every
+    // workgroup's far-count atomic completed before its arrival)
+    st_sc1_u32(fa.cnt + 6, ld_sc1_u32(fa.cnt + 5));
+    st_sc1_u32(fa.cnt + 4, 0u);
+    st_sc1_u32(fa.cnt + 5, 0u);
+  }
+  const IkfCtl* src = fa.src;
+  const bool first = src != ctl;
+  t0 = 0;
+  for (;;) {
+    bool ok = true;
+    if (t >= SLIO_NPROD) {
+      // 14 rows x 91 values (segment rows q != g of super s, then super rows
+      // q != s) over the 165 threads >= 91, and the control block
+      constexpr int NC = NT - SLIO_NPROD;
+      constexpr int nV = 14 * SLIO_NPROD, kV = (nV + NC - 1) / NC;
+      constexpr int nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
+      const int tt = t - SLIO_NPROD;
+      uint64_t gr[2 * kV];
+      int dst[kV];
+#pragma unroll
+      for (int u = 0; u < kV; ++u) {
+        const int e = tt + u * NC;
+        const uint64_t* p = nullptr;
+        dst[u] = -1;
+        if (e < nV) {
+          const int r = e / SLIO_NPROD, k = e - r * SLIO_NPROD;
+          if (r < 7) {
+            const int q = r < g ? r : r + 1;
+            p = fa.tseg + ((size_t)(s * kSuperSeg + q) * SLIO_NPROD + k) * 2;
+            dst[u] = q * SLIO_NPROD + k;  // L.seg
+          } else {
+            const int q = r - 7 < s ? r - 7 : r - 6;
+            p = fa.tsup + ((size_t)q * SLIO_NPROD + k) * 2;
+            dst[u] = 1024 + q * SLIO_NPROD + k;  // L.sup
+          }
+        }
+        gr[2 * u] = p ? ld_g(p) : 0;
+        gr[2 * u + 1] = p ? ld_g(p + 1) : 0;
+      }
+      double cv[kC];
+#pragma unroll
+      for (int u = 0; u < kC; ++u) {
+        const int e = tt + u * NC;
+        cv[u] = e < nC ? ld_sc1(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : 0.0;
+      }
+      int32_t fl = 0;
+      if (tt < 8) fl = (int32_t)ld_sc1_u32(reinterpret_cast<const uint32_t*>(&src->converge) + tt);
+#pragma unroll
+      for (int u = 0; u < kV; ++u) {
+        if (dst[u] >= 0) {
+          const double v = untag(gr[2 * u], gr[2 * u + 1], tag, ok);
+          if (dst[u] >= 1024)
+            (&L.sup[0][0])[dst[u] - 1024] = v;
+          else
+            (&L.seg[0][0])[dst[u]] = v;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kC; ++u) {
+        const int e = tt + u * NC;
+        if (e < nC) {
+          ctl_dst<D>(L, e) = cv[u];
+          if (first) reinterpret_cast<double*>(ctl)[ctl_src<D>(e)] = cv[u];  // keep it in HBM
+        }
+      }
+      if (tt < 8) L.fl[tt] = fl;
+      if (first && tt == 0) ctl->singular = 0;
+    } else {
+      L.seg[g][t] = row;
+    }
+    if (__syncthreads_and(ok)) break;
+    if (handoff_late(t0)) {
+      handoff_abort(fa);
+      return;
+    }
+  }
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) {
     ts[3] = wall_clock64();
     for (int k = 0; k < 4; ++k) g_sstamp[16 + k] = ts[k];
   }
 #endif
-  if (t == 0) {
-    reset_counter(fa.cnt);
-    // the pass's number of far queries (slio_far_queries); queue reset
-    st_sc1_u32(fa.cnt + 6, ld_sc1_u32(fa.cnt + 5));
-    st_sc1_u32(fa.cnt + 4, 0u);
-    st_sc1_u32(fa.cnt + 5, 0u);
+  if (t < SLIO_NPROD) {
+    double a = L.seg[0][t];
+#pragma unroll
+    for (int q = 1; q < kSuperSeg; ++q) a = a + L.seg[q][t];
+    L.sup[s][t] = a;
+    double tot = L.sup[0][t];
+#pragma unroll
+    for (int q = 1; q < SLIO_NSUPER; ++q) tot = tot + L.sup[q][t];
+    L.tot[t] = tot;
+    if (t < SLIO_NHTH)
+      L.Mt[t] = tot / fa.R;
+    else if (t < SLIO_NHTH + 12)
+      L.hR[t - SLIO_NHTH] = tot / fa.R;
+#pragma unroll
+    for (int q = 0; q < SLIO_NSUPER; ++q) fa.super_out[q * SLIO_NPROD + t] = L.sup[q][t];
   }
-  final_step<NT, D, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+  __syncthreads();
+  SSTAMP(4);
+  if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
+  ikf_step<NT, D>(ctl, fa.hblk, fa.R, fa.iter, fa.maxit, L);
 }
 
 // One h_share_model search pass over one 128-point chunk.
@@ -2348,8 +2602,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
 #ifdef SLIO_SOLVE_STAMP
   if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) g_sstamp[20] = wall_clock64();
 #endif
-  if constexpr (FUSE && !DEVPOSE)
-    if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
+  if constexpr (FUSE) {
+    // the next launch's arrival counters (this launch's were zeroed by the
+    // previous one, which has completed)
+    if (blockIdx.x == 0 && threadIdx.x < kBankWords) st_sc1_u32(fa.bank_next + threadIdx.x, 0u);
+    if constexpr (!DEVPOSE)
+      if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
+  }
   // DEVPOSE: pose and pass selection come from the device-resident update.
   // A fused pass runs whichever pass the update wants (search or reuse,
   // ctl->search_now = converge, esekfom.hpp:138): one launch per pass in the
@@ -2423,8 +2682,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         for (int j = 0; j < kRow; ++j) lds.s.rr.rows[threadIdx.x][j] = row[j];
       }
       __syncthreads();
-      chunk_sums_256(lds.s.rr.rows, lds.s.part, out.chunk_part + chunk * SLIO_NPROD, cfg.mfma, true);
-      fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
+      const double pv = chunk_sums_256(lds.s.rr.rows, lds.s.part, cfg.mfma);
+      fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, pv, chunk);
       return;
     }
   }
@@ -2704,9 +2963,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (nfar > 0) {
     // (3) this chunk's deferred queries, one per wavefront on the coarse
     // level (far_search); no other workgroup is involved or waited for
-    if (tid == 0)
-      __hip_atomic_fetch_add((gu32*)(out.far_ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      // waited for here (its result is consumed): a fused pass's last
+      // workgroup reads the count after every arrival, and arrivals no longer
+      // drain the workgroup's stores
+      const uint32_t old = __hip_atomic_fetch_add((gu32*)(out.far_ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("; far count %0" ::"v"(old));
+    }
     const int lane = tid & 63;
     for (int k = tid >> 6; k < nfar; k += NT / 64) {
       const float4 q = far_q[k];
@@ -2830,12 +3094,19 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   }
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
-  if constexpr (NT == 256)
-    chunk_sums_256(rows, part, out.chunk_part + chunk * SLIO_NPROD, cfg.mfma, FUSE);
-  else
-    chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD, FUSE);
-  if (tid == 0) STAMP(3);
-  if constexpr (FUSE) fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
+  if constexpr (FUSE) {
+    const double pv = chunk_sums_256(rows, part, cfg.mfma);
+    if (tid == 0) STAMP(3);
+    fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, pv, chunk);
+  } else {
+    if constexpr (NT == 256) {
+      const double pv = chunk_sums_256(rows, part, cfg.mfma);
+      if (tid < SLIO_NPROD) out.chunk_part[chunk * SLIO_NPROD + tid] = pv;
+    } else {
+      chunk_products<NT>(rows, part, out.chunk_part + chunk * SLIO_NPROD);
+    }
+    if (tid == 0) STAMP(3);
+  }
 }
 
 // Nearest_Points ids and pointSearchSqDis of the last search pass, derived
@@ -2891,7 +3162,8 @@ __global__ __launch_bounds__(256) void k_reuse_pass(const ScanDev scan,
     for (int j = 0; j < kRow; ++j) rows[t][j] = row[j];
   }
   __syncthreads();
-  chunk_sums_256(rows, part, out.chunk_part + chunk * SLIO_NPROD, cfg.mfma, false);
+  const double pv = chunk_sums_256(rows, part, cfg.mfma);
+  if (t < SLIO_NPROD) out.chunk_part[chunk * SLIO_NPROD + t] = pv;
 }
 
 // chunk_order: the order in which the next search pass's workgroups take
@@ -3084,7 +3356,13 @@ struct Ctx {
   void* comm = nullptr;        // RCCL communicator of the rank group (slio_comm_init / slio_create_group)
   int group_reduce = 0;        // slio_create_group: 1 RCCL communicator, 2 in-device reduce (k_group_reduce)
   hipEvent_t grp_ev = nullptr; // in-device reduce: end of this rank's pass / of the reduce (rank 0)
-  uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail
+  uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail,
+                              // [kCountWords, + 2 kBankWords) the fused passes' two counter banks
+  uint64_t* tpart = nullptr;  // fused passes: tagged chunk partials, segment rows, super rows
+  uint64_t* tseg = nullptr;
+  uint64_t* tsup = nullptr;
+  uint32_t epoch = 0;          // tag of the last fused launch (never 0)
+  uint64_t fused_launches = 0; // bank parity
   MapDev::Buf inc[7];         // map_incremental temporaries, kept across scans
                               // (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
@@ -3239,6 +3517,8 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->sel);
   (void)hipFree(c->resid);
   (void)hipFree(c->chunk_part);
+  (void)hipFree(c->tpart);
+  c->tpart = nullptr;
   (void)hipFree(c->chunk_cost);
   (void)hipFree(c->chunk_perm);
   c->chunk_cost = c->chunk_perm = nullptr;
@@ -3644,8 +3924,12 @@ int slio_create(slio_handle* out, const slio_params* p) {
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.d_seg, sizeof(double) * kNSeg * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
-      hipMalloc(&h->c.count, sizeof(uint32_t) * kCountWords) != hipSuccess ||
-      hipMemset(h->c.count, 0, sizeof(uint32_t) * kCountWords) != hipSuccess ||
+      hipMalloc(&h->c.count, sizeof(uint32_t) * (kCountWords + 2 * kBankWords)) != hipSuccess ||
+      hipMemset(h->c.count, 0, sizeof(uint32_t) * (kCountWords + 2 * kBankWords)) != hipSuccess ||
+      hipMalloc(&h->c.tseg, 16 * kNSeg * SLIO_NPROD) != hipSuccess ||
+      hipMemset(h->c.tseg, 0, 16 * kNSeg * SLIO_NPROD) != hipSuccess ||
+      hipMalloc(&h->c.tsup, 16 * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
+      hipMemset(h->c.tsup, 0, 16 * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       false) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
@@ -3669,6 +3953,8 @@ int slio_destroy(slio_handle h) {
   (void)hipFree(h->c.d_super_own);
   (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
+  (void)hipFree(h->c.tseg);
+  (void)hipFree(h->c.tsup);
   for (auto& b : h->c.inc)
     if (b.p) (void)hipFree(b.p);
   if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
@@ -4081,6 +4367,7 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
+        (e = hipMalloc(&c.tpart, 16 * SLIO_NPROD * capc)) || (e = hipMemset(c.tpart, 0, 16 * SLIO_NPROD * capc)) ||
         (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));
@@ -6536,8 +6823,25 @@ struct UpdateRun {
           return SLIO_EINVAL;
         }
       }
-      const FuseArgs fa{c.ctl, p0 ? (const IkfCtl*)c.d_hctl : nullptr, c.d_seg, c.d_super, c.ctl, c.d_hctl,
-                        c.count, R, i, maxit, num_chunks(c.n)};
+      if (++c.epoch == 0) c.epoch = 1;  // tag 0 is the buffers' initial contents
+      uint32_t* banks = c.count + kCountWords;
+      const uint64_t par = c.fused_launches++ & 1;
+      const FuseArgs fa{c.ctl,
+                        p0 ? (const IkfCtl*)c.d_hctl : nullptr,
+                        c.d_super,
+                        c.ctl,
+                        c.d_hctl,
+                        c.count,
+                        banks + par * kBankWords,
+                        banks + (par ^ 1) * kBankWords,
+                        c.tpart,
+                        c.tseg,
+                        c.tsup,
+                        c.epoch,
+                        R,
+                        i,
+                        maxit,
+                        num_chunks(c.n)};
       int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
       if (rc) return rc;
       SLIO_HIP(hipGetLastError());
@@ -6595,6 +6899,10 @@ struct UpdateRun {
     const IkfCtl& hc = *c.h_ctl;
     if (!hc.done) {
       set_error("slio_ikf_update_device: the update did not complete");
+      return SLIO_EDEVICE;
+    }
+    if (hc.singular == 2) {
+      set_error("slio_ikf_update_device: a fused pass's hand-off between workgroups timed out");
       return SLIO_EDEVICE;
     }
     if (hc.singular) {

@@ -244,6 +244,133 @@ def bench_c3(args, rank, world, dev, dist):
         f.close()
 
 
+def bench_lego(args, rank, world, dev, dist):
+    """LeGO-LOAM front-end: ImageProjection
+    (projectPointCloud, groundRemoval, cloudSegmentation) + the front half of
+    FeatureAssociation (adjustDistortion with the IMU ring, calculateSmoothness,
+    markOccludedPoints, extractFeatures) on one VLP-16 sweep (16 x 1800, the
+    sensor LeGO-LOAM hard-codes, utility.h:53-58), IMU on.  One step = one
+    sweep through the whole device pipeline with the sweep resident in HBM.
+    N > 1: replicas (no collective)."""
+    import ctypes as C
+    from agi_lidar_slam_amd import _lib as L, build, synth
+    from agi_lidar_slam_amd.lego import LegoFrontEnd, LegoImu, LegoParams
+
+    if rank == 0:
+        build.build()
+    if world > 1:
+        dist.barrier()
+    L.load()
+    P = LegoParams()
+    sw = synth.make_vlp16_sweep(seed=20261015 + rank)
+    imu = LegoImu()
+    imu.feed(sw["imu"], sw["time_scan_cur"] + 0.15)
+    fe = LegoFrontEnd(P, device=dev, max_points=sw["x"].size)
+    fe.set_imu(imu, sw["time_scan_cur"])
+    fe.upload(sw["x"], sw["y"], sw["z"])
+    lib, h = fe.lib, fe.h
+    for _ in range(args.warmup):
+        fe.run()
+    counts = L.SlioLegoCounts()
+    lib.slio_lego_profile(h, 0)
+    if world > 1:
+        dist.barrier()
+    L.check(lib.slio_lego_get_counts(h, C.byref(counts)), "counts")
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        rc = lib.slio_lego_run_async(h)
+        if rc:
+            L.check(rc, "slio_lego_run_async")
+    L.check(lib.slio_lego_get_counts(h, C.byref(counts)), "counts")  # waits for the stream
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    # the feature stage's kernel time (HIP events), further sweeps after the timed region
+    if not args.no_kernel_timing:
+        lib.slio_lego_profile(h, 1)
+        for k in range(max(1, args.timing_steps)):
+            L.check(lib.slio_lego_run_async(h), "slio_lego_run_async")
+        lib.slio_lego_profile(h, 1 | L.SLIO_LIO_PROFILE_KEEP)
+    L.check(lib.slio_lego_get_counts(h, C.byref(counts)), "counts")
+    ms, nl = C.c_double(), C.c_int64()
+    lib.slio_lego_profile_read(h, C.byref(ms), C.byref(nl))
+    if world > 1:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    value = args.steps * world / el
+    avg_s = (ms.value / max(nl.value, 1)) * 1e-3
+    nseg = counts.n_segmented
+    nfeat = counts.n_sharp + counts.n_less_sharp + counts.n_flat + counts.n_less_flat
+    # feature stage compulsory bytes (as C3): per segmented point curvature 4 + column 4 + flag 1 +
+    # label 4 + the point 16, and the four feature clouds 16 B per point
+    alg_bytes = 29 * nseg + 16 * nfeat
+    achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        n = max(1, args.cpu_scans_lego)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            si = O.lego_project(sw["x"], sw["y"], sw["z"], P)
+            O.lego_features(si, P, imu, sw["time_scan_cur"])
+        cel = time.perf_counter() - t0
+        cpu = {
+            "value": n / cel,
+            "unit": "scans/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": (f"{n} sweeps through the single-threaded C++ restatement of LeGO-LOAM "
+                       f"projectPointCloud + groundRemoval + cloudSegmentation + adjustDistortion + "
+                       f"calculateSmoothness + markOccludedPoints + extractFeatures (IMU on), same "
+                       f"16 x 1800 VLP-16 sweep; host {cpu_model()}, nproc {os.cpu_count()}"),
+        }
+    out = {
+        "metric": "LeGO-LOAM imageProjection + featureAssociation front half scans/sec, VLP-16 16x1800 sweep",
+        "value": value,
+        "unit": "scans/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (points, ranges, angles, curvature)",
+        "data": "synthetic (seeded urban scene, VLP-16 sweep in firing order with a 200 Hz IMU stream)",
+        "config": {
+            "workload": ("LeGO-LOAM ImageProjection::cloudHandler (projection, ground removal, "
+                         "segmentation) + FeatureAssociation adjustDistortion .. extractFeatures, "
+                         "16 x 1800 VLP-16 sweep, IMU on"),
+            "points_in": int(sw["x"].size),
+            "points_segmented": int(nseg),
+            "features": {"sharp": int(counts.n_sharp), "less_sharp": int(counts.n_less_sharp),
+                         "flat": int(counts.n_flat), "less_flat": int(counts.n_less_flat)},
+            "parallelism": (f"replicas x{world}: one sweep stream per GPU, no collective"
+                            if world > 1 else "single GPU"),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "feature stage: k_fe_pick + k_fe_ring (one timed span)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": None,
+            "alg_bytes_per_launch": alg_bytes,
+            "avg_launch_us": avg_s * 1e6,
+            "launches": int(nl.value),
+            "timing": (f"HIP events in the dispatch packet, {args.timing_steps} further sweeps after "
+                       "the timed region"),
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    fe.close()
+
+
 def bench_c5(args, rank, world, dev, dist):
     """C5 (BASELINE config 5): batched replay -- `--replicas`
     DIFFERENT 100k-point scans in flight at once per GPU against one shared
@@ -382,11 +509,12 @@ def main():
     ap.add_argument("--host-loop", action="store_true",
                     help="run the 24x24 step on the host after every pass (slio_ikf_update)")
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
-    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c5", "lego"], default="c2",
                     help="c2: IKF iterations/s, 100k Avia scan vs 10M map (BASELINE.json metric); "
                          "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan; "
                          "c5: batched replay, --replicas concurrent distinct 100k scans per GPU vs a "
-                         "shared 50M map (BASELINE config 5: 32 scans on 8 GPUs = 4 per GPU)")
+                         "shared 50M map (BASELINE config 5: 32 scans on 8 GPUs = 4 per GPU); "
+                         "lego: LeGO-LOAM front-end scans/s on a VLP-16 16 x 1800 sweep, IMU on")
     ap.add_argument("--replicas", type=int, default=4, help="c5: concurrent scans per GPU")
     ap.add_argument("--cpu-scans-c5", type=int, default=4)
     ap.add_argument("--reduce-hook", action="store_true",
@@ -394,6 +522,7 @@ def main():
                          "instead of the library's own RCCL communicator (slio_comm_init); implied by "
                          "--dist-backend gloo (RCCL refuses two ranks on one device)")
     ap.add_argument("--cpu-scans-c3", type=int, default=300)
+    ap.add_argument("--cpu-scans-lego", type=int, default=300)
     ap.add_argument("--c3-streams", type=int, default=1,
                     help="c3: independent scans in flight per GPU, each on its own handle and stream "
                          "(1: one scan stream, the latency-bound rate)")
@@ -418,8 +547,8 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev)
         dist.init_process_group(args.dist_backend if args.workload == "c2" else "gloo")
-    if args.workload in ("c3", "c5"):
-        (bench_c3 if args.workload == "c3" else bench_c5)(args, rank, world, dev, dist)
+    if args.workload in ("c3", "c5", "lego"):
+        {"c3": bench_c3, "c5": bench_c5, "lego": bench_lego}[args.workload](args, rank, world, dev, dist)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -79,6 +79,77 @@ def mapping(n_map, n_scan, frames_n=6):
                       "search_ms_launches_farq_each": search}), flush=True)
 
 
+def chain(n_map, n_raw, frames_n=8):
+    """Live laserMapping with a realistic prior: the C2-size map, raw scans
+    rendered along a street with per-point time (100 ms sweep), 200 Hz IMU;
+    per scan ImuProcess forward propagation (P carried, no reset) +
+    undistortion + downSizeFilterSurf on the device, lasermap_fov_segment,
+    the reference-flow update (maximum_iter 4), map_incremental; the index
+    rebuild runs inside the next scan's first search (timed inside the
+    update).  Host wall clock per stage (each stage synchronises), HIP events
+    on the search launches, medians over scans 2.."""
+    from agi_lidar_slam_amd import _lib as L, synth
+    from agi_lidar_slam_amd.esekf import StateIkfom
+    from agi_lidar_slam_amd.imu import ImuProcess, MeasureGroup
+    from agi_lidar_slam_amd.mapping import LaserMapping
+    import test_gpu_chain as TC
+    seed = 20261015
+    mp, _ = synth.make_problem(n_map, n_raw, cache_dir="/tmp/slio_cache")
+    seq = TC.make_sequence(seed, n_map, frames_n, n_raw, 0.5)
+    lib = L.load()
+    lm = LaserMapping(filter_size_map_min=0.5, cube_len=1000.0, maximum_iter=4, max_points=n_raw)
+    lm.ikdtree.set_downsample_param(0.5)
+    lm.ikdtree.Build(mp)
+    lm.built = True
+    ip = ImuProcess(mean_acc=np.array([0.0, 0.0, 1.0]), cov_gyr=TC.COV12[0:3], cov_acc=TC.COV12[3:6],
+                    cov_bias_gyr=TC.COV12[6:9], cov_bias_acc=TC.COV12[9:12])
+    fr0 = seq[0]["frame"]
+    lm.kf.change_x(StateIkfom(pos=fr0.gt_pos.copy(), rot=fr0.gt_rot.copy(), offset_T_L_I=synth.AVIA_T_LI.copy(),
+                              vel=seq[1]["v"].copy(), grav=np.array([0.0, 0.0, -9.81])))
+    lm.kf.change_P(np.eye(24) * 1e-3)
+    ip.last_imu_ = np.array([seq[0]["end"], 0.0, 0.0, 1.0, 0.0, 0.0, 0.0])
+    ip.last_lidar_end_time_ = seq[0]["end"]
+    rows = []
+    for k, s in enumerate(seq[1:], start=1):
+        t0 = time.perf_counter()
+        meas = MeasureGroup(lidar_beg_time=s["beg"], lidar_end_time=s["end"], points=s["raw"],
+                            t_ms=s["t_ms"], imu=s["imu"])
+        nd = ip.undistort_downsample(meas, lm.kf, 0.5)
+        t1 = time.perf_counter()
+        xp = lm.kf.get_x().to_array()
+        pos_lid = xp[0:3] + synth.quat_matrix(xp[3:7]) @ xp[11:14]
+        lm.lasermap_fov_segment(pos_lid)
+        t2 = time.perf_counter()
+        lib.slio_profile(lm.kf.h, 1 << (L.SLIO_KERNEL_SEARCH + 1))
+        # Nearest_Points stay on the device (map_incremental reads them there)
+        lm.kf.update_iterated_dyn_share_modified(0.001, None, lm.ikdtree, None, 4, False)
+        t3 = time.perf_counter()
+        ms, nl = C.c_double(), C.c_int64()
+        lib.slio_profile_read(lm.kf.h, L.SLIO_KERNEL_SEARCH, C.byref(ms), C.byref(nl))
+        lib.slio_profile(lm.kf.h, 0)
+        nfar = C.c_int64()
+        lib.slio_far_queries(lm.kf.h, C.byref(nfar))
+        t4 = time.perf_counter()
+        cnt = lm.kf.map_incremental(lm.ikdtree, 0.5, True)
+        t5 = time.perf_counter()
+        st = lm.kf.last_stats
+        xg = lm.kf.get_x().to_array()
+        rows.append(dict(scan=k, down=int(nd), ms_imu_undistort_voxel=(t1 - t0) * 1e3,
+                         ms_fov=(t2 - t1) * 1e3, ms_update_incl_rebuild=(t3 - t2) * 1e3,
+                         ms_map_incremental=(t5 - t4) * 1e3, passes=int(st.passes), searches=int(st.searches),
+                         launch_ms=[round(ms.value, 3), int(nl.value)], far=int(nfar.value),
+                         err_m=float(np.abs(xg[0:3] - s["frame"].gt_pos).max()),
+                         added=[int(v) for v in cnt]))
+    keys = ["ms_imu_undistort_voxel", "ms_fov", "ms_update_incl_rebuild", "ms_map_incremental"]
+    med = {k_: float(np.median([r[k_] for r in rows[1:]])) for k_ in keys}
+    print(json.dumps({"bench": "live_chain_per_scan", "map_points": n_map, "raw_points": n_raw,
+                      "median": med, "ms_per_scan_mapping": med["ms_fov"] + med["ms_update_incl_rebuild"]
+                      + med["ms_map_incremental"], "ms_per_scan_all": sum(med.values()), "scans": rows}),
+          flush=True)
+    lm.kf.close()
+    lm.ikdtree.close()
+
+
 def preproc(n_raw):
     from agi_lidar_slam_amd.esekf import Esekf, StateIkfom
     from agi_lidar_slam_amd.imu import ImuProcess, MeasureGroup
@@ -127,6 +198,8 @@ if __name__ == "__main__":
     what = sys.argv[1:] or ["mapping", "preproc", "s2m"]
     if "mapping" in what:
         mapping(10_000_000, 100_000)
+    if "chain" in what:
+        chain(10_000_000, int(os.environ.get("CHAIN_RAW", "200000")))
     if "preproc" in what:
         preproc(200_000)
     if "s2m" in what:

@@ -28,6 +28,31 @@ for step in "$@"; do
     benchc3)
       timeout -k 10 600 python bench.py --workload c3 --steps 500 --warmup 10 > gpurun_out/${tag}_benchc3.json 2> gpurun_out/${tag}_benchc3.err || { echo "benchc3 failed"; tail -20 gpurun_out/${tag}_benchc3.err; exit 4; }
       cat gpurun_out/${tag}_benchc3.json ;;
+    benchlego)
+      timeout -k 10 600 python bench.py --workload lego --steps 1000 --warmup 20 > gpurun_out/${tag}_benchlego.json 2> gpurun_out/${tag}_benchlego.err || { echo "benchlego failed"; tail -20 gpurun_out/${tag}_benchlego.err; exit 4; }
+      cat gpurun_out/${tag}_benchlego.json ;;
+    proflego)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_proflego -o run --output-format csv -- python3 bench.py --workload lego --steps 500 --warmup 10 --no-cpu-baseline > gpurun_out/${tag}_proflego.log 2>&1 || { echo "proflego failed"; tail -20 gpurun_out/${tag}_proflego.log; exit 5; }
+      for f in $(find gpurun_out/${tag}_proflego -name "*kernel_stats.csv"); do head -20 $f | cut -c1-150; done ;;
+    profref)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profref -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline --mode reference --iters 3 > gpurun_out/${tag}_profref.log 2>&1 || { echo "profref failed"; tail -20 gpurun_out/${tag}_profref.log; exit 5; }
+      for f in $(find gpurun_out/${tag}_profref -name "*kernel_stats.csv"); do head -8 $f; done ;;
+    ab)
+      # same-box in-process A/B: this tree vs agi_lidar_slam_amd/_abl/libslio_prev.so, alternating
+      for k in 1 2; do
+        timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/main /" || exit 7
+        SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_prev.so timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/prev /" || exit 7
+      done > gpurun_out/${tag}_ab.log 2>&1
+      cat gpurun_out/${tag}_ab.log ;;
+    tail)
+      SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so timeout -k 10 200 python scripts/tail_stamps.py > gpurun_out/${tag}_tail.log 2>&1 || { tail gpurun_out/${tag}_tail.log; exit 8; }
+      grep maxit gpurun_out/${tag}_tail.log ;;
+    chain)
+      timeout -k 10 600 python scripts/bench_aux.py chain > gpurun_out/${tag}_chain.jsonl 2> gpurun_out/${tag}_chain.err || { echo "chain failed"; tail -20 gpurun_out/${tag}_chain.err; exit 9; }
+      cut -c1-1500 gpurun_out/${tag}_chain.jsonl ;;
+    mapping)
+      timeout -k 10 600 python scripts/bench_aux.py mapping > gpurun_out/${tag}_mapping.jsonl 2> gpurun_out/${tag}_mapping.err || { echo "mapping failed"; tail -20 gpurun_out/${tag}_mapping.err; exit 9; }
+      cut -c1-1500 gpurun_out/${tag}_mapping.jsonl ;;
     benchc5)
       timeout -k 10 900 python bench.py --workload c5 --steps 50 --warmup 3 > gpurun_out/${tag}_benchc5.json 2> gpurun_out/${tag}_benchc5.err || { echo "benchc5 failed"; tail -20 gpurun_out/${tag}_benchc5.err; exit 4; }
       cat gpurun_out/${tag}_benchc5.json ;;
