@@ -1410,6 +1410,16 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The caller's mapped host block is read with system-scope loads: the previous update's final
+// workgroup wrote the same lines from the GPU (x, P, the flags), and a plain
+// load on that workgroup's XCD could be served from its L2 copy instead of
+// the host's new contents.
+__device__ __forceinline__ double ld_sys(const double* p) {
+  return __hip_atomic_load((const gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys_u32(const uint32_t* p) {
+  return __hip_atomic_load((const guint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ uint32_t arrive(uint32_t* p) {
   return __hip_atomic_fetch_add((guint*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1425,7 +1435,6 @@ struct StepLds {
     double K[288];  // 24 x D: G S^-1 M = K H[:, :D]
   } zk;
   double sup[SLIO_NSUPER][SLIO_NPROD];  // super-chunk sums
-  double seg[kSuperSeg][SLIO_NPROD];    // a fused pass's last super-chunk: its segment rows
   double tot[SLIO_NPROD];               // H^T H (78, upper triangle), H^T h (12), m
   double Mt[SLIO_NHTH];                 // H^T H / R (upper triangle)
   double hR[12];                        // H^T h / R
@@ -1513,10 +1522,13 @@ __device__ __forceinline__ void step_load(StepLds& L, double* rows_lds, const do
 #pragma unroll
   for (int u = 0; u < kC; ++u) {
     const int e = t + u * NT;
-    cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
+    cv[u] = e < nC ? (first ? ld_sys(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : gc[ctl_src<D>(e)])
+                   : 0.0;
   }
   typedef __attribute__((address_space(1))) int32_t gint;
-  const int32_t fl = t < 8 ? ((const gint*)(const int32_t*)&src->converge)[t] : 0;
+  const int32_t fl = t < 8 ? (first ? (int32_t)ld_sys_u32(reinterpret_cast<const uint32_t*>(&src->converge) + t)
+                                    : ((const gint*)(const int32_t*)&src->converge)[t])
+                           : 0;
 #pragma unroll
   for (int u = 0; u < kR; ++u) {
     const int e = t + u * NT;
@@ -2132,6 +2144,8 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
       const int e = tt + u * NC;
       if (CTL_SC1)
         cv[u] = e < nC ? ld_sc1(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : 0.0;
+      else if (first)
+        cv[u] = e < nC ? ld_sys(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : 0.0;
       else
         cv[u] = e < nC ? gc[ctl_src<D>(e)] : 0.0;
     }
@@ -2139,6 +2153,7 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
     int32_t fl = 0;
     if (tt < 8)
       fl = CTL_SC1 ? (int32_t)ld_sc1_u32(reinterpret_cast<const uint32_t*>(&src->converge) + tt)
+           : first ? (int32_t)ld_sys_u32(reinterpret_cast<const uint32_t*>(&src->converge) + tt)
                    : ((const gint*)(const int32_t*)&src->converge)[tt];
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
@@ -2229,69 +2244,27 @@ __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
 }
 
 // Fused pass (single rank, device-resident update, the filter step in the
-// pass's own launch).  The pass's sums follow the fixed tree of k_super_sums
-// (segment row b = 8 s + g of super-chunk s sums chunks c0 + g, c0 + g + 8,
-// ... in order; super row s = segment rows 8 s .. 8 s + 7 in order; the
-// total = super rows 0 .. 7 in order), handed between workgroups as TAGGED
-// values instead of fenced stores and counter chains:
-//   * every value crosses as two 8-byte granules {32 bits of the double, the
-//     pass's epoch}, stored and loaded write-through (sc1); an 8-byte access
-//     is single-copy atomic, so a reader that sees the epoch in both granules
-//     has the value, and one that does not re-polls -- no drain before an
-//     arrival, no second load round trip after a flag;
-//   * a chunk's workgroup stores its tagged partial and arrives, in one round
-//     trip, on its segment row's counter and on the pass's chunk counter; the
-//     last chunk of a row sums the row (its own partial from registers) and
-//     stores it tagged, then arrives on its super-chunk's counter, whose last
-//     arrival sums and stores the super row; the last chunk of the pass runs
-//     the filter step: its own row, the 7 other rows of its super-chunk and
-//     the 7 other super rows in ONE batch of loads with the control block.
-//     Every workgroup it waits for has already arrived (is running), so
-//     every wait ends; a wait is still bounded (kHandoffTicks) and a timeout
-//     ends the update with an error rather than a hang.
-// The counters are banked by the epoch's parity and never reset in the pass
-// that uses them: block 0 of each launch zeroes the NEXT launch's bank (the
-// previous launch, which used it, has completed).  The sums are bit for bit
-// those of k_super_sums (same tree, same order).
-constexpr int kBankWords = 80;  // [0, 64) segment rows, [64, 72) super rows, [72] chunks
-constexpr int kBankSup = 64, kBankChunks = 72;
-constexpr long long kHandoffTicks = 5000000;  // 50 ms at the 100 MHz wall clock
+// pass's own launch): what the search workgroups need to finish the pass's
+// sums and run its filter step.  Segment row b = 8 s + g of super-chunk s
+// sums chunks c0 + g, c0 + g + 8, ... (k_super_sums' order); the workgroup
+// that completes a segment's last chunk sums the row, and the one that
+// completes the 64th row runs final_step.
 struct FuseArgs {
   IkfCtl* ctl;        // the update's control block in HBM
   const IkfCtl* pre;  // first pass: the mapped host block, copied into ctl by block 0 at
                       // the launch's start (its PCIe round trip hidden behind the search),
                       // so the filter step reads HBM (src == ctl); else null
+  double* seg_out;    // 64 segment rows
   double* super_out;  // 8 super rows (slio_super_download)
   const IkfCtl* src;  // control block source (ctl: passes after the first)
   IkfCtl* hblk;       // mapped host block
-  uint32_t* cnt;      // [4..6] far queue words
-  uint32_t* bank;     // this launch's arrival counters (kBankWords)
-  uint32_t* bank_next;  // the next launch's, zeroed here
-  uint64_t* tpart;    // tagged chunk partials [C][91][2]
-  uint64_t* tseg;     // tagged segment rows [64][91][2]
-  uint64_t* tsup;     // tagged super rows [8][91][2]
-  uint32_t epoch;     // this launch's tag (never 0)
+  uint32_t* cnt;      // [0] row arrivals, [4..6] far queue, [kSegCnt + b] chunk arrivals of row b
   double R;
   int iter, maxit;
   int64_t C;          // chunks of the scan
 };
 constexpr int kSegCnt = 16;
 constexpr int kCountWords = kSegCnt + kNSeg;
-
-typedef __attribute__((address_space(1))) uint64_t gu64;
-__device__ __forceinline__ void st_tag(uint64_t* p, double v, uint32_t tag) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v), tg = (uint64_t)tag << 32;
-  __hip_atomic_store((gu64*)p, (b & 0xFFFFFFFFull) | tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gu64*)(p + 1), (b >> 32) | tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_g(const uint64_t* p) {
-  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// the value of a granule pair, and whether both carry the tag
-__device__ __forceinline__ double untag(uint64_t g0, uint64_t g1, uint32_t tag, bool& ok) {
-  ok = ok && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag;
-  return __longlong_as_double((long long)((g1 << 32) | (g0 & 0xFFFFFFFFull)));
-}
 
 // the segment row of chunk c (single rank) and its number of chunks
 __device__ __forceinline__ int seg_of_chunk(int64_t C, int64_t c, int64_t& lim) {
@@ -2317,271 +2290,77 @@ __device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, Ik
   double* cd = reinterpret_cast<double*>(ctl);
   for (int e = threadIdx.x; e < nC; e += blockDim.x) {
     const int o = ctl_src<D>(e);
-    st_sc1(cd + o, hs[o]);
+    st_sc1(cd + o, ld_sys(hs + o));
   }
   if (threadIdx.x < 8)
     st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->converge) + threadIdx.x,
-               reinterpret_cast<const uint32_t*>(&hsrc->converge)[threadIdx.x]);
+               ld_sys_u32(reinterpret_cast<const uint32_t*>(&hsrc->converge) + threadIdx.x));
   if (threadIdx.x == 8) st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->singular), 0u);
 }
 
-// A hand-off wait that ran past kHandoffTicks: the update ends (done, error
-// 2 in `singular`, published) instead of hanging; the host reports it.
-__device__ __forceinline__ void handoff_abort(const FuseArgs& fa) {
-  if (threadIdx.x == 0) {
-    st_sc1_u32(reinterpret_cast<uint32_t*>(&fa.ctl->singular), 2u);
-    st_sc1_u32(reinterpret_cast<uint32_t*>(&fa.ctl->done), 1u);
-    fa.hblk->singular = 2;
-    fa.hblk->done = 1;
-    __threadfence_system();
-    __hip_atomic_store(&fa.hblk->published, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-// Whether a hand-off wait that started at t0 (0: this is its first miss;
-// thread 0's clock) has run past kHandoffTicks -- the same answer in every
-// thread of the workgroup (a barrier inside).  Every thread calls it.
-__device__ __forceinline__ bool handoff_late(long long& t0) {
-  bool late = false;
-  if (threadIdx.x == 0) {
-    const long long now = wall_clock64();
-    if (t0 == 0) t0 = now;
-    late = now - t0 > kHandoffTicks;
-  }
-  return __syncthreads_or(late) != 0;
-}
-
-// Sum of rows q = 0..7 of a tagged [8][91] block for product t, in order,
-// with row `own` taken from `ownv` (already in registers); false if a row is
-// not yet there (caller re-polls).
-__device__ __forceinline__ bool sum8_tagged(const uint64_t* rows, int own, double ownv, uint32_t tag,
-                                           int t, double& out) {
-  uint64_t g[16];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint64_t* p = rows + ((size_t)q * SLIO_NPROD + t) * 2;
-    g[2 * q] = q == own ? 0 : ld_g(p);
-    g[2 * q + 1] = q == own ? 0 : ld_g(p + 1);
-  }
-  bool ok = true;
-  double a = 0.0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    bool okq = true;
-    const double v = q == own ? ownv : untag(g[2 * q], g[2 * q + 1], tag, okq);
-    ok = ok && okq;
-    a = q == 0 ? v : a + v;
-  }
-  out = a;
-  return ok;
-}
-
-// After the chunk's products: the tagged partial, the arrivals and the levels
-// of the tree above it; the pass's last chunk runs the filter step.  `part`
-// is product t of this chunk in thread t < 91.  Every thread calls it.
+// After the chunk partial is stored (sc1): arrival on the chunk's segment row;
+// the last arrival sums the row, and the last row runs the filter step.
+// Every thread of the workgroup calls it.
 template <int NT, int D>
-__device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl, double part,
-                                           int64_t chunk) {
+__device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl,
+                                           const double* chunk_part, int64_t chunk) {
   const int t = threadIdx.x;
-  const uint32_t tag = fa.epoch;
   int64_t lim;
   const int b = seg_of_chunk(fa.C, chunk, lim);
-  const int s = b / kSuperSeg, g = b - s * kSuperSeg;
-  const int64_t c0 = super_lo(fa.C, s);
-  const int jown = (int)((chunk - c0 - g) / kSuperSeg);
 #ifdef SLIO_SOLVE_STAMP
-  // the final workgroup's tail: partial issued, arrivals back, own row summed,
-  // batch loaded (g_sstamp[16..19]); the launch's first block start is [20]
+  // the final workgroup's tail: partial issued, segment arrival, row stored,
+  // row arrival (g_sstamp[16..19]); the launch's first block start is [20]
   unsigned long long ts[4] = {0, 0, 0, 0};
   if (t == 0) ts[0] = wall_clock64();
 #endif
-  if (t < SLIO_NPROD) st_tag(fa.tpart + ((size_t)chunk * SLIO_NPROD + t) * 2, part, tag);
-  // block 0's stores that the filter step reads (the prefetched control
-  // block, dx_new) complete before its arrival
-  if (blockIdx.x == 0) drain_stores();
+  drain_stores();
   __syncthreads();
-  if (t == 0) {
-    const uint32_t r_row = arrive(fa.bank + b);
-    const uint32_t r_all = arrive(fa.bank + kBankChunks);
-    bcast = (r_row == (uint32_t)lim - 1 ? 1 : 0) | (r_all == (uint32_t)fa.C - 1 ? 2 : 0);
-  }
+  if (t == 0) bcast = (int)arrive(fa.cnt + kSegCnt + b);
   __syncthreads();
-  const int role = bcast;
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) ts[1] = wall_clock64();
 #endif
-  if (!(role & 1)) return;  // not the last chunk of its segment row
-  const bool final = (role & 2) != 0;
-  // the segment row: chunks c0 + g + 8 j, j < lim, in order (thread t < 91)
-  double row = 0.0;
-  long long t0 = 0;
-  for (;;) {
-    bool ok = true;
-    if (t < SLIO_NPROD) {
-      const uint64_t* p = fa.tpart + ((size_t)(c0 + g) * SLIO_NPROD + t) * 2;
-      constexpr int kJ = 16;  // C2's 100k-point scan has <= 13 chunks per segment: one round trip
-      double acc = 0.0;
-      for (int64_t j0 = 0; j0 < lim; j0 += kJ) {
-        uint64_t gr[2 * kJ];
+  if (bcast != (int)lim - 1) return;
+  if (t < SLIO_NPROD) {
+    const int s = b / kSuperSeg, g = b - s * kSuperSeg;
+    const double* p = chunk_part + (super_lo(fa.C, s) + g) * SLIO_NPROD + t;
+    constexpr int kJ = 16;  // C2's 100k-point scan has <= 13 chunks per segment: one round trip
+    double acc = 0.0;
+    for (int64_t j0 = 0; j0 < lim; j0 += kJ) {
+      double v[kJ];
 #pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          const bool ld = j0 + j < lim && j0 + j != jown;
-          const uint64_t* q = p + (size_t)(j0 + j) * (kSuperSeg * SLIO_NPROD * 2);
-          gr[2 * j] = ld ? ld_g(q) : 0;
-          gr[2 * j + 1] = ld ? ld_g(q + 1) : 0;
-        }
+      for (int j = 0; j < kJ; ++j) v[j] = (j0 + j < lim) ? ld_sc1(p + (j0 + j) * (kSuperSeg * SLIO_NPROD)) : 0.0;
 #pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          if (j0 + j < lim) {
-            bool okj = true;
-            const double v = j0 + j == jown ? part : untag(gr[2 * j], gr[2 * j + 1], tag, okj);
-            ok = ok && okj;
-            acc = acc + v;
-          }
-        }
-      }
-      row = acc;
+      for (int j = 0; j < kJ; ++j) acc = acc + v[j];
     }
-    if (__syncthreads_and(ok)) break;
-    if (handoff_late(t0)) {
-      handoff_abort(fa);
-      return;
-    }
+    st_sc1(fa.seg_out + b * SLIO_NPROD + t, acc);
   }
+  if (t == 0) reset_counter(fa.cnt + kSegCnt + b);
+  drain_stores();
+  __syncthreads();
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) ts[2] = wall_clock64();
 #endif
-  if (!final) {
-    if (t < SLIO_NPROD) st_tag(fa.tseg + ((size_t)b * SLIO_NPROD + t) * 2, row, tag);
-    __syncthreads();
-    if (t == 0) bcast = arrive(fa.bank + kBankSup + s) == kSuperSeg - 1 ? 1 : 0;
-    __syncthreads();
-    if (!bcast) return;
-    // the super row of s: its 8 segment rows in order (this row from registers)
-    t0 = 0;
-    for (;;) {
-      double sv = 0.0;
-      const bool ok = t < SLIO_NPROD ? sum8_tagged(fa.tseg + (size_t)s * kSuperSeg * SLIO_NPROD * 2, g, row, tag,
-                                                    t, sv)
-                                     : true;
-      if (__syncthreads_and(ok)) {
-        if (t < SLIO_NPROD) st_tag(fa.tsup + ((size_t)s * SLIO_NPROD + t) * 2, sv, tag);
-        return;
-      }
-      if (handoff_late(t0)) {
-        handoff_abort(fa);
-        return;
-      }
-    }
-  }
-  // ---- the pass's last chunk: its super row from the other 7 segment rows,
-  // the total from the other 7 super rows, and the control block, in one
-  // batch (threads >= 91 load the rows' granules into LDS and the control
-  // block; threads < 91 then sum)
-  if (t == 0) {
-    // the pass's number of far queries (slio_far_queries); queue reset (every
-    // workgroup's far-count atomic completed before its arrival)
-    st_sc1_u32(fa.cnt + 6, ld_sc1_u32(fa.cnt + 5));
-    st_sc1_u32(fa.cnt + 4, 0u);
-    st_sc1_u32(fa.cnt + 5, 0u);
-  }
-  const IkfCtl* src = fa.src;
-  const bool first = src != ctl;
-  t0 = 0;
-  for (;;) {
-    bool ok = true;
-    if (t >= SLIO_NPROD) {
-      // 14 rows x 91 values (segment rows q != g of super s, then super rows
-      // q != s) over the 165 threads >= 91, and the control block
-      constexpr int NC = NT - SLIO_NPROD;
-      constexpr int nV = 14 * SLIO_NPROD, kV = (nV + NC - 1) / NC;
-      constexpr int nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
-      const int tt = t - SLIO_NPROD;
-      uint64_t gr[2 * kV];
-      int dst[kV];
-#pragma unroll
-      for (int u = 0; u < kV; ++u) {
-        const int e = tt + u * NC;
-        const uint64_t* p = nullptr;
-        dst[u] = -1;
-        if (e < nV) {
-          const int r = e / SLIO_NPROD, k = e - r * SLIO_NPROD;
-          if (r < 7) {
-            const int q = r < g ? r : r + 1;
-            p = fa.tseg + ((size_t)(s * kSuperSeg + q) * SLIO_NPROD + k) * 2;
-            dst[u] = q * SLIO_NPROD + k;  // L.seg
-          } else {
-            const int q = r - 7 < s ? r - 7 : r - 6;
-            p = fa.tsup + ((size_t)q * SLIO_NPROD + k) * 2;
-            dst[u] = 1024 + q * SLIO_NPROD + k;  // L.sup
-          }
-        }
-        gr[2 * u] = p ? ld_g(p) : 0;
-        gr[2 * u + 1] = p ? ld_g(p + 1) : 0;
-      }
-      double cv[kC];
-#pragma unroll
-      for (int u = 0; u < kC; ++u) {
-        const int e = tt + u * NC;
-        cv[u] = e < nC ? ld_sc1(reinterpret_cast<const double*>(src) + ctl_src<D>(e)) : 0.0;
-      }
-      int32_t fl = 0;
-      if (tt < 8) fl = (int32_t)ld_sc1_u32(reinterpret_cast<const uint32_t*>(&src->converge) + tt);
-#pragma unroll
-      for (int u = 0; u < kV; ++u) {
-        if (dst[u] >= 0) {
-          const double v = untag(gr[2 * u], gr[2 * u + 1], tag, ok);
-          if (dst[u] >= 1024)
-            (&L.sup[0][0])[dst[u] - 1024] = v;
-          else
-            (&L.seg[0][0])[dst[u]] = v;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kC; ++u) {
-        const int e = tt + u * NC;
-        if (e < nC) {
-          ctl_dst<D>(L, e) = cv[u];
-          if (first) reinterpret_cast<double*>(ctl)[ctl_src<D>(e)] = cv[u];  // keep it in HBM
-        }
-      }
-      if (tt < 8) L.fl[tt] = fl;
-      if (first && tt == 0) ctl->singular = 0;
-    } else {
-      L.seg[g][t] = row;
-    }
-    if (__syncthreads_and(ok)) break;
-    if (handoff_late(t0)) {
-      handoff_abort(fa);
-      return;
-    }
-  }
+  if (t == 0) bcast = (int)arrive(fa.cnt);
+  __syncthreads();
+  if (bcast != kNSeg - 1) return;
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) {
     ts[3] = wall_clock64();
     for (int k = 0; k < 4; ++k) g_sstamp[16 + k] = ts[k];
   }
 #endif
-  if (t < SLIO_NPROD) {
-    double a = L.seg[0][t];
-#pragma unroll
-    for (int q = 1; q < kSuperSeg; ++q) a = a + L.seg[q][t];
-    L.sup[s][t] = a;
-    double tot = L.sup[0][t];
-#pragma unroll
-    for (int q = 1; q < SLIO_NSUPER; ++q) tot = tot + L.sup[q][t];
-    L.tot[t] = tot;
-    if (t < SLIO_NHTH)
-      L.Mt[t] = tot / fa.R;
-    else if (t < SLIO_NHTH + 12)
-      L.hR[t - SLIO_NHTH] = tot / fa.R;
-#pragma unroll
-    for (int q = 0; q < SLIO_NSUPER; ++q) fa.super_out[q * SLIO_NPROD + t] = L.sup[q][t];
+  if (t == 0) {
+    reset_counter(fa.cnt);
+    // the pass's number of far queries (slio_far_queries); queue reset
+    st_sc1_u32(fa.cnt + 6, ld_sc1_u32(fa.cnt + 5));
+    st_sc1_u32(fa.cnt + 4, 0u);
+    st_sc1_u32(fa.cnt + 5, 0u);
   }
-  __syncthreads();
-  SSTAMP(4);
-  if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
-  ikf_step<NT, D>(ctl, fa.hblk, fa.R, fa.iter, fa.maxit, L);
+  final_step<NT, D, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+#ifdef SLIO_SOLVE_STAMP
+  if (t == 0) g_sstamp[25 + ((fa.iter + 1) & 3)] = wall_clock64();  // per pass: the filter step's end
+#endif
 }
 
 // One h_share_model search pass over one 128-point chunk.
@@ -2600,15 +2379,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     const PassOut out, const FuseArgs fa) {
   static_assert(!FUSE || search_block<LPQ>() == kSolveThreads, "fused pass: 256 threads");
 #ifdef SLIO_SOLVE_STAMP
-  if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) g_sstamp[20] = wall_clock64();
-#endif
-  if constexpr (FUSE) {
-    // the next launch's arrival counters (this launch's were zeroed by the
-    // previous one, which has completed)
-    if (blockIdx.x == 0 && threadIdx.x < kBankWords) st_sc1_u32(fa.bank_next + threadIdx.x, 0u);
-    if constexpr (!DEVPOSE)
-      if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
+  if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) {
+    g_sstamp[20] = wall_clock64();
+    g_sstamp[21 + ((fa.iter + 1) & 3)] = g_sstamp[20];  // per pass: block 0's start
   }
+#endif
+  if constexpr (FUSE && !DEVPOSE)
+    if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
   // DEVPOSE: pose and pass selection come from the device-resident update.
   // A fused pass runs whichever pass the update wants (search or reuse,
   // ctl->search_now = converge, esekfom.hpp:138): one launch per pass in the
@@ -2672,28 +2449,29 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   auto& far_pre = lds.s.far_pre;
   auto& far_beg = lds.s.far_beg;
   int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
-  if constexpr (FUSE && DEVPOSE) {
-    if (!cfg.ctl->search_now) {
-      // reuse pass (k_reuse_pass's rows and products), then the fused tail
-      if (threadIdx.x < SLIO_CHUNK) {
-        double row[kRow];
-        reuse_row(scan, pose, cfg, out, chunk * SLIO_CHUNK + threadIdx.x, row);
+  const int tid = threadIdx.x;
+  // a fused pass of the device-resident update runs whichever pass the
+  // update wants: a reuse pass (esekfom.hpp:138-150, converge == false) forms
+  // its rows here and shares the products and the tail below with the search
+  // pass (one copy of the tail in the kernel: a second one, in a branch of
+  // its own, cost ~2.5 % of the search pass's time)
+  bool reuse = false;
+  if constexpr (FUSE && DEVPOSE) reuse = !cfg.ctl->search_now;
+  if (reuse) {
+    if (tid < SLIO_CHUNK) {
+      double row[kRow];
+      reuse_row(scan, pose, cfg, out, chunk * SLIO_CHUNK + tid, row);
 #pragma unroll
-        for (int j = 0; j < kRow; ++j) lds.s.rr.rows[threadIdx.x][j] = row[j];
-      }
-      __syncthreads();
-      const double pv = chunk_sums_256(lds.s.rr.rows, lds.s.part, cfg.mfma);
-      fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, pv, chunk);
-      return;
+      for (int j = 0; j < kRow; ++j) lds.s.rr.rows[tid][j] = row[j];
     }
-  }
+    __syncthreads();
+  } else {
   if (cfg.perm) {
     // (a permutation of [0, nblk) by construction; the range check only
     // keeps a corrupt order from writing outside the chunk arrays)
     const uint32_t pc = cfg.perm[chunk - cfg.c_begin];
     if (pc < (uint32_t)(cfg.c_end - cfg.c_begin)) chunk = cfg.c_begin + pc;
   }
-  const int tid = threadIdx.x;
   const int sub = tid & (LPQ - 1);
   const int grp = tid / LPQ;
   const GridGeom g = map.g;
@@ -2963,14 +2741,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (nfar > 0) {
     // (3) this chunk's deferred queries, one per wavefront on the coarse
     // level (far_search); no other workgroup is involved or waited for
-    if (tid == 0) {
-      // waited for here (its result is consumed): a fused pass's last
-      // workgroup reads the count after every arrival, and arrivals no longer
-      // drain the workgroup's stores
-      const uint32_t old = __hip_atomic_fetch_add((gu32*)(out.far_ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("; far count %0" ::"v"(old));
-    }
+    if (tid == 0)
+      __hip_atomic_fetch_add((gu32*)(out.far_ctr + 1), (uint32_t)nfar, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     const int lane = tid & 63;
     for (int k = tid >> 6; k < nfar; k += NT / 64) {
       const float4 q = far_q[k];
@@ -3092,12 +2865,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       }
     }
   }
+  }  // search pass
   // ---------------- phase 3: fixed-order products
   if (cfg.knn_only) return;
   if constexpr (FUSE) {
     const double pv = chunk_sums_256(rows, part, cfg.mfma);
+    if (tid < SLIO_NPROD) st_sc1(out.chunk_part + chunk * SLIO_NPROD + tid, pv);  // read by another workgroup
     if (tid == 0) STAMP(3);
-    fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, pv, chunk);
+    fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
   } else {
     if constexpr (NT == 256) {
       const double pv = chunk_sums_256(rows, part, cfg.mfma);
@@ -3357,12 +3132,6 @@ struct Ctx {
   int group_reduce = 0;        // slio_create_group: 1 RCCL communicator, 2 in-device reduce (k_group_reduce)
   hipEvent_t grp_ev = nullptr; // in-device reduce: end of this rank's pass / of the reduce (rank 0)
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail,
-                              // [kCountWords, + 2 kBankWords) the fused passes' two counter banks
-  uint64_t* tpart = nullptr;  // fused passes: tagged chunk partials, segment rows, super rows
-  uint64_t* tseg = nullptr;
-  uint64_t* tsup = nullptr;
-  uint32_t epoch = 0;          // tag of the last fused launch (never 0)
-  uint64_t fused_launches = 0; // bank parity
   MapDev::Buf inc[7];         // map_incremental temporaries, kept across scans
                               // (zero between launches)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
@@ -3517,8 +3286,6 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->sel);
   (void)hipFree(c->resid);
   (void)hipFree(c->chunk_part);
-  (void)hipFree(c->tpart);
-  c->tpart = nullptr;
   (void)hipFree(c->chunk_cost);
   (void)hipFree(c->chunk_perm);
   c->chunk_cost = c->chunk_perm = nullptr;
@@ -3924,12 +3691,8 @@ int slio_create(slio_handle* out, const slio_params* p) {
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.d_seg, sizeof(double) * kNSeg * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
-      hipMalloc(&h->c.count, sizeof(uint32_t) * (kCountWords + 2 * kBankWords)) != hipSuccess ||
-      hipMemset(h->c.count, 0, sizeof(uint32_t) * (kCountWords + 2 * kBankWords)) != hipSuccess ||
-      hipMalloc(&h->c.tseg, 16 * kNSeg * SLIO_NPROD) != hipSuccess ||
-      hipMemset(h->c.tseg, 0, 16 * kNSeg * SLIO_NPROD) != hipSuccess ||
-      hipMalloc(&h->c.tsup, 16 * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
-      hipMemset(h->c.tsup, 0, 16 * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
+      hipMalloc(&h->c.count, sizeof(uint32_t) * kCountWords) != hipSuccess ||
+      hipMemset(h->c.count, 0, sizeof(uint32_t) * kCountWords) != hipSuccess ||
       false) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
@@ -3953,8 +3716,6 @@ int slio_destroy(slio_handle h) {
   (void)hipFree(h->c.d_super_own);
   (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
-  (void)hipFree(h->c.tseg);
-  (void)hipFree(h->c.tsup);
   for (auto& b : h->c.inc)
     if (b.p) (void)hipFree(b.p);
   if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
@@ -4367,7 +4128,6 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
-        (e = hipMalloc(&c.tpart, 16 * SLIO_NPROD * capc)) || (e = hipMemset(c.tpart, 0, 16 * SLIO_NPROD * capc)) ||
         (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));
@@ -4684,14 +4444,16 @@ __global__ void k_ds_sequential(const float4* __restrict__ in, const uint64_t* _
 // sequential rules of Add_Points on the box's stored points and the group's
 // points.  Stored points in storage order = ascending id; a stored point
 // wins only when strictly nearer the box centre (ties: the lower id).
-__global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __restrict__ keys,
-                            const uint32_t* __restrict__ order, int64_t n, float ds, MapView map,
-                            uint8_t* __restrict__ keep, uint32_t* __restrict__ surv,
-                            unsigned long long* __restrict__ counter) {
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i0 >= n || (i0 > 0 && keys[i0] == keys[i0 - 1])) return;
-  if (counter[1]) return;  // interacting groups: k_ds_sequential instead
-  const float4 q0 = in[order[i0]];
+// One downsample group (the points of one voxel key) against the stored
+// map, in list order -- the sequential rules of Add_Points (ikd_Tree.cpp:
+// 428-512) for a group no other group interacts with.  member(j) is the
+// list index of the group's j-th point in list order, j < m.
+template <typename Member>
+__device__ __forceinline__ void ds_group(const float4* __restrict__ in, float ds, const MapView& map,
+                                         uint8_t* __restrict__ keep, uint32_t* __restrict__ surv,
+                                         unsigned long long* __restrict__ counter, int64_t m, Member member) {
+  const uint32_t li0 = member(0);
+  const float4 q0 = in[li0];
   float lo[3], hi[3];
   const float c0[3] = {q0.x, q0.y, q0.z};
 #pragma unroll
@@ -4745,8 +4507,8 @@ __global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __res
   int64_t cur_new = -1;       // list index of this call's surviving new point
   bool best_new = false;
   unsigned long long ops = 0;
-  for (int64_t j = i0; j < n && keys[j] == keys[i0]; ++j) {
-    const uint32_t li = order[j];
+  for (int64_t j = 0; j < m; ++j) {
+    const uint32_t li = j == 0 ? li0 : member(j);  // member() is called once per j, in order
     const float4 q = in[li];
     const float dq = map_dist(q.x, q.y, q.z, mx, my, mz);
     const bool stored_wins = cnt > 0 && bd < dq;
@@ -4776,6 +4538,92 @@ __global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __res
       }
   if (cur_new >= 0) surv[cur_new] = 1;
   if (ops) atomicAdd(counter, ops);
+}
+
+// groups from the keys sorted stably (keys, order = list indices): one
+// thread per group head
+__global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __restrict__ keys,
+                            const uint32_t* __restrict__ order, int64_t n, float ds, MapView map,
+                            uint8_t* __restrict__ keep, uint32_t* __restrict__ surv,
+                            unsigned long long* __restrict__ counter) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= n || (i0 > 0 && keys[i0] == keys[i0 - 1])) return;
+  if (counter[1]) return;  // interacting groups: k_ds_sequential instead
+  int64_t m = 1;
+  while (i0 + m < n && keys[i0 + m] == keys[i0]) ++m;
+  ds_group(in, ds, map, keep, surv, counter, m, [&](int64_t j) { return order[i0 + j]; });
+}
+
+// Grouping without a sort (exact boxes: groups are independent and need no
+// global order, only their own points in list order).  Open-addressing hash
+// of the voxel key (ds_key) into H = 2^hb slots: each point claims or finds
+// its key's slot (atomicCAS), takes a member position (atomicAdd) and stores
+// its list index there (up to kDsInline per slot); a slot with more members
+// rescans the list for its key (rare: a 0.5 m voxel of a downsampled scan).
+// A key outside ds_key's 21-bit range sets *flag (counter[2] of the groups
+// kernel): the caller then takes the sorting path.
+constexpr int kDsInline = 16;
+constexpr uint64_t kDsEmpty = ~0ull;
+__global__ void k_ds_hash(const float4* __restrict__ in, int64_t n, float ds, int hb, uint64_t* __restrict__ hkey,
+                          uint32_t* __restrict__ hcnt, uint32_t* __restrict__ hmem,
+                          unsigned long long* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  const int64_t kx = (int64_t)floorf(p.x / ds), ky = (int64_t)floorf(p.y / ds), kz = (int64_t)floorf(p.z / ds);
+  constexpr int64_t kLim = (1 << 20) - 1;
+  if (kx < -kLim || kx > kLim || ky < -kLim || ky > kLim || kz < -kLim || kz > kLim) {
+    atomicExch(flag, 1ull);
+    return;
+  }
+  const uint64_t key = ds_key(kx, ky, kz);
+  const uint64_t mask = ((uint64_t)1 << hb) - 1;
+  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> (64 - hb);
+  for (;;) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&hkey[h], kDsEmpty, key);
+    if (prev == kDsEmpty || prev == key) break;
+    h = (h + 1) & mask;
+  }
+  const uint32_t pos = atomicAdd(&hcnt[h], 1u);
+  if (pos < (uint32_t)kDsInline) hmem[h * kDsInline + pos] = (uint32_t)i;
+}
+
+// one thread per occupied slot: its members sorted into list order, then
+// ds_group
+__global__ void k_ds_groups_hash(const float4* __restrict__ in, int64_t n, float ds, int hb,
+                                 const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ hcnt,
+                                 const uint32_t* __restrict__ hmem, MapView map, uint8_t* __restrict__ keep,
+                                 uint32_t* __restrict__ surv, unsigned long long* __restrict__ counter) {
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= ((int64_t)1 << hb) || counter[2]) return;  // counter[2]: a key out of range
+  const uint64_t key = hkey[h];
+  if (key == kDsEmpty) return;
+  const int64_t m = hcnt[h];
+  if (m <= kDsInline) {
+    uint32_t mem[kDsInline];
+#pragma unroll
+    for (int j = 0; j < kDsInline; ++j) mem[j] = j < m ? hmem[h * kDsInline + j] : 0xFFFFFFFFu;
+    // insertion sort into list order (m is small)
+    for (int j = 1; j < m; ++j) {
+      const uint32_t v = mem[j];
+      int k = j - 1;
+      for (; k >= 0 && mem[k] > v; --k) mem[k + 1] = mem[k];
+      mem[k + 1] = v;
+    }
+    ds_group(in, ds, map, keep, surv, counter, m, [&](int64_t j) { return mem[j]; });
+  } else {
+    // more members than the slot holds: the list in order, filtered by key
+    int64_t next = 0;
+    auto member = [&](int64_t j) {
+      (void)j;  // called with j = 0, 1, ... in order
+      for (;; ++next) {
+        const float4 p = in[next];
+        const uint64_t k = ds_key((int64_t)floorf(p.x / ds), (int64_t)floorf(p.y / ds), (int64_t)floorf(p.z / ds));
+        if (k == key) return (uint32_t)next++;
+      }
+    };
+    ds_group(in, ds, map, keep, surv, counter, m, member);
+  }
 }
 
 // surviving points -> add4[base + rank] with id next_id + rank
@@ -5057,6 +4905,63 @@ static MapView map_view(const MapDev& m) {
 
 // KD_TREE::Add_Points on the device map: n points at `in` (device float4,
 // .w ignored); returns the downsample counter (tmp_counter).
+// Add_Points(downsample) for exact boxes by hash grouping (k_ds_hash,
+// k_ds_groups_hash); *fallback = a voxel key outside ds_key's range was seen
+// and nothing was changed (the caller then sorts).
+static int map_add_hashed(Ctx& c, const float4* in, int64_t n, float ds, int64_t* counter, bool* fallback) {
+  MapDev& m = *c.map;
+  hipStream_t st = c.stream;
+  *fallback = false;
+  int hb = 10;
+  while (((int64_t)1 << hb) < 2 * n) ++hb;
+  const int64_t H = (int64_t)1 << hb;
+  auto& B = m.b_add;
+  hipError_t e;
+  // B[0]: hash keys, B[1]: member counts, B[2]: members, B[4]: survivor flags,
+  // B[5]: their ranks, B[6]: counters (ops, -, out-of-range)
+  if ((e = m.take(B[0], 8 * H)) || (e = m.take(B[1], 4 * H)) || (e = m.take(B[2], 4 * kDsInline * H)) ||
+      (e = m.take(B[4], 4 * n)) || (e = m.take(B[5], 4 * n)) || (e = m.take(B[6], 64))) {
+    set_error(std::string("slio map: hipMalloc: ") + hipGetErrorString(e));
+    return SLIO_ENOMEM;
+  }
+  uint64_t* hkey = (uint64_t*)B[0].p;
+  uint32_t* hcnt = (uint32_t*)B[1].p;
+  uint32_t* hmem = (uint32_t*)B[2].p;
+  uint32_t* surv = (uint32_t*)B[4].p;
+  uint32_t* rank = (uint32_t*)B[5].p;
+  unsigned long long* dcount = (unsigned long long*)B[6].p;
+  if ((e = hipMemsetAsync(hkey, 0xFF, 8 * H, st)) || (e = hipMemsetAsync(hcnt, 0, 4 * H, st)) ||
+      (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 24, st))) {
+    set_error(std::string("slio map: memset: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  k_ds_hash<<<grid_blocks(n), 256, 0, st>>>(in, n, ds, hb, hkey, hcnt, hmem, dcount + 2);
+  k_ds_groups_hash<<<grid_blocks(H), 256, 0, st>>>(in, n, ds, hb, hkey, hcnt, hmem, map_view(m), m.keep, surv,
+                                                   dcount);
+  uint32_t total = 0;
+  if (int rc = scan_flags(surv, rank, n, st, &total)) return rc;  // (reads `total` back: synchronises)
+  unsigned long long ops[3] = {0, 0, 0};
+  if ((e = hipMemcpyAsync(ops, dcount, 24, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+    set_error(std::string("slio map: groups: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  if (ops[2]) {
+    *fallback = true;
+    return SLIO_OK;
+  }
+  *counter = (int64_t)ops[0];
+  if (int rc = add_reserve(m, total, st)) return rc;
+  k_append<<<grid_blocks(n), 256, 0, st>>>(in, surv, rank, n, m.add4, m.akeep, m.nadd, m.next_id);
+  if ((e = hipGetLastError())) {
+    set_error(std::string("slio map: append: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  }
+  m.nadd += total;
+  m.next_id += total;
+  m.dirty = true;  // deletions (keep flags) and / or additions
+  return SLIO_OK;
+}
+
 static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float ds, int64_t* counter) {
   MapDev& m = *c.map;
   hipStream_t st = c.stream;
@@ -5077,6 +4982,19 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
   }
   // the box searches need every stored point in the index
   if (int rc = map_refresh_locked(c, true)) return rc;
+  {
+    // exact boxes (a power-of-two size <= 1, see below): groups by hashing
+    // the voxel keys -- no key-range readback, no sort (SLIO_NO_DS_HASH=1:
+    // the sorting path)
+    int ds_exp0 = 0;
+    const char* nh = std::getenv("SLIO_NO_DS_HASH");
+    const bool no_hash = nh && nh[0] && nh[0] != '0';
+    if (!no_hash && std::frexp(ds, &ds_exp0) == 0.5f && ds <= 1.0f) {
+      bool fallback = false;
+      if (int rc = map_add_hashed(c, in, n, ds, counter, &fallback)) return rc;
+      if (!fallback) return SLIO_OK;
+    }
+  }
   uint64_t *k0 = nullptr, *k1 = nullptr;
   uint32_t *v0 = nullptr, *v1 = nullptr, *surv = nullptr, *rank = nullptr;
   unsigned long long* dcount = nullptr;
@@ -6823,25 +6741,8 @@ struct UpdateRun {
           return SLIO_EINVAL;
         }
       }
-      if (++c.epoch == 0) c.epoch = 1;  // tag 0 is the buffers' initial contents
-      uint32_t* banks = c.count + kCountWords;
-      const uint64_t par = c.fused_launches++ & 1;
-      const FuseArgs fa{c.ctl,
-                        p0 ? (const IkfCtl*)c.d_hctl : nullptr,
-                        c.d_super,
-                        c.ctl,
-                        c.d_hctl,
-                        c.count,
-                        banks + par * kBankWords,
-                        banks + (par ^ 1) * kBankWords,
-                        c.tpart,
-                        c.tseg,
-                        c.tsup,
-                        c.epoch,
-                        R,
-                        i,
-                        maxit,
-                        num_chunks(c.n)};
+      const FuseArgs fa{c.ctl, p0 ? (const IkfCtl*)c.d_hctl : nullptr, c.d_seg, c.d_super, c.ctl, c.d_hctl,
+                        c.count, R, i, maxit, num_chunks(c.n)};
       int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
       if (rc) return rc;
       SLIO_HIP(hipGetLastError());
@@ -6898,7 +6799,9 @@ struct UpdateRun {
     SLIO_HIP(wait_published(c));
     const IkfCtl& hc = *c.h_ctl;
     if (!hc.done) {
-      set_error("slio_ikf_update_device: the update did not complete");
+      set_error("slio_ikf_update_device: the update did not complete (passes " + std::to_string(hc.passes) +
+                ", searches " + std::to_string(hc.searches) + ", converge " + std::to_string(hc.converge) +
+                ", published " + std::to_string(hc.published) + ")");
       return SLIO_EDEVICE;
     }
     if (hc.singular == 2) {

@@ -34,7 +34,6 @@
 // entries the reference never initialises are never picked.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
-#include <hipcub/block/block_radix_sort.hpp>
 
 #include <algorithm>
 #include <cfloat>
@@ -207,119 +206,68 @@ __device__ int block_exclusive_scan(int v, int* scratch /* NT/64 + 1 */, int& ex
   return total;
 }
 
-// in-LDS bitonic sort of P (power of two) 64-bit keys, ascending
-template <int NT>
-__device__ void bitonic_sort(uint64_t* key, int P) {
-  for (int k = 2; k <= P; k <<= 1) {
+// Bitonic sort of N = 64 * E * NW 64-bit keys in LDS (ascending), by the
+// first NW wavefronts of the block; every thread of the block calls it (the
+// cross-wavefront stages use block barriers).  Lane l of wavefront w holds
+// elements e = 64 E w + E l + r, r < E, in registers: partner distances j < E
+// are register compare-exchanges, E <= j < 64 E cross-lane shuffles of
+// distance j / E, only j >= 64 E goes through LDS (log2(NW) (log2(NW) + 1) / 2
+// of the stages).  Keys are unique (value bits << 32 | position), so the
+// result is the stable sort of the values.  Barriers on entry and exit.
+template <int NW, int E>
+__device__ __forceinline__ void sort_keys_lds(uint64_t* key) {
+  constexpr int N = 64 * E * NW;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const bool act = w < NW;
+  const int e0 = 64 * E * w + E * lane;
+  __syncthreads();  // the caller's writes of key[]
+  uint64_t v[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) v[r] = act ? key[e0 + r] : 0;
+  auto cx = [](uint64_t a, uint64_t p, bool keep_min) { return keep_min ? (a < p ? a : p) : (a < p ? p : a); };
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += NT) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint64_t a = key[i], b = key[l];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            key[i] = b;
-            key[l] = a;
+      if (j >= 64 * E) {
+        __syncthreads();  // every wavefront's previous reads of key[] are done
+        if (act)
+#pragma unroll
+          for (int r = 0; r < E; ++r) key[e0 + r] = v[r];
+        __syncthreads();
+        if (act)
+#pragma unroll
+          for (int r = 0; r < E; ++r) {
+            const int e = e0 + r;
+            const uint64_t p = key[e ^ j];
+            v[r] = cx(v[r], p, ((e & k) == 0) == ((e & j) == 0));
+          }
+      } else if (j >= E) {
+        if (act)
+#pragma unroll
+          for (int r = 0; r < E; ++r) {
+            const int e = e0 + r;
+            const uint64_t p = __shfl_xor(v[r], j / E, 64);
+            v[r] = cx(v[r], p, ((e & k) == 0) == ((e & j) == 0));
+          }
+      } else {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          if ((r & j) == 0) {
+            const int e = e0 + r;
+            const uint64_t a = v[r], b = v[r + j];
+            const bool up = (e & k) == 0;
+            v[r] = up ? (a < b ? a : b) : (a < b ? b : a);
+            v[r + j] = up ? (a < b ? b : a) : (a < b ? a : b);
           }
         }
       }
-      __syncthreads();
     }
   }
-}
-
-// Bitonic sort of P <= 2 * NT keys (P a power of two >= 64), ascending.
-// Thread t holds indices t and t + NT; stages whose partner distance j <= 32
-// stay inside a wavefront (register shuffles), only j >= 64 goes through LDS.
-template <int NT>
-__device__ void bitonic_sort_shfl(uint64_t* key, int P) {
-  const int t = threadIdx.x;
-  const int i0 = t, i1 = t + NT;
-  const bool h0 = i0 < P, h1 = i1 < P;
-  uint64_t v0 = h0 ? key[i0] : 0, v1 = h1 ? key[i1] : 0;
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-        if (h0) key[i0] = v0;
-        if (h1) key[i1] = v1;
-        __syncthreads();
-        if (h0) {
-          const uint64_t p = key[i0 ^ j];
-          const bool up = (i0 & k) == 0, lower = (i0 & j) == 0;
-          v0 = (lower == up) ? (v0 < p ? v0 : p) : (v0 < p ? p : v0);
-        }
-        if (h1) {
-          const uint64_t p = key[i1 ^ j];
-          const bool up = (i1 & k) == 0, lower = (i1 & j) == 0;
-          v1 = (lower == up) ? (v1 < p ? v1 : p) : (v1 < p ? p : v1);
-        }
-        __syncthreads();
-      } else {
-        const uint64_t p0 = __shfl_xor(v0, j, 64);
-        const uint64_t p1 = __shfl_xor(v1, j, 64);
-        {
-          const bool up = (i0 & k) == 0, lower = (i0 & j) == 0;
-          v0 = (lower == up) ? (v0 < p0 ? v0 : p0) : (v0 < p0 ? p0 : v0);
-        }
-        {
-          const bool up = (i1 & k) == 0, lower = (i1 & j) == 0;
-          v1 = (lower == up) ? (v1 < p1 ? v1 : p1) : (v1 < p1 ? p1 : v1);
-        }
-      }
-    }
-  }
-  if (h0) key[i0] = v0;
-  if (h1) key[i1] = v1;
   __syncthreads();
-}
-
-// Independent bitonic sorts of the cap-sized segments of key[0, total)
-// (cap a power of two >= 64, total a multiple of cap): the network's k never
-// exceeds cap, so partners stay inside a segment.  Thread t holds slots
-// t + s * NT; partner distances j <= 32 use register shuffles.
-template <int NT>
-__device__ void seg_bitonic_shfl(uint64_t* key, int total, int cap) {
-  constexpr int S = 4;  // slots per thread (total <= S * NT)
-  const int t = threadIdx.x;
-  uint64_t v[S];
-  bool h[S];
+  if (act)
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const int i = t + s * NT;
-    h[s] = i < total;
-    v[s] = h[s] ? key[i] : ~0ull;
-  }
-  for (int k = 2; k <= cap; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-          if (h[s]) key[t + s * NT] = v[s];
-        __syncthreads();
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const int i = t + s * NT;
-          if (h[s]) {
-            const uint64_t p = key[i ^ j];
-            const bool up = (i & (cap - 1) & k) == 0, lower = (i & j) == 0;  // direction from the in-segment offset
-            v[s] = (lower == up) ? (v[s] < p ? v[s] : p) : (v[s] < p ? p : v[s]);
-          }
-        }
-        __syncthreads();
-      } else {
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const int i = t + s * NT;
-          const uint64_t p = __shfl_xor(v[s], j, 64);
-          const bool up = (i & (cap - 1) & k) == 0, lower = (i & j) == 0;  // direction from the in-segment offset
-          v[s] = (lower == up) ? (v[s] < p ? v[s] : p) : (v[s] < p ? p : v[s]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < S; ++s)
-    if (h[s]) key[t + s * NT] = v[s];
+    for (int r = 0; r < E; ++r) key[e0 + r] = v[r];
   __syncthreads();
 }
 
@@ -657,13 +605,13 @@ __device__ unsigned long long g_rstamp[256][8];
 // kModeLego: LeGO-LOAM extractFeatures (featureAssociation.cpp:883-1007):
 // edges only off the ground (labels 2 for the first 2 = sharp, 1 up to 20),
 // flats only on the ground, at most 4 per sector (the 4th does not suppress).
-template <int MODE, int ITEMS>
+template <int MODE, int SORTN>
 __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     const CloudInfo ci, const float* __restrict__ curvature, const uint8_t* __restrict__ picked0,
     const uint8_t* __restrict__ ground, FeatCfg cfg, FeatWork fw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using BRS = hipcub::BlockRadixSort<uint32_t, kPickThreads, ITEMS, int32_t>;
-  __shared__ typename BRS::TempStorage tmp;
+  static_assert(SORTN >= 64 && SORTN <= 2048 && (SORTN & (SORTN - 1)) == 0, "sort size");
+  constexpr int kSortW = SORTN >= 256 ? 4 : SORTN / 64, kSortE = SORTN / (64 * kSortW);
   const int j = blockIdx.x, r = blockIdx.y;
   const int t = threadIdx.x, lane = t & 63, v = t >> 6;
   const int n = *ci.n_ext;
@@ -684,7 +632,8 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   FSTAMP(0);
   const int cap = cfg.sort_cap, pcap = cfg.sort_cap + 16;
   const int pb = max(sp - 5, base), pe = min(ep + 5, span_end);
-  int32_t* spos = reinterpret_cast<int32_t*>(smem);  // the sector in sort order
+  uint64_t* skey = reinterpret_cast<uint64_t*>(smem);  // SORTN (= cap) sort keys
+  int32_t* spos = reinterpret_cast<int32_t*>(skey + SORTN);  // the sector in sort order
   float* curv = reinterpret_cast<float*>(spos + cap);
   int32_t* col = reinterpret_cast<int32_t*>(curv + pcap);
   uint8_t* pk0 = reinterpret_cast<uint8_t*>(col + pcap);  // cloudNeighborPicked on entry
@@ -701,26 +650,18 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     pk0[q - pb] = picked0[q];
     if (MODE == kModeLego) gfl[q - pb] = ground[q];
   }
-  // the sector's sort
+  // the sector's sort: (value bits, position) keys, bitonic in registers and
+  // LDS (sort_keys_lds) -- the stable sort by value
   const int len = ep - sp;
-  {
-    uint32_t key[ITEMS];
-    int32_t val[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const int idx = t * ITEMS + i, k = sp + idx;
-      key[i] = 0xFFFFFFFFu;
-      val[i] = 0x7FFFFFFF;
-      if (idx < len) {
-        key[i] = __float_as_uint((k >= 5 && k < n - 5) ? curvature[k] : 0.0f);
-        val[i] = k;
-      }
-    }
-    BRS(tmp).Sort(key, val);
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-      if (t * ITEMS + i < len) spos[t * ITEMS + i] = val[i];
+  for (int idx = t; idx < SORTN; idx += kPickThreads) {
+    const int k = sp + idx;
+    skey[idx] = idx < len ? ((uint64_t)__float_as_uint((k >= 5 && k < n - 5) ? curvature[k] : 0.0f) << 32) |
+                                (uint32_t)k
+                          : ~0ull;
   }
+  __syncthreads();
+  sort_keys_lds<kSortW, kSortE>(skey);
+  for (int idx = t; idx < len; idx += kPickThreads) spos[idx] = (int32_t)(uint32_t)skey[idx];
   __syncthreads();
   FSTAMP(1);
   // suppression reach (:220-237, 247-262): points ind + l, l = 1..5 (and
@@ -874,17 +815,17 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
 // index over the list order (a voxel's points keep list order), one thread
 // per voxel run start, centroid summed in list order (CentroidPoint), voxels
 // in ascending index (applyFilter).
-template <int MODE, int ITEMS>
+template <int MODE, int VOXN>
 __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, FeatCfg cfg,
                                                           FeatOut out, FeatWork fw) {
+  static_assert(VOXN >= 64 && VOXN <= 4096 && (VOXN & (VOXN - 1)) == 0, "voxel sort size");
+  constexpr int kSortW = VOXN >= 1024 ? kFeatThreads / 64 : VOXN / 64, kSortE = VOXN / (64 * kSortW);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float4* rp = reinterpret_cast<float4*>(smem);                 // ring_cap: the ring's points
   float4* vp = rp + cfg.ring_cap;                               // vox_cap: voxel order
   uint64_t* keys = reinterpret_cast<uint64_t*>(vp + cfg.vox_cap);  // vox_cap
   int32_t* slist = reinterpret_cast<int32_t*>(keys + cfg.vox_cap);  // ring_cap
   int8_t* labr = reinterpret_cast<int8_t*>(slist + cfg.ring_cap);   // ring_cap
-  using BRS = hipcub::BlockRadixSort<uint32_t, kFeatThreads, ITEMS, int32_t>;
-  __shared__ typename BRS::TempStorage tmp;
   __shared__ int s_sp[6], s_ep[6], s_slot[6], s_cb[7], s_fb[7];
   __shared__ int s_hdr[36][3];  // the ring's variants: ncorner, nflat, fwd_end
   __shared__ int scratch[kFeatThreads / 64 + 1];
@@ -1047,32 +988,22 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
     return;
   }
   const float inv = 1.0f / cfg.leaf;
-  uint32_t key[ITEMS];
-  int32_t val[ITEMS];
-#pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    const int q = t * ITEMS + i;
-    key[i] = 0xFFFFFFFFu >> (32 - s_bits);  // above every voxel index: sorts last
-    val[i] = 0x7FFFFFFF;
+  // (voxel index, list index) keys: the bitonic sort (sort_keys_lds) is the
+  // stable sort of the voxel indices over the list order
+  for (int q = t; q < VOXN; q += kFeatThreads) {
+    uint64_t kv = ~0ull;  // past the list: sorts last
     if (q < m) {
       const float4 p = rp[slist[q] - start];
       const int i0 = (int)(floorf(p.x * inv) - (float)s_minb[0]);
       const int i1 = (int)(floorf(p.y * inv) - (float)s_minb[1]);
       const int i2 = (int)(floorf(p.z * inv) - (float)s_minb[2]);
-      key[i] = (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
-      val[i] = q;
+      kv = ((uint64_t)(uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]) << 32) | (uint32_t)q;
     }
+    keys[q] = kv;
   }
   RGSTAMP(5);
-  BRS(tmp).Sort(key, val, 0, s_bits);
-#pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    const int q = t * ITEMS + i;
-    if (q < m) {
-      keys[q] = ((uint64_t)key[i] << 32) | (uint32_t)val[i];
-      vp[q] = rp[slist[val[i]] - start];
-    }
-  }
+  sort_keys_lds<kSortW, kSortE>(keys);
+  for (int q = t; q < m; q += kFeatThreads) vp[q] = rp[slist[(uint32_t)keys[q]] - start];
   __syncthreads();
   RGSTAMP(6);
   const int per = (m + kFeatThreads - 1) / kFeatThreads;
@@ -1107,16 +1038,15 @@ struct FeatSmem {
 };
 inline FeatSmem feat_smem_sizes(const FeatCfg& fc) {
   const size_t pcap = (size_t)fc.sort_cap + 16;
-  return FeatSmem{4 * (size_t)fc.sort_cap + (4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
+  return FeatSmem{12 * (size_t)fc.sort_cap + (4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
                   24 * (size_t)fc.vox_cap + 21 * (size_t)fc.ring_cap};
 }
-// items per thread of the block radix sorts (0: capacity not supported)
+// the sorts' sizes (powers of two; 0: capacity not supported)
 inline int sort_items(int sort_cap) {
-  return sort_cap <= kPickThreads ? 1 : sort_cap <= 2 * kPickThreads ? 2 : sort_cap <= 3 * kPickThreads ? 3
-         : sort_cap <= 6 * kPickThreads ? 6 : 0;
+  return (sort_cap >= 64 && sort_cap <= 2048 && (sort_cap & (sort_cap - 1)) == 0) ? sort_cap : 0;
 }
 inline int vox_items(int vox_cap) {
-  return vox_cap <= kFeatThreads ? 1 : vox_cap <= 4 * kFeatThreads ? vox_cap / kFeatThreads : 0;
+  return (vox_cap >= 64 && vox_cap <= 4096 && (vox_cap & (vox_cap - 1)) == 0) ? vox_cap : 0;
 }
 
 inline hipError_t feat_work_alloc(FeatWork& fw, int R, const FeatCfg& fc) {
@@ -1138,17 +1068,28 @@ inline void feat_work_free(FeatWork& fw) {
 }
 
 template <int MODE>
-inline const void* ring_kernel(int vitems) {
-  return vitems == 1 ? (const void*)k_fe_ring<MODE, 1>
-         : vitems == 2 ? (const void*)k_fe_ring<MODE, 2> : (const void*)k_fe_ring<MODE, 4>;
+inline const void* ring_kernel(int vn) {
+  switch (vn) {
+    case 64: return (const void*)k_fe_ring<MODE, 64>;
+    case 128: return (const void*)k_fe_ring<MODE, 128>;
+    case 256: return (const void*)k_fe_ring<MODE, 256>;
+    case 512: return (const void*)k_fe_ring<MODE, 512>;
+    case 1024: return (const void*)k_fe_ring<MODE, 1024>;
+    case 2048: return (const void*)k_fe_ring<MODE, 2048>;
+    default: return (const void*)k_fe_ring<MODE, 4096>;
+  }
 }
 
-// kernels whose LDS may exceed the 64 KB default
 template <int MODE>
-inline const void* pick_kernel(int sitems) {
-  return sitems == 1 ? (const void*)k_fe_pick<MODE, 1>
-         : sitems == 2 ? (const void*)k_fe_pick<MODE, 2>
-         : sitems == 3 ? (const void*)k_fe_pick<MODE, 3> : (const void*)k_fe_pick<MODE, 6>;
+inline const void* pick_kernel(int sn) {
+  switch (sn) {
+    case 64: return (const void*)k_fe_pick<MODE, 64>;
+    case 128: return (const void*)k_fe_pick<MODE, 128>;
+    case 256: return (const void*)k_fe_pick<MODE, 256>;
+    case 512: return (const void*)k_fe_pick<MODE, 512>;
+    case 1024: return (const void*)k_fe_pick<MODE, 1024>;
+    default: return (const void*)k_fe_pick<MODE, 2048>;
+  }
 }
 
 // kernels whose LDS may exceed the 64 KB default
@@ -1172,18 +1113,36 @@ inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, const flo
   const dim3 gs(6, R);
   const uint32_t ps = (uint32_t)sm.pick;
   const uint8_t* gr = fo.ground;
+#define SLIO_PICK(N)                                                                                     \
+  case N:                                                                                              \
+    hipExtLaunchKernelGGL((k_fe_pick<MODE, N>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, \
+                          curv, picked0, gr, fc, fw);                                                  \
+    break
   switch (sort_items(fc.sort_cap)) {
-    case 1: hipExtLaunchKernelGGL((k_fe_pick<MODE, 1>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
-    case 2: hipExtLaunchKernelGGL((k_fe_pick<MODE, 2>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
-    case 3: hipExtLaunchKernelGGL((k_fe_pick<MODE, 3>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
-    default: hipExtLaunchKernelGGL((k_fe_pick<MODE, 6>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, curv, picked0, gr, fc, fw); break;
+    SLIO_PICK(64);
+    SLIO_PICK(128);
+    SLIO_PICK(256);
+    SLIO_PICK(512);
+    SLIO_PICK(1024);
+    default: SLIO_PICK(2048);
   }
+#undef SLIO_PICK
   const uint32_t rs = (uint32_t)sm.ring;
+#define SLIO_RING(N)                                                                                          \
+  case N:                                                                                                   \
+    hipExtLaunchKernelGGL((k_fe_ring<MODE, N>), dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, \
+                          fc, fo, fw);                                                                      \
+    break
   switch (vox_items(fc.vox_cap)) {
-    case 1: hipExtLaunchKernelGGL(k_fe_ring<MODE, 1>, dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, fc, fo, fw); break;
-    case 2: hipExtLaunchKernelGGL(k_fe_ring<MODE, 2>, dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, fc, fo, fw); break;
-    default: hipExtLaunchKernelGGL(k_fe_ring<MODE, 4>, dim3(R), dim3(kFeatThreads), rs, s, nullptr, ev.second, 0, ci, fc, fo, fw); break;
+    SLIO_RING(64);
+    SLIO_RING(128);
+    SLIO_RING(256);
+    SLIO_RING(512);
+    SLIO_RING(1024);
+    SLIO_RING(2048);
+    default: SLIO_RING(4096);
   }
+#undef SLIO_RING
 }
 
 __global__ __launch_bounds__(256) void k_lio_concat(int n_scan, const int32_t* start_ring,

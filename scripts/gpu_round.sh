@@ -44,6 +44,15 @@ for step in "$@"; do
         SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_prev.so timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/prev /" || exit 7
       done > gpurun_out/${tag}_ab.log 2>&1
       cat gpurun_out/${tag}_ab.log ;;
+    ab3)
+      # same-box A/B: this tree (+ two-launch with / without chunk order) vs the previous commit's library
+      # and the no-reuse-branch ablation
+      for k in 1 2; do
+        timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/main /" || exit 7
+        SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_prev.so timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/prev /" || exit 7
+        SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_noreuse.so timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/noreuse /" || exit 7
+      done > gpurun_out/${tag}_ab3.log 2>&1
+      cat gpurun_out/${tag}_ab3.log ;;
     tail)
       SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so timeout -k 10 200 python scripts/tail_stamps.py > gpurun_out/${tag}_tail.log 2>&1 || { tail gpurun_out/${tag}_tail.log; exit 8; }
       grep maxit gpurun_out/${tag}_tail.log ;;

@@ -85,12 +85,19 @@ def test_deferred_block_rows_after_rebuild(L, oracle_mod):
         L.load().slio_destroy(h)
 
 
-@pytest.mark.parametrize("cell", [1.25, 0.37])
-def test_add_delete_vs_oracle(L, oracle_mod, cell):
+@pytest.mark.parametrize("cell,grouping", [(1.25, "hash"), (0.37, "hash"), (1.25, "sort")])
+def test_add_delete_vs_oracle(L, oracle_mod, cell, grouping, monkeypatch):
     """Add_Points with downsampling (voxel groups of 1..5 new points against
-    0..4 stored points, exact duplicates for same_point), without it, box
+    0..4 stored points, exact duplicates for same_point, and voxels of 20-40
+    new points: more than a hash slot holds inline), without it, box
     deletions (also of points still waiting to be indexed), a search in
-    between: the device map equals the oracle's after every call."""
+    between: the device map equals the oracle's after every call.  Both
+    groupings of the exact-box path: hashed voxel keys (the default) and the
+    stable key sort (SLIO_NO_DS_HASH=1)."""
+    if grouping == "sort":
+        monkeypatch.setenv("SLIO_NO_DS_HASH", "1")
+    else:
+        monkeypatch.delenv("SLIO_NO_DS_HASH", raising=False)
     rng = np.random.default_rng(3)
     base = rng.uniform(-20, 20, (20000, 3)).astype(np.float32)
     base[:, 2] *= 0.2
@@ -105,6 +112,8 @@ def test_add_delete_vs_oracle(L, oracle_mod, cell):
                 base[rng.choice(base.shape[0], 500)] + rng.normal(0, 0.05, (500, 3)),
                 np.repeat(rng.uniform(-20, 20, (200, 3)), 3, axis=0),          # same voxel, same point
                 base[rng.choice(base.shape[0], 100)],                          # exact duplicates of stored
+                np.floor(rng.uniform(-20, 20, (1, 3)) / 0.5) * 0.5 + rng.uniform(0.01, 0.49, (40, 3)),
+                np.floor(rng.uniform(-20, 20, (1, 3)) / 0.5) * 0.5 + rng.uniform(0.01, 0.49, (20, 3)),
             ]).astype(np.float32)
             new = new[rng.permutation(new.shape[0])]
             assert add(L, h, new, True) == om.add_points(new, True, 0.5)

@@ -287,6 +287,27 @@ def test_fused_pass_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
         lib.slio_destroy(h)
 
 
+@pytest.mark.parametrize("mode,maxit", [(0, 3), (0, 4), (1, 4)])
+def test_fused_fresh_handle_repeated(L, c2, mode, maxit):
+    """A fresh handle whose first update is fused (bench.py's order: no
+    two-launch update before), then 12 more: every update completes and gives
+    the same bits."""
+    mp, fr, _ = c2
+    st = state_of(fr)
+    lib = L.load()
+    h = mk(L, cell=C2_CELL)
+    try:
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, fr.body) == 0
+        first = _update_once(L, h, st, maxit=maxit, mode=mode)
+        for rep in range(12):
+            again = _update_once(L, h, st, maxit=maxit, mode=mode)
+            for a, b in zip(first, again):
+                np.testing.assert_array_equal(a, b)
+    finally:
+        lib.slio_destroy(h)
+
+
 def test_batched_replay_distinct_scans(L, oracle_mod):
     """C5 replay: 4 handles share one map, each runs a DIFFERENT scan (own
     seed, own pose) from its own host thread, 3 updates each; every result
