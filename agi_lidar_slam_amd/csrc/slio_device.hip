@@ -126,15 +126,18 @@ struct GridGeom {
 
 // Coarse level for the queries the fine grid cannot finish cheaply (5th
 // neighbour beyond the 5x5x5 fine cube, query cells outside the grid): cells
-// of edge 4h on the fine grid's origin, the points sorted by coarse cell, and
-// the TIGHT bounding box of every coarse cell's points (exact pruning: a
-// float distance to a point is never below the float distance to a box that
-// contains it, both rounded monotonically).
+// of edge 4h on the fine grid's origin -- coarse cell (cx, cy, cz) is the fine
+// cells [4cx, 4cx + 4) x [4cy, 4cy + 4) x [4cz, 4cz + 4), so its points are 16
+// runs of the fine cell-sorted pts (one per fine (y, z) row) -- and a bounding
+// box of every coarse cell's points: exact pruning, since a float distance to
+// a point is never below the float distance to a box that contains it, both
+// rounded monotonically.  An upload or a sorting rebuild makes the boxes
+// tight; a merge rebuild (the live map) only widens them by its additions
+// (k_coarse_extend): a deleted point leaves a box merely conservative.  No
+// coarse copy of the points, so a merge rebuild does not rewrite one.
 struct CoarseView {
   GridGeom g;               // h = 4 x the fine cell edge
-  const float4* pts;        // sorted by coarse cell: x, y, z, bits(position in the fine pts)
-  const uint32_t* start;    // ncells + 1 prefix offsets
-  const float4* lo;         // per coarse cell: min x, y, z, bits(point count)
+  const float4* lo;         // per coarse cell: min x, y, z, bits(points ever counted: 0 = empty)
   const float4* hi;         // per coarse cell: max x, y, z
 };
 
@@ -149,8 +152,6 @@ struct MapDev {
   // coarse level (CoarseView)
   GridGeom cg;
   int64_t nccells = 0;
-  float4* cpts = nullptr;
-  uint32_t* cstart = nullptr;
   float4* clo = nullptr;
   float4* chi = nullptr;
   // block rows (optional, ~9x the points): entry (x, y, z) holds the points
@@ -199,7 +200,7 @@ struct MapDev {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf b_pts, b_keep, b_cpts, b_start, b_cstart, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6], b_add[8], b_start2;
+  Buf b_pts, b_keep, b_start, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6], b_add[8], b_start2;
   static hipError_t take(Buf& b, size_t bytes) {
     bytes = std::max<size_t>(bytes, 16);
     if (bytes <= b.cap) return hipSuccess;
@@ -221,8 +222,6 @@ struct MapDev {
     start = nullptr;
     blk = nullptr;
     bstart = nullptr;
-    cpts = nullptr;
-    cstart = nullptr;
     clo = nullptr;
     chi = nullptr;
     keep = nullptr;
@@ -230,7 +229,7 @@ struct MapDev {
   }
   ~MapDev() {
     if (ready) (void)hipEventDestroy(ready);
-    for (Buf* b : {&b_pts, &b_keep, &b_cpts, &b_start, &b_cstart, &b_clo, &b_chi, &b_bstart, &b_blk, &b_start2})
+    for (Buf* b : {&b_pts, &b_keep, &b_start, &b_clo, &b_chi, &b_bstart, &b_blk, &b_start2})
       if (b->p) (void)hipFree(b->p);
     for (Buf& b : b_tmp)
       if (b.p) (void)hipFree(b.p);
@@ -422,22 +421,20 @@ __global__ void k_coarse_count(const uint32_t* __restrict__ start, GridGeom g, G
   }
   cnt[c] = sum;
 }
-// one wavefront per 64 coarse cells: each lane reads its cell's size (empty
-// cells -- most of a surface map's -- are written by their lane at once),
-// then 16-lane groups copy the non-empty cells' rows (.w = fine position),
-// four cells at a time, and form their tight boxes (count in lo.w).  (One
-// wavefront per cell: ~240 us of a 10M map's rebuild.)
-__global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __restrict__ start, GridGeom g,
-                              GridGeom cg, const uint32_t* __restrict__ cstart, int64_t nc,
-                              float4* __restrict__ cpts, float4* __restrict__ lo, float4* __restrict__ hi) {
+// one wavefront per 64 coarse cells: each lane reads its cell's size
+// (k_coarse_count; empty cells -- most of a surface map's -- are written by
+// their lane at once), then 16-lane groups read the non-empty cells' rows,
+// four cells at a time, and form their tight boxes (count in lo.w).
+__global__ void k_coarse_boxes(const float4* __restrict__ pts, const uint32_t* __restrict__ start, GridGeom g,
+                               GridGeom cg, const uint32_t* __restrict__ cnt, int64_t nc,
+                               float4* __restrict__ lo, float4* __restrict__ hi) {
   const int64_t c_base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) << 6;
   const int lane = threadIdx.x & 63;
   const float INF = __int_as_float(0x7f800000);
   const int64_t mc = c_base + lane;
-  uint32_t mb = 0, mt = 0;
+  uint32_t mt = 0;
   if (mc < nc) {
-    mb = cstart[mc];
-    mt = cstart[mc + 1] - mb;
+    mt = cnt[mc];
     if (mt == 0) {
       lo[mc] = make_float4(INF, INF, INF, __uint_as_float(0u));
       hi[mc] = make_float4(-INF, -INF, -INF, 0.0f);
@@ -457,7 +454,7 @@ __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __
     const int64_t c = c_base + l;
     // (every lane shuffles: a cross-lane read inside a condition would read
     // lanes the condition turned off)
-    const uint32_t base = __shfl(mb, l, 64), tsrc = __shfl(mt, l, 64);
+    const uint32_t tsrc = __shfl(mt, l, 64);
     const uint32_t total = act ? tsrc : 0u;
     int cx, cy, cz;
     coarse_decode(cg, c, cx, cy, cz);
@@ -493,7 +490,6 @@ __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __
 #pragma unroll
       for (int r = 1; r < 16; ++r) src = (j >= E[r]) ? S[r] + j : src;
       const float4 v = pts[src];
-      cpts[base + j] = make_float4(v.x, v.y, v.z, __uint_as_float(src));
       l3[0] = fminf(l3[0], v.x);
       l3[1] = fminf(l3[1], v.y);
       l3[2] = fminf(l3[2], v.z);
@@ -513,6 +509,48 @@ __global__ void k_coarse_fill(const float4* __restrict__ pts, const uint32_t* __
       hi[c] = make_float4(u3[0], u3[1], u3[2], 0.0f);
     }
   }
+}
+
+// float min / max by compare-and-swap (vector atomics): the coarse boxes of
+// a merge rebuild's additions
+__device__ __forceinline__ void atomic_fmin(float* a, float v) {
+  int* ai = reinterpret_cast<int*>(a);
+  int old = __hip_atomic_load(ai, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (v < __int_as_float(old)) {
+    const int prev = atomicCAS(ai, old, __float_as_int(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+__device__ __forceinline__ void atomic_fmax(float* a, float v) {
+  int* ai = reinterpret_cast<int*>(a);
+  int old = __hip_atomic_load(ai, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (v > __int_as_float(old)) {
+    const int prev = atomicCAS(ai, old, __float_as_int(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+// widen the boxes (and counts) of the coarse cells the na additions fall in;
+// a point's coarse cell is its (clamped) fine cell / 4 on every axis
+__global__ void k_coarse_extend(const float4* __restrict__ adds, int64_t na, GridGeom g,
+                                float4* __restrict__ lo, float4* __restrict__ hi, GridGeom cg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na) return;
+  const float4 v = adds[i];
+  const int fx = min(max(cell_coord(v.x, g.ox, g.inv_h), 0), g.dx - 1);
+  const int fy = min(max(cell_coord(v.y, g.oy, g.inv_h), 0), g.dy - 1);
+  const int fz = min(max(cell_coord(v.z, g.oz, g.inv_h), 0), g.dz - 1);
+  const int64_t c = ((int64_t)(fz >> 2) * cg.dy + (fy >> 2)) * cg.dx + (fx >> 2);
+  float* l = reinterpret_cast<float*>(lo + c);
+  float* h = reinterpret_cast<float*>(hi + c);
+  atomic_fmin(l + 0, v.x);
+  atomic_fmin(l + 1, v.y);
+  atomic_fmin(l + 2, v.z);
+  atomic_fmax(h + 0, v.x);
+  atomic_fmax(h + 1, v.y);
+  atomic_fmax(h + 2, v.z);
+  atomicAdd(reinterpret_cast<unsigned int*>(l + 3), 1u);
 }
 
 // ---------------------------------------------------------------- math helpers
@@ -1218,19 +1256,21 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
 // cell; a cell is scanned unless its tight box lies farther than the bound
 // (the 5th distance found so far, or bound0: the 5th distance of 5 real map
 // points, or +inf).  The candidate cells of a batch of 64 ring positions are
-// flattened into one list (lane prefix sums in LDS, a 6-step binary search
-// per candidate) and swept with U loads in flight per lane.  The search ends
+// expanded, four at a time, into their 16 runs of the fine pts (one per fine
+// (y, z) row), flattened into one list (lane prefix sums in LDS, a 6-step
+// binary search per candidate) and swept with U loads in flight per lane.  The search ends
 // when every unscanned cell lies beyond the 5th distance: the bound over the
 // six slabs outside the ring's cube is per-axis exact (face distance on the
 // slab's axis, distance to the grid's range on the other two).  Keys carry
-// the fine pts position (.w), so results equal the fine grid's.  Returns the
-// list in every lane.
+// the fine pts position, so results equal the fine grid's.  Returns the list
+// in every lane.
 template <int U>
-__device__ __forceinline__ void far_search(const CoarseView& cv, float qx, float qy, float qz,
+__device__ __forceinline__ void far_search(const MapView& map, float qx, float qy, float qz,
                                         float bound, uint32_t* __restrict__ pre,
                                         uint32_t* __restrict__ beg, Top5& t) {
   const int lane = threadIdx.x & 63;
-  const GridGeom g = cv.g;
+  const CoarseView& cv = map.cl;
+  const GridGeom g = cv.g, fg = map.g;
   const float INF = __int_as_float(0x7f800000);
   top5_clear(t);
   bool full = false;
@@ -1294,7 +1334,8 @@ __device__ __forceinline__ void far_search(const CoarseView& cv, float qx, float
     const int total = cum[6];
     for (int base = 0; base < total; base += 64) {
       const int p = base + lane;
-      uint32_t s = 0, k = 0;
+      bool pass = false;
+      int ccx = 0, ccy = 0, ccz = 0;
       if (p < total) {
         int f = 0;
 #pragma unroll
@@ -1311,59 +1352,74 @@ __device__ __forceinline__ void far_search(const CoarseView& cv, float qx, float
         const int l = p - (f == 0 ? 0 : f == 1 ? cum[1] : f == 2 ? cum[2] : f == 3 ? cum[3] : f == 4 ? cum[4] : cum[5]);
         const int ua = A + l % NA, ub = B + l / NA;
         const int fax = f >> 1;
-        const int x = fax == 0 ? V : ua;
-        const int y = fax == 0 ? ua : fax == 1 ? V : ub;
-        const int z = fax == 2 ? V : ub;
-        {
-          const uint32_t c = ((uint32_t)z * (uint32_t)g.dy + (uint32_t)y) * (uint32_t)g.dx + (uint32_t)x;
-          const float4 lo = cv.lo[c];
-          const uint32_t cnt = __float_as_uint(lo.w);
-          if (cnt) {
-            const float4 hi = cv.hi[c];
-            const float gx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
-            const float gy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
-            const float gz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
-            const float gd = (gx * gx + gy * gy) + gz * gz;
-            if (!(gd > fminf(bound, d5))) {  // a point at exactly d5 may still win on position
-              s = cv.start[c];
-              k = cnt;
-            }
+        ccx = fax == 0 ? V : ua;
+        ccy = fax == 0 ? ua : fax == 1 ? V : ub;
+        ccz = fax == 2 ? V : ub;
+        const uint32_t c = ((uint32_t)ccz * (uint32_t)g.dy + (uint32_t)ccy) * (uint32_t)g.dx + (uint32_t)ccx;
+        const float4 lo = cv.lo[c];
+        if (__float_as_uint(lo.w)) {
+          const float4 hi = cv.hi[c];
+          const float gx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
+          const float gy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
+          const float gz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
+          const float gd = (gx * gx + gy * gy) + gz * gz;
+          pass = !(gd > fminf(bound, d5));  // a point at exactly d5 may still win on position
+        }
+      }
+      // the passing coarse cells, four at a time: lane l reads the bounds of
+      // fine row (l & 15) of passing cell (l >> 4), one run of the fine pts
+      uint64_t pm = __ballot(pass);
+      const int gi = lane >> 4, sl = lane & 15;
+      while (pm) {
+        uint64_t bm = pm;
+        for (int q = 0; q < gi && bm; ++q) bm &= bm - 1;  // the gi-th passing cell
+        const bool act = bm != 0;
+        const int src = act ? __ffsll((unsigned long long)bm) - 1 : 0;
+        // (every lane shuffles: a cross-lane read inside a condition would
+        // read lanes the condition turned off)
+        const int x = __shfl(ccx, src, 64), y = __shfl(ccy, src, 64), z = __shfl(ccz, src, 64);
+        for (int q = 0; q < 4 && pm; ++q) pm &= pm - 1;
+        uint32_t s = 0, k = 0;
+        const int fy = 4 * y + (sl & 3), fz = 4 * z + (sl >> 2);
+        if (act && fy < fg.dy && fz < fg.dz) {
+          const int64_t rb = ((int64_t)fz * fg.dy + fy) * fg.dx;
+          s = map.start[rb + 4 * x];
+          k = map.start[rb + min(4 * x + 4, fg.dx)] - s;
+        }
+        if (!__any(k != 0)) continue;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(k, tot);
+        pre[lane] = ex;
+        beg[lane] = s;
+        wave_fence();
+        for (uint32_t f0 = 0; f0 < tot; f0 += 64 * U) {
+          uint32_t a[U];
+          float4 c[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t f = min(f0 + (uint32_t)(u * 64 + lane), tot - 1);
+            int j = 0;
+#pragma unroll
+            for (int st = 32; st > 0; st >>= 1)
+              if (pre[j + st] <= f) j += st;
+            a[u] = beg[j] + (f - pre[j]);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) c[u] = map.pts[a[u]];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
+            const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+            const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)a[u];
+            top5_insert(t, (f0 + (uint32_t)(u * 64 + lane) < tot) ? key : kInfKey);
           }
         }
+        group_merge<64>(t);  // every lane: the merged list
+        full = t.k[4] != kInfKey;
+        if (full) d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
+        if (lane != 0) top5_clear(t);  // lane 0 keeps it
+        wave_fence();                  // pre / beg are rewritten by the next batch
       }
-      if (!__any(k != 0)) continue;
-      uint32_t tot;
-      const uint32_t ex = wave_excl_scan(k, tot);
-      pre[lane] = ex;
-      beg[lane] = s;
-      wave_fence();
-      for (uint32_t f0 = 0; f0 < tot; f0 += 64 * U) {
-        uint32_t a[U];
-        float4 c[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const uint32_t f = min(f0 + (uint32_t)(u * 64 + lane), tot - 1);
-          int j = 0;
-#pragma unroll
-          for (int st = 32; st > 0; st >>= 1)
-            if (pre[j + st] <= f) j += st;
-          a[u] = beg[j] + (f - pre[j]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) c[u] = cv.pts[a[u]];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
-          const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
-          const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c[u].w);
-          top5_insert(t, (f0 + (uint32_t)(u * 64 + lane) < tot) ? key : kInfKey);
-        }
-      }
-      group_merge<64>(t);  // every lane: the merged list
-      full = t.k[4] != kInfKey;
-      if (full) d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
-      if (lane != 0) top5_clear(t);  // lane 0 keeps it
-      wave_fence();                  // pre / beg are rewritten by the next batch
     }
     // lower bound of the squared distance to every cell outside this cube
     float lb = INF;
@@ -2703,7 +2759,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           const float d5n = __uint_as_float((uint32_t)(tr.k[4] >> 32));
           const bool fin = cov2 || (tr.k[4] != kInfKey && b2 > 0.0f && d5n < (b2 * b2) * 0.99999f);
           const int slot = ref.slot[k];
-          const int64_t i = chunk * SLIO_CHUNK + slot;
           if (fin) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
@@ -2748,9 +2803,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     for (int k = tid >> 6; k < nfar; k += NT / 64) {
       const float4 q = far_q[k];
       Top5 tf;
-      far_search<4>(map.cl, q.x, q.y, q.z, q.w, far_pre[tid >> 6], far_beg[tid >> 6], tf);
+      far_search<4>(map, q.x, q.y, q.z, q.w, far_pre[tid >> 6], far_beg[tid >> 6], tf);
       const int slot = far_slot[k];
-      const int64_t i = chunk * SLIO_CHUNK + slot;
       uint64_t mk = tf.k[0];
 #pragma unroll
       for (int j = 1; j < 5; ++j) mk = (lane == j) ? tf.k[j] : mk;
@@ -3134,6 +3188,8 @@ struct Ctx {
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail,
   MapDev::Buf inc[7];         // map_incremental temporaries, kept across scans
                               // (zero between launches)
+  MapDev::Buf pre[16];        // undistortion / VoxelGrid temporaries, kept across scans
+                              // (per-call hipMalloc + hipFree cost more than the kernels)
   IkfCtl* ctl = nullptr;    // device-resident update state (HBM)
   IkfCtl* h_ctl = nullptr;  // mapped, coherent host block: update input and output
   IkfCtl* d_hctl = nullptr; // its device view
@@ -3445,7 +3501,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   };
   if (nblk > 0 && run_search) {
     const auto ev = timing(SLIO_KERNEL_SEARCH);
-    const CoarseView cv{c.map->cg, c.map->cpts, c.map->cstart, c.map->clo, c.map->chi};
+    const CoarseView cv{c.map->cg, c.map->clo, c.map->chi};
     const MapView mv{c.map->g,   c.map->n,    c.map->pts,    c.map->start, c.map->blk,
                      c.map->bstart, c.map->nblk, c.map->ncells, cv};
     const bool sph = cfg.radius_sq > 0.0f;
@@ -3717,6 +3773,8 @@ int slio_destroy(slio_handle h) {
   (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
   for (auto& b : h->c.inc)
+    if (b.p) (void)hipFree(b.p);
+  for (auto& b : h->c.pre)
     if (b.p) (void)hipFree(b.p);
   if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
   if (h->c.grp_ev) (void)hipEventDestroy(h->c.grp_ev);
@@ -4005,26 +4063,21 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
   };
   hipError_t e;
   if ((e = m.take(m.b_start, sizeof(uint32_t) * (m.ncells + 1))) ||
-      (e = m.take(m.b_cstart, sizeof(uint32_t) * (m.nccells + 1))) ||
       (e = m.take(m.b_clo, sizeof(float4) * m.nccells)) || (e = m.take(m.b_chi, sizeof(float4) * m.nccells)))
     return fail("hipMalloc", e);
   m.start = (uint32_t*)m.b_start.p;
-  m.cstart = (uint32_t*)m.b_cstart.p;
   m.clo = (float4*)m.b_clo.p;
   m.chi = (float4*)m.b_chi.p;
   if (n == 0) {
     if ((e = hipMemsetAsync(m.start, 0, sizeof(uint32_t) * (m.ncells + 1), st)) ||
-        (e = hipMemsetAsync(m.cstart, 0, sizeof(uint32_t) * (m.nccells + 1), st)) ||
         (e = hipMemsetAsync(m.clo, 0, sizeof(float4) * m.nccells, st)) || (e = hipStreamSynchronize(st)))
       return fail("empty map", e);
     return SLIO_OK;
   }
-  if ((e = m.take(m.b_pts, sizeof(float4) * n)) || (e = m.take(m.b_keep, n)) ||
-      (e = m.take(m.b_cpts, sizeof(float4) * n)))
+  if ((e = m.take(m.b_pts, sizeof(float4) * n)) || (e = m.take(m.b_keep, n)))
     return fail("hipMalloc", e);
   m.pts = (float4*)m.b_pts.p;
   m.keep = (uint8_t*)m.b_keep.p;
-  m.cpts = (float4*)m.b_cpts.p;
   uint64_t *k0 = nullptr, *k1 = nullptr;
   uint32_t *v0 = nullptr, *v1 = nullptr, *cnt = nullptr, *c0 = nullptr, *c1 = nullptr;
   void* tmp = nullptr;
@@ -4088,15 +4141,11 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     }
     k_gather4<<<nb, 256, 0, st>>>(in, v1, n, m.pts);
     k_fill_u8<<<nb, 256, 0, st>>>(m.keep, n, 1);
-    // coarse level from the fine cell table (k_coarse_count / k_coarse_fill:
+    // coarse level from the fine cell table (k_coarse_count / k_coarse_boxes:
     // no sort), tight boxes
     k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, cg, m.nccells, cnt);
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, t4, cnt, m.cstart, (int)(m.nccells + 1), st))) {
-      rc = fail("coarse scan", e);
-      break;
-    }
-    k_coarse_fill<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, cg, m.cstart, m.nccells,
-                                                                  m.cpts, m.clo, m.chi);
+    k_coarse_boxes<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, cg, cnt, m.nccells, m.clo,
+                                                                   m.chi);
     if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
       rc = fail("build kernels", e);
       break;
@@ -4727,13 +4776,34 @@ __global__ void k_vg_bbox(const float* __restrict__ x, const float* __restrict__
       hi[a] = max(hi[a], __shfl_xor(hi[a], d, 64));
     }
   for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  // one set of atomics per workgroup on a small grid (as k_bbox4): one per
+  // wavefront of a 391-block grid serialised on the 7 counters' cache line,
+  // 128 us for a 100k-point scan
+  __shared__ int32_t wl[3][4], wh[3][4];
+  __shared__ int wc[4];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      atomicMin(out + a, lo[a]);
-      atomicMax(out + 3 + a, hi[a]);
+      wl[a][w] = lo[a];
+      wh[a][w] = hi[a];
     }
-    atomicAdd(out + 6, cnt);
+    wc[w] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int a = threadIdx.x;
+    int32_t l = wl[a][0], h = wh[a][0];
+    for (int q = 1; q < (int)(blockDim.x >> 6); ++q) {
+      l = min(l, wl[a][q]);
+      h = max(h, wh[a][q]);
+    }
+    atomicMin(out + a, l);
+    atomicMax(out + 3 + a, h);
+  } else if (threadIdx.x == 3) {
+    int c = 0;
+    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) c += wc[q];
+    atomicAdd(out + 6, c);
   }
 }
 
@@ -4899,7 +4969,7 @@ static int add_reserve(MapDev& m, int64_t more, hipStream_t st) {
 }
 
 static MapView map_view(const MapDev& m) {
-  const CoarseView cv{m.cg, m.cpts, m.cstart, m.clo, m.chi};
+  const CoarseView cv{m.cg, m.clo, m.chi};
   return MapView{m.g, m.n, m.pts, m.start, m.blk, m.bstart, m.nblk, m.ncells, cv};
 }
 
@@ -5304,24 +5374,12 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   m.pts = (float4*)m.b_pts.p;
   m.start = (uint32_t*)m.b_start.p;
   m.n = n;
-  if ((e = m.take(m.b_keep, std::max<int64_t>(n, 1))) || (e = m.take(m.b_cpts, sizeof(float4) * std::max<int64_t>(n, 1))))
-    return fail("hipMalloc", e);
+  if ((e = m.take(m.b_keep, std::max<int64_t>(n, 1)))) return fail("hipMalloc", e);
   m.keep = (uint8_t*)m.b_keep.p;
-  m.cpts = (float4*)m.b_cpts.p;
   k_fill_u8<<<grid_blocks(n), 256, 0, st>>>(m.keep, n, 1);
-  // coarse level from the new cell table (as build_index)
-  if ((e = m.take(m.b_tmp[6], 4 * (m.nccells + 1)))) return fail("hipMalloc", e);
-  uint32_t* cnt = (uint32_t*)m.b_tmp[6].p;
-  size_t t3 = 0;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, t3, cnt, m.cstart, (int)(m.nccells + 1), st)) ||
-      (e = m.take(m.b_tmp[7], t3)))
-    return fail("coarse scan size", e);
-  t3 = m.b_tmp[7].cap;
-  k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, m.cg, m.nccells, cnt);
-  if ((e = hipcub::DeviceScan::ExclusiveSum(m.b_tmp[7].p, t3, cnt, m.cstart, (int)(m.nccells + 1), st)))
-    return fail("coarse scan", e);
-  k_coarse_fill<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, m.cg, m.cstart, m.nccells, m.cpts,
-                                                               m.clo, m.chi);
+  // coarse level: the boxes widened by the additions (deleted points leave
+  // them conservative); the points themselves are the fine runs
+  if (na) k_coarse_extend<<<grid_blocks(na), 256, 0, st>>>(acomp, na, g, m.clo, m.chi, m.cg);
   if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) return fail("coarse kernels", e);
   m.blk = nullptr;
   m.bstart = nullptr;
@@ -5368,7 +5426,7 @@ static int map_refresh_locked(Ctx& c, bool adds_only) {
     // a grid that still holds every point: merge instead of sorting
     // (SLIO_NO_MERGE=1: always sort)
     const char* nm = std::getenv("SLIO_NO_MERGE");
-    if (n0 > 0 && m.start && m.cstart && !(nm && nm[0] && nm[0] != '0')) {
+    if (n0 > 0 && m.start && m.clo && !(nm && nm[0] && nm[0] != '0')) {
       bool handled = false;
       const int rc = merge_rebuild(m, st, &handled);
       if (handled || rc) {
@@ -5863,7 +5921,6 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
   hipStream_t st = c.stream;
   uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *hd = nullptr, *rk = nullptr;
   int32_t* bb = nullptr;
-  void* tmp = nullptr;
   int rc = nbr_settle_shared(c);  // the scan it was searched with is replaced
   if (rc) return rc;
   int64_t m = 0;
@@ -5871,13 +5928,22 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
   do {
     if (n == 0) break;
     hipError_t e;
-    if ((e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) || (e = hipMalloc(&v0, 4 * n)) ||
-        (e = hipMalloc(&v1, 4 * n)) || (e = hipMalloc(&hd, 4 * n)) || (e = hipMalloc(&rk, 4 * n)) ||
-        (e = hipMalloc(&bb, 32))) {
+    // (pre[0..3] may hold the undistorted input: slio_scan_upload_undistort_voxel)
+    MapDev::Buf* B = c.pre + 8;
+    if ((e = MapDev::take(B[0], 4 * n)) || (e = MapDev::take(B[1], 4 * n)) || (e = MapDev::take(B[2], 4 * n)) ||
+        (e = MapDev::take(B[3], 4 * n)) || (e = MapDev::take(B[4], 4 * n)) || (e = MapDev::take(B[5], 4 * n)) ||
+        (e = MapDev::take(B[6], 32))) {
       set_error(std::string("slio_scan_upload_voxel: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
       break;
     }
+    k0 = (uint32_t*)B[0].p;
+    k1 = (uint32_t*)B[1].p;
+    v0 = (uint32_t*)B[2].p;
+    v1 = (uint32_t*)B[3].p;
+    hd = (uint32_t*)B[4].p;
+    rk = (uint32_t*)B[5].p;
+    bb = (int32_t*)B[6].p;
     const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
     int32_t got[8];
     if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
@@ -5885,7 +5951,7 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
       rc = SLIO_EDEVICE;
       break;
     }
-    k_vg_bbox<<<std::min(grid_blocks(n), 1024), 256, 0, st>>>(dx_, dy_, dz_, n, bb);
+    k_vg_bbox<<<std::min(grid_blocks(n), 64), 256, 0, st>>>(dx_, dy_, dz_, n, bb);
     if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
       set_error(std::string("slio_scan_upload_voxel: bbox: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
@@ -5918,8 +5984,8 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
     k_vg_keys<<<nb, 256, 0, st>>>(dx_, dy_, dz_, n, G, k0, v0);
     size_t tb = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
-        (e = hipMalloc(&tmp, tb)) ||
-        (e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
+        (e = MapDev::take(B[7], tb)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(B[7].p, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
       set_error(std::string("slio_scan_upload_voxel: sort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
@@ -5960,8 +6026,6 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
     c.searched = false;
     if (n_down) *n_down = m;
   }
-  for (void* q : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)hd, (void*)rk, (void*)bb, tmp})
-    if (q) (void)hipFree(q);
   return rc;
 }
 
@@ -6464,18 +6528,25 @@ static int undistort_device(Ctx& c, const float* x, const float* y, const float*
   float *dx_ = nullptr, *dy_ = nullptr, *dz_ = nullptr, *dt_ = nullptr;
   uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr;
   slio_imu_pose* dp = nullptr;
-  void* tmp = nullptr;
   int rc = SLIO_OK;
   do {
     hipError_t e;
-    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n)) ||
-        (e = hipMalloc(&dt_, 4 * n)) || (e = hipMalloc(&k0, 4 * n)) || (e = hipMalloc(&k1, 4 * n)) ||
-        (e = hipMalloc(&v0, 4 * n)) || (e = hipMalloc(&v1, 4 * n)) ||
-        (e = hipMalloc(&dp, sizeof(slio_imu_pose) * std::max(np, 1)))) {
+    MapDev::Buf* B = c.pre + 4;  // pre[0..3]: the caller's output; pre[8..15]: voxel_device
+    if ((e = MapDev::take(B[0], 16 * n)) || (e = MapDev::take(B[1], 16 * n)) ||
+        (e = MapDev::take(B[2], sizeof(slio_imu_pose) * std::max(np, 1)))) {
       set_error(std::string("slio undistort: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
       break;
     }
+    dx_ = (float*)B[0].p;
+    dy_ = dx_ + n;
+    dz_ = dx_ + 2 * n;
+    dt_ = dx_ + 3 * n;
+    k0 = (uint32_t*)B[1].p;
+    k1 = k0 + n;
+    v0 = k0 + 2 * n;
+    v1 = k0 + 3 * n;
+    dp = (slio_imu_pose*)B[2].p;
     if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, st)) ||
         (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, st)) ||
         (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, st)) ||
@@ -6489,8 +6560,8 @@ static int undistort_device(Ctx& c, const float* x, const float* y, const float*
     k_time_keys<<<nb, 256, 0, st>>>(dt_, n, k0, v0);
     size_t tb = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
-        (e = hipMalloc(&tmp, tb)) ||
-        (e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
+        (e = MapDev::take(B[3], tb)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(B[3].p, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
       set_error(std::string("slio undistort: sort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
@@ -6502,9 +6573,6 @@ static int undistort_device(Ctx& c, const float* x, const float* y, const float*
       break;
     }
   } while (0);
-  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)dt_, (void*)k0, (void*)k1, (void*)v0, (void*)v1,
-                  (void*)dp, tmp})
-    if (q) (void)hipFree(q);
   return rc;
 }
 
@@ -6521,8 +6589,8 @@ int slio_undistort(slio_handle h, const float* x, const float* y, const float* z
   }
   if (n == 0) return SLIO_OK;
   Ctx& c = h->c;
-  float* u = nullptr;
-  SLIO_HIP(hipMalloc(&u, 16 * n));
+  SLIO_HIP(MapDev::take(c.pre[0], 16 * n));
+  float* u = (float*)c.pre[0].p;
   int rc = undistort_device(c, x, y, z, t_ms, n, poses, npose, x_end, u, u + n, u + 2 * n, u + 3 * n);
   if (!rc) {
     hipError_t e;
@@ -6533,7 +6601,6 @@ int slio_undistort(slio_handle h, const float* x, const float* y, const float* z
       rc = SLIO_EDEVICE;
     }
   }
-  (void)hipFree(u);
   return rc;
 }
 
@@ -6548,11 +6615,13 @@ int slio_scan_upload_undistort_voxel(slio_handle h, const float* x, const float*
   }
   Ctx& c = h->c;
   float* u = nullptr;
-  if (n > 0) SLIO_HIP(hipMalloc(&u, 16 * n));
+  if (n > 0) {
+    SLIO_HIP(MapDev::take(c.pre[0], 16 * n));
+    u = (float*)c.pre[0].p;
+  }
   int rc = n > 0 ? undistort_device(c, x, y, z, t_ms, n, poses, npose, x_end, u, u + n, u + 2 * n, u + 3 * n)
                  : SLIO_OK;
   if (!rc) rc = voxel_device(c, u, u ? u + n : nullptr, u ? u + 2 * n : nullptr, n, leaf, n_down);
-  if (u) (void)hipFree(u);
   return rc;
 }
 
@@ -6568,19 +6637,21 @@ int slio_scan_upload_voxel(slio_handle h, const float* x, const float* y, const 
   int rc = SLIO_OK;
   if (n > 0) {
     hipError_t e;
-    if ((e = hipMalloc(&dx_, 4 * n)) || (e = hipMalloc(&dy_, 4 * n)) || (e = hipMalloc(&dz_, 4 * n))) {
+    if ((e = MapDev::take(c.pre[0], 12 * n))) {
       set_error(std::string("slio_scan_upload_voxel: hipMalloc: ") + hipGetErrorString(e));
-      rc = SLIO_ENOMEM;
-    } else if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
-               (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
-               (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, c.stream))) {
+      return SLIO_ENOMEM;
+    }
+    dx_ = (float*)c.pre[0].p;
+    dy_ = dx_ + n;
+    dz_ = dx_ + 2 * n;
+    if ((e = hipMemcpyAsync(dx_, x, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
+        (e = hipMemcpyAsync(dy_, y, 4 * n, hipMemcpyHostToDevice, c.stream)) ||
+        (e = hipMemcpyAsync(dz_, z, 4 * n, hipMemcpyHostToDevice, c.stream))) {
       set_error(std::string("slio_scan_upload_voxel: H2D: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
     }
   }
   if (!rc) rc = voxel_device(c, dx_, dy_, dz_, n, leaf, n_down);
-  for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_})
-    if (q) (void)hipFree(q);
   return rc;
 }
 

@@ -206,7 +206,7 @@ __device__ int block_exclusive_scan(int v, int* scratch /* NT/64 + 1 */, int& ex
   return total;
 }
 
-// Bitonic sort of N = 64 * E * NW 64-bit keys in LDS (ascending), by the
+// Bitonic sort of N = 64 * E * NW keys (K: 32 or 64 bits) in LDS (ascending), by the
 // first NW wavefronts of the block; every thread of the block calls it (the
 // cross-wavefront stages use block barriers).  Lane l of wavefront w holds
 // elements e = 64 E w + E l + r, r < E, in registers: partner distances j < E
@@ -214,17 +214,17 @@ __device__ int block_exclusive_scan(int v, int* scratch /* NT/64 + 1 */, int& ex
 // distance j / E, only j >= 64 E goes through LDS (log2(NW) (log2(NW) + 1) / 2
 // of the stages).  Keys are unique (value bits << 32 | position), so the
 // result is the stable sort of the values.  Barriers on entry and exit.
-template <int NW, int E>
-__device__ __forceinline__ void sort_keys_lds(uint64_t* key) {
+template <int NW, int E, typename K = uint64_t>
+__device__ __forceinline__ void sort_keys_lds(K* key) {
   constexpr int N = 64 * E * NW;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const bool act = w < NW;
   const int e0 = 64 * E * w + E * lane;
   __syncthreads();  // the caller's writes of key[]
-  uint64_t v[E];
+  K v[E];
 #pragma unroll
-  for (int r = 0; r < E; ++r) v[r] = act ? key[e0 + r] : 0;
-  auto cx = [](uint64_t a, uint64_t p, bool keep_min) { return keep_min ? (a < p ? a : p) : (a < p ? p : a); };
+  for (int r = 0; r < E; ++r) v[r] = act ? key[e0 + r] : K(0);
+  auto cx = [](K a, K p, bool keep_min) { return keep_min ? (a < p ? a : p) : (a < p ? p : a); };
 #pragma unroll
   for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
@@ -239,7 +239,7 @@ __device__ __forceinline__ void sort_keys_lds(uint64_t* key) {
 #pragma unroll
           for (int r = 0; r < E; ++r) {
             const int e = e0 + r;
-            const uint64_t p = key[e ^ j];
+            const K p = key[e ^ j];
             v[r] = cx(v[r], p, ((e & k) == 0) == ((e & j) == 0));
           }
       } else if (j >= E) {
@@ -247,7 +247,7 @@ __device__ __forceinline__ void sort_keys_lds(uint64_t* key) {
 #pragma unroll
           for (int r = 0; r < E; ++r) {
             const int e = e0 + r;
-            const uint64_t p = __shfl_xor(v[r], j / E, 64);
+            const K p = __shfl_xor(v[r], j / E, 64);
             v[r] = cx(v[r], p, ((e & k) == 0) == ((e & j) == 0));
           }
       } else {
@@ -255,7 +255,7 @@ __device__ __forceinline__ void sort_keys_lds(uint64_t* key) {
         for (int r = 0; r < E; ++r) {
           if ((r & j) == 0) {
             const int e = e0 + r;
-            const uint64_t a = v[r], b = v[r + j];
+            const K a = v[r], b = v[r + j];
             const bool up = (e & k) == 0;
             v[r] = up ? (a < b ? a : b) : (a < b ? b : a);
             v[r + j] = up ? (a < b ? b : a) : (a < b ? a : b);
@@ -819,7 +819,11 @@ template <int MODE, int VOXN>
 __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, FeatCfg cfg,
                                                           FeatOut out, FeatWork fw) {
   static_assert(VOXN >= 64 && VOXN <= 4096 && (VOXN & (VOXN - 1)) == 0, "voxel sort size");
-  constexpr int kSortW = VOXN >= 1024 ? kFeatThreads / 64 : VOXN / 64, kSortE = VOXN / (64 * kSortW);
+#ifndef SLIO_RING_SORT_W
+#define SLIO_RING_SORT_W 16
+#endif
+  constexpr int kSortW0 = VOXN / 64 < SLIO_RING_SORT_W ? VOXN / 64 : SLIO_RING_SORT_W;
+  constexpr int kSortW = kSortW0 < kFeatThreads / 64 ? kSortW0 : kFeatThreads / 64, kSortE = VOXN / (64 * kSortW);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float4* rp = reinterpret_cast<float4*>(smem);                 // ring_cap: the ring's points
   float4* vp = rp + cfg.ring_cap;                               // vox_cap: voxel order
@@ -989,20 +993,43 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
   }
   const float inv = 1.0f / cfg.leaf;
   // (voxel index, list index) keys: the bitonic sort (sort_keys_lds) is the
-  // stable sort of the voxel indices over the list order
-  for (int q = t; q < VOXN; q += kFeatThreads) {
-    uint64_t kv = ~0ull;  // past the list: sorts last
-    if (q < m) {
-      const float4 p = rp[slist[q] - start];
-      const int i0 = (int)(floorf(p.x * inv) - (float)s_minb[0]);
-      const int i1 = (int)(floorf(p.y * inv) - (float)s_minb[1]);
-      const int i2 = (int)(floorf(p.z * inv) - (float)s_minb[2]);
-      kv = ((uint64_t)(uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]) << 32) | (uint32_t)q;
-    }
-    keys[q] = kv;
+  // stable sort of the voxel indices over the list order.  When the voxel
+  // index fits 32 - log2(VOXN) bits (the usual ring) the keys are 32-bit --
+  // half the cross-lane traffic and one-instruction compares -- and widen to
+  // the 64-bit (voxel << 32 | list index) layout after the sort.
+  auto voxel_of = [&](int q) {
+    const float4 p = rp[slist[q] - start];
+    const int i0 = (int)(floorf(p.x * inv) - (float)s_minb[0]);
+    const int i1 = (int)(floorf(p.y * inv) - (float)s_minb[1]);
+    const int i2 = (int)(floorf(p.z * inv) - (float)s_minb[2]);
+    return (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
+  };
+  constexpr int kQBits = __builtin_ctz(VOXN);
+#ifdef SLIO_RING_NO_NARROW
+  if (false) {
+#else
+  if (s_bits + kQBits <= 32) {
+#endif
+    uint32_t* k32 = reinterpret_cast<uint32_t*>(keys);
+    for (int q = t; q < VOXN; q += kFeatThreads) k32[q] = q < m ? (voxel_of(q) << kQBits) | (uint32_t)q : ~0u;
+    RGSTAMP(5);
+    sort_keys_lds<kSortW, kSortE, uint32_t>(k32);
+    constexpr int kHeld = (VOXN + kFeatThreads - 1) / kFeatThreads;
+    uint32_t held[kHeld];
+#pragma unroll
+    for (int i = 0; i < kHeld; ++i) held[i] = t + i * kFeatThreads < VOXN ? k32[t + i * kFeatThreads] : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kHeld; ++i)
+      if (t + i * kFeatThreads < VOXN)
+        keys[t + i * kFeatThreads] = ((uint64_t)(held[i] >> kQBits) << 32) | (held[i] & (VOXN - 1));
+    __syncthreads();
+  } else {
+    for (int q = t; q < VOXN; q += kFeatThreads)  // past the list: sorts last
+      keys[q] = q < m ? ((uint64_t)voxel_of(q) << 32) | (uint32_t)q : ~0ull;
+    RGSTAMP(5);
+    sort_keys_lds<kSortW, kSortE>(keys);
   }
-  RGSTAMP(5);
-  sort_keys_lds<kSortW, kSortE>(keys);
   for (int q = t; q < m; q += kFeatThreads) vp[q] = rp[slist[(uint32_t)keys[q]] - start];
   __syncthreads();
   RGSTAMP(6);
@@ -1672,9 +1699,10 @@ __global__ __launch_bounds__(256) void k_lego_fill(const float* __restrict__ x,
                                                    const float* __restrict__ y,
                                                    const float* __restrict__ z, LGeo g,
                                                    const int32_t* owner, float* range_mat,
-                                                   float4* full) {
+                                                   float4* full, int8_t* ground) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= g.cells) return;
+  ground[c] = 0;  // k_lego_ground sets the ground rows' flags
   const int o = owner[c];
   if (o < 0) {
     range_mat[c] = FLT_MAX;
@@ -1687,24 +1715,61 @@ __global__ __launch_bounds__(256) void k_lego_fill(const float* __restrict__ x,
   full[c] = make_float4(px, py, pz, (float)((double)(float)row + (double)(float)col / 10000.0));
 }
 
-__global__ __launch_bounds__(256) void k_lego_ground(LGeo g, const int32_t* owner, const float4* full,
-                                                     int8_t* ground, int32_t* parent) {
+// groundRemoval per column (:216-262): the ground rows' cells and points are
+// read up front (one round trip instead of one per row: the loop's flag
+// stores could alias the loads), the flags formed in registers in the
+// reference's row order, then stored.  init_parent: the union-find roots of
+// the global labelComponents kernels (k_lego_cc sets its own).
+constexpr int kLegoGroundRows = 16;
+__global__ __launch_bounds__(256) void k_lego_ground(LGeo g, const int32_t* __restrict__ owner,
+                                                     const float4* __restrict__ full, int8_t* __restrict__ ground,
+                                                     int32_t* __restrict__ parent, bool init_parent) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= g.H) return;
-  for (int i = 0; i < g.gsi; ++i) {
-    const int64_t lo = j + (int64_t)i * g.H, up = lo + g.H;
-    if (owner[lo] < 0 || owner[up] < 0) {
-      ground[lo] = -1;
-      continue;
-    }
-    const float4 a = full[lo], b = full[up];
+  auto ground_test = [&](const float4& a, const float4& b) {
     const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
     const float angle = (float)((double)(fatan2(dz, sqrtf(dx * dx + dy * dy)) * 180.0f) / M_PI);
-    if (fabsf(angle - g.mount) <= 10) {
-      ground[lo] = 1;
-      ground[up] = 1;
+    return fabsf(angle - g.mount) <= 10;
+  };
+  if (g.gsi < kLegoGroundRows) {
+    int own[kLegoGroundRows + 1];
+    float4 f[kLegoGroundRows + 1];
+    int8_t gr[kLegoGroundRows + 1];
+#pragma unroll
+    for (int i = 0; i <= kLegoGroundRows; ++i) {
+      own[i] = i <= g.gsi ? owner[j + (int64_t)i * g.H] : -1;
+      gr[i] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i <= kLegoGroundRows; ++i)
+      f[i] = (i <= g.gsi && own[i] >= 0) ? full[j + (int64_t)i * g.H] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < kLegoGroundRows; ++i) {
+      if (i >= g.gsi) break;
+      if (own[i] < 0 || own[i + 1] < 0) {
+        gr[i] = -1;
+      } else if (ground_test(f[i], f[i + 1])) {
+        gr[i] = 1;
+        gr[i + 1] = 1;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i <= kLegoGroundRows; ++i)
+      if (i <= g.gsi && gr[i] != 0) ground[j + (int64_t)i * g.H] = gr[i];
+  } else {
+    for (int i = 0; i < g.gsi; ++i) {
+      const int64_t lo = j + (int64_t)i * g.H, up = lo + g.H;
+      if (owner[lo] < 0 || owner[up] < 0) {
+        ground[lo] = -1;
+        continue;
+      }
+      if (ground_test(full[lo], full[up])) {
+        ground[lo] = 1;
+        ground[up] = 1;
+      }
     }
   }
+  if (!init_parent) return;
   // labelMat = -1 for ground and empty cells (:247-254); the rest start as
   // their own union-find roots
   for (int i = 0; i < g.N; ++i) {
@@ -1779,6 +1844,183 @@ __global__ __launch_bounds__(256) void k_lego_compress(LGeo g, int32_t* parent, 
     const int row = (int)(c / g.H);
     atomicOr(&rows[2 * (int64_t)r + (row >> 6)], 1ull << (row & 63));
   }
+}
+
+// ---- labelComponents in one workgroup's LDS (images of <= kLegoCcCells
+// cells, e.g. VLP-16's 16 x 1800): the union-find of k_lego_union /
+// k_lego_compress ran on global atomics with chains as long as a row's runs
+// (~70 us a sweep).  k_lego_edges (per cell) forms the two edge tests of the
+// BFS (:355-372) and zeroes the per-root statistics; k_lego_cc links every
+// horizontal run to its first cell with a wavefront prefix max (one
+// wavefront per row), unites the vertical and the column-wrap edges with LDS
+// atomics (linking the larger root below the smaller, path halving), then
+// counts the component sizes in the roots' own entries and sets the row bits
+// of the components under 30 cells (the only ones lego_feasible reads them
+// for).  Same roots (each component's first row-major cell), sizes and row
+// sets as the global kernels, so every later kernel is unchanged.
+#ifdef SLIO_FE_STAMP
+__device__ unsigned long long g_ccstamp[8];
+#define CCSTAMP(k)                                                             \
+  do {                                                                         \
+    if (threadIdx.x == 0) g_ccstamp[k] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define CCSTAMP(k) \
+  do {             \
+  } while (0)
+#endif
+constexpr int kLegoCcThreads = 1024;
+constexpr int kLegoCcCells = 31 * 1024;  // 5 B of LDS a cell: 155 KB
+__global__ __launch_bounds__(256) void k_lego_edges(LGeo g, const int32_t* __restrict__ owner,
+                                                    const int8_t* __restrict__ ground,
+                                                    const float* __restrict__ range_mat,
+                                                    uint8_t* __restrict__ edges, int32_t* __restrict__ csize,
+                                                    unsigned long long* __restrict__ rows) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.cells) return;
+  csize[c] = 0;
+  rows[2 * c] = 0ull;
+  rows[2 * c + 1] = 0ull;
+  auto valid = [&](int64_t k) { return owner[k] >= 0 && ground[k] != 1; };
+  uint8_t e = 0;
+  if (valid(c)) {
+    e = 4;
+    const int row = (int)(c / g.H), col = (int)(c - (int64_t)row * g.H);
+    const float rc = range_mat[c];
+    const int64_t cr = (col + 1 < g.H ? col + 1 : 0) + (int64_t)row * g.H;
+    if (cr != c && valid(cr) && lego_edge(g, rc, range_mat[cr], true)) e |= 1;
+    if (row + 1 < g.N && valid(c + g.H) && lego_edge(g, rc, range_mat[c + g.H], false)) e |= 2;
+  }
+  edges[c] = e;
+}
+
+__device__ __forceinline__ int lds_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int cc_find(int* par, int x) {
+  int p = lds_ld(par + x);
+  while (p != x) {
+    const int gp = lds_ld(par + p);
+    if (gp != p) __hip_atomic_store(par + x, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // halving
+    x = p;
+    p = gp;
+  }
+  return x;
+}
+__device__ __forceinline__ void cc_unite(int* par, int a, int b) {
+  while (true) {
+    a = cc_find(par, a);
+    b = cc_find(par, b);
+    if (a == b) return;
+    if (a > b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    const int old = atomicCAS(par + b, b, a);  // link the larger root below the smaller
+    if (old == b) return;
+    b = old;
+  }
+}
+
+__global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_t* __restrict__ edges,
+                                                            int32_t* __restrict__ parent,
+                                                            int32_t* __restrict__ csize,
+                                                            unsigned long long* __restrict__ rows) {
+  extern __shared__ int par[];  // cells, then the edge flags (cells bytes)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int C = (int)g.cells;
+  uint8_t* edg = reinterpret_cast<uint8_t*>(par + C);
+  CCSTAMP(0);
+  constexpr int kPer = (kLegoCcCells + kLegoCcThreads - 1) / kLegoCcThreads;
+  // the edge flags into LDS first, every load in flight at once (the phases
+  // below read them in dependent loops: from global memory each step paid
+  // a round trip, ~50 us a sweep)
+  {
+    uint8_t ev[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int c = t + i * kLegoCcThreads;
+      ev[i] = c < C ? edges[c] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int c = t + i * kLegoCcThreads;
+      if (c < C) edg[c] = ev[i];
+    }
+  }
+  __syncthreads();
+  CCSTAMP(1);
+  // horizontal runs: a valid cell with no edge from its left neighbour
+  // starts a run; every cell of a run points at the run's first cell
+  for (int r = w; r < g.N; r += kLegoCcThreads / 64) {
+    int carry = -1;
+    const int rb = r * g.H;
+    for (int b0 = 0; b0 < g.H; b0 += 64) {
+      const int col = b0 + lane;
+      const int e = col < g.H ? edg[rb + col] : 0;
+      const bool from_left = col > 0 && col < g.H && (edg[rb + col - 1] & 1);
+      int v = ((e & 4) && !from_left) ? rb + col : -1;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v = max(v, u);
+      }
+      v = max(v, carry);
+      if (col < g.H) par[rb + col] = (e & 4) ? v : -1;
+      carry = __shfl(v, 63, 64);
+    }
+  }
+  __syncthreads();
+  CCSTAMP(2);
+  // vertical edges and the column wrap (col H - 1 -> 0)
+  for (int c = t; c < C; c += kLegoCcThreads) {
+    const int e = edg[c];
+    const int col = c % g.H;
+    if (e & 2) cc_unite(par, c, c + g.H);
+    if ((e & 1) && col == g.H - 1) cc_unite(par, c, c - (g.H - 1));
+  }
+  __syncthreads();
+  CCSTAMP(3);
+  // roots of every cell (registers: the entries are rewritten below)
+  int root[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int c = t + i * kLegoCcThreads;
+    root[i] = (c < C && lds_ld(par + c) >= 0) ? cc_find(par, c) : -1;
+  }
+  __syncthreads();
+  CCSTAMP(4);
+  // sizes: a root's entry becomes -(size + 1) (<= -2; -1 stays "no label")
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int c = t + i * kLegoCcThreads;
+    if (c < C) {
+      parent[c] = root[i];
+      if (root[i] == c) par[c] = -2;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int c = t + i * kLegoCcThreads;
+    if (c < C && root[i] >= 0 && root[i] != c) atomicSub(par + root[i], 1);
+  }
+  __syncthreads();
+  CCSTAMP(5);
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int c = t + i * kLegoCcThreads;
+    if (c >= C || root[i] < 0) continue;
+    const int sz = -lds_ld(par + root[i]) - 1;
+    if (root[i] == c) csize[c] = sz;
+    // lineCountFlag: every pushed cell's row (not the seed's, :373)
+    if (root[i] != c && sz < 30) {
+      const int row = c / g.H;
+      atomicOr(&rows[2 * (int64_t)root[i] + (row >> 6)], 1ull << (row & 63));
+    }
+  }
+  CCSTAMP(6);
 }
 
 __device__ __forceinline__ bool lego_feasible(const LGeo& g, const int32_t* csize,
@@ -1986,10 +2228,10 @@ __device__ ImuCur imu_at(const LegoImuDev& m, float pointTime) {
   int f = m.last_it;
   while (f != m.last) {
     if (tq < m.time[f]) break;
-    f = (f + 1) % m.Q;
+    f = f + 1 == m.Q ? 0 : f + 1;  // (f + 1) % Q without the division
   }
   c.f = f;
-  c.b = (f + m.Q - 1) % m.Q;
+  c.b = f == 0 ? m.Q - 1 : f - 1;
   c.after = tq > m.time[f];
   c.rf = c.rb = 0.f;
   if (c.after) {
@@ -2208,6 +2450,12 @@ __global__ __launch_bounds__(256) void k_lego_concat(int n_scan, const int32_t* 
 
 using namespace slio::lego;
 
+#ifdef SLIO_FE_STAMP
+extern "C" int slio_dbg_cc_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ccstamp), sizeof(g_ccstamp)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 struct slio_lego {
   slio_lego_params prm{};
   LGeo g{};
@@ -2222,12 +2470,14 @@ struct slio_lego {
   int que = 0;
   LegoImuDev imu{};
   int imu_last_host = 0;
+  bool cc_global = false;  // labelComponents by k_lego_union / k_lego_compress
   // image / segmentation
   int32_t* owner = nullptr;
   float* range_mat = nullptr;
   float4* full = nullptr;
   int8_t* ground = nullptr;
   int32_t* parent = nullptr;
+  uint8_t* edges = nullptr;
   int32_t* csize = nullptr;
   unsigned long long* rows = nullptr;
   int32_t* cnt = nullptr;
@@ -2281,7 +2531,7 @@ void lego_free(slio_lego* h) {
     (void)hipEventDestroy(p.second);
   }
   void* dev[] = {h->x, h->y, h->z, h->itime, h->iarr, h->owner, h->range_mat, h->full, h->ground,
-                 h->parent, h->csize, h->rows, h->cnt, h->rootlab, h->label, h->start_ring,
+                 h->parent, h->edges, h->csize, h->rows, h->cnt, h->rootlab, h->label, h->start_ring,
                  h->end_ring, h->col_ind, h->nseg, h->gflag, h->srange, h->sxyzi, h->outlier,
                  h->slot, h->desk, h->io, h->curvature, h->picked0, h->flabel, h->corner_stage,
                  h->corner_sharp, h->corner_count, h->sharp_count, h->flat_count, h->surf_count,
@@ -2371,6 +2621,7 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   A(h->full, 16 * C);
   A(h->ground, C);
   A(h->parent, 4 * C);
+  A(h->edges, C);
   A(h->csize, 4 * C);
   A(h->rows, 16 * C);
   A(h->cnt, 12 * R);
@@ -2435,6 +2686,15 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
     return SLIO_ENOMEM;
   }
   feat_set_smem<kModeLego>(fsm, sort_items(h->fc.sort_cap), vox_items(h->fc.vox_cap));
+  // labelComponents in LDS when the image fits (SLIO_LEGO_CC_GLOBAL=1: the
+  // global-atomic kernels, for A/B and tests)
+  {
+    const char* cg = std::getenv("SLIO_LEGO_CC_GLOBAL");
+    h->cc_global = cg && cg[0] && cg[0] != '0';
+  }
+  if (h->cells <= kLegoCcCells)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lego_cc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(5 * h->cells));
   *out = h;
   return SLIO_OK;
 }
@@ -2538,17 +2798,24 @@ int slio_lego_run_async(slio_lego_handle h) {
   const LGeo& g = h->g;
   const int R = g.N;
   const unsigned cb = (unsigned)((g.cells + 255) / 256);
+  const bool cc_lds = g.cells <= kLegoCcCells && !h->cc_global;
   LIO_HIP(hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream));
-  LIO_HIP(hipMemsetAsync(h->ground, 0, g.cells, h->stream));
-  LIO_HIP(hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream));
-  LIO_HIP(hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream));
+  if (!cc_lds) {
+    LIO_HIP(hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream));
+    LIO_HIP(hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream));
+  }
   if (h->n > 0)
     k_lego_claim<<<(unsigned)((h->n + 255) / 256), 256, 0, h->stream>>>(h->x, h->y, h->z, h->n, g,
                                                                           h->owner);
-  k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, h->owner, h->range_mat, h->full);
-  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, h->owner, h->full, h->ground, h->parent);
-  k_lego_union<<<cb, 256, 0, h->stream>>>(g, h->range_mat, h->parent);
-  k_lego_compress<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows);
+  k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, h->owner, h->range_mat, h->full, h->ground);
+  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, h->owner, h->full, h->ground, h->parent, !cc_lds);
+  if (cc_lds) {
+    k_lego_edges<<<cb, 256, 0, h->stream>>>(g, h->owner, h->ground, h->range_mat, h->edges, h->csize, h->rows);
+    k_lego_cc<<<1, kLegoCcThreads, 5 * g.cells, h->stream>>>(g, h->edges, h->parent, h->csize, h->rows);
+  } else {
+    k_lego_union<<<cb, 256, 0, h->stream>>>(g, h->range_mat, h->parent);
+    k_lego_compress<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows);
+  }
   k_lego_rowcount<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
                                                         h->cnt);
   const LegoSeg sg{h->start_ring, h->end_ring, h->col_ind, h->gflag, h->srange, h->sxyzi,

@@ -94,7 +94,7 @@ def chain(n_map, n_raw, frames_n=8):
     from agi_lidar_slam_amd.mapping import LaserMapping
     import test_gpu_chain as TC
     seed = 20261015
-    mp, _ = synth.make_problem(n_map, n_raw, cache_dir="/tmp/slio_cache")
+    mp, _ = synth.make_problem(n_map, 100000, cache_dir="/tmp/slio_cache")
     seq = TC.make_sequence(seed, n_map, frames_n, n_raw, 0.5)
     lib = L.load()
     lm = LaserMapping(filter_size_map_min=0.5, cube_len=1000.0, maximum_iter=4, max_points=n_raw)
@@ -199,7 +199,7 @@ if __name__ == "__main__":
     if "mapping" in what:
         mapping(10_000_000, 100_000)
     if "chain" in what:
-        chain(10_000_000, int(os.environ.get("CHAIN_RAW", "200000")))
+        chain(10_000_000, int(os.environ.get("CHAIN_RAW", "100000")))
     if "preproc" in what:
         preproc(200_000)
     if "s2m" in what:

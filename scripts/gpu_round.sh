@@ -53,12 +53,27 @@ for step in "$@"; do
         SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_noreuse.so timeout -k 10 300 python scripts/ab_inproc.py - --rounds 5 | sed "s/^/noreuse /" || exit 7
       done > gpurun_out/${tag}_ab3.log 2>&1
       cat gpurun_out/${tag}_ab3.log ;;
+    abenv)
+      # in-process A/B of environment switches of this library: ABENV="SLIO_X=1 SLIO_Y=1"
+      timeout -k 10 400 python scripts/ab_inproc.py - $ABENV --rounds 7 > gpurun_out/${tag}_abenv.log 2>&1 || { tail gpurun_out/${tag}_abenv.log; exit 7; }
+      cat gpurun_out/${tag}_abenv.log ;;
+    tailenv)
+      # tail stamps with and without the environment switch TAILENV (e.g. SLIO_NO_INTERLEAVE=1)
+      SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so timeout -k 10 200 python scripts/tail_stamps.py > gpurun_out/${tag}_tail.log 2>&1 || exit 8
+      env $TAILENV SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so timeout -k 10 200 python scripts/tail_stamps.py > gpurun_out/${tag}_tail_env.log 2>&1 || exit 8
+      grep "per pass" gpurun_out/${tag}_tail.log gpurun_out/${tag}_tail_env.log ;;
     tail)
       SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so timeout -k 10 200 python scripts/tail_stamps.py > gpurun_out/${tag}_tail.log 2>&1 || { tail gpurun_out/${tag}_tail.log; exit 8; }
       grep maxit gpurun_out/${tag}_tail.log ;;
     chain)
       timeout -k 10 600 python scripts/bench_aux.py chain > gpurun_out/${tag}_chain.jsonl 2> gpurun_out/${tag}_chain.err || { echo "chain failed"; tail -20 gpurun_out/${tag}_chain.err; exit 9; }
       cut -c1-1500 gpurun_out/${tag}_chain.jsonl ;;
+    profchain)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profchain -o run --output-format csv -- python3 scripts/bench_aux.py chain > gpurun_out/${tag}_profchain.log 2>&1 || { echo "profchain failed"; tail -20 gpurun_out/${tag}_profchain.log; exit 5; }
+      for f in $(find gpurun_out/${tag}_profchain -name "*kernel_stats.csv"); do head -30 $f | cut -c1-150; done ;;
+    festamps)
+      SLIO_LIB=agi_lidar_slam_amd/_abl/libslio_fe.so timeout -k 10 200 python scripts/fe_stamps.py > gpurun_out/${tag}_festamps.log 2>&1 || { tail gpurun_out/${tag}_festamps.log; exit 8; }
+      grep -v amdgpu.ids gpurun_out/${tag}_festamps.log ;;
     mapping)
       timeout -k 10 600 python scripts/bench_aux.py mapping > gpurun_out/${tag}_mapping.jsonl 2> gpurun_out/${tag}_mapping.err || { echo "mapping failed"; tail -20 gpurun_out/${tag}_mapping.err; exit 9; }
       cut -c1-1500 gpurun_out/${tag}_mapping.jsonl ;;

@@ -73,8 +73,12 @@ def check_features(oracle_mod, fe, si, P, imu=None, t0=0.0):
     return got
 
 
-@pytest.mark.parametrize("with_imu", [False, True])
-def test_vlp16_sweep_bitexact(oracle_mod, with_imu):
+@pytest.mark.parametrize("with_imu,cc", [(False, "lds"), (True, "lds"), (False, "global")])
+def test_vlp16_sweep_bitexact(oracle_mod, with_imu, cc, monkeypatch):
+    """cc: labelComponents by the one-workgroup LDS union-find (k_lego_cc, the
+    default when the image fits) or the global-atomic kernels."""
+    if cc == "global":
+        monkeypatch.setenv("SLIO_LEGO_CC_GLOBAL", "1")
     from agi_lidar_slam_amd import synth
     from agi_lidar_slam_amd.lego import LegoImu, LegoParams
     P = LegoParams()
