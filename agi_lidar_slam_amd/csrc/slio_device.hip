@@ -1745,20 +1745,27 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
       }
       SSTAMP(10);
       if (ok) {
-        // dx = G y - dx_new, |dx| > epsi (esekfom.hpp:17, 325-331); lanes
-        // 32 / 33 form their rotation's 3 components themselves
+        // dx = G y - dx_new, |dx| > epsi (esekfom.hpp:17, 325-331): lane q < 24
+        // forms component q (one dot product, its D LDS reads in flight); the
+        // rotation lanes 32 / 33 take their 3 components from lanes 3..5 / 6..8
         const int lane = t;
-        const int q0 = lane < 24 ? lane : (lane == 32 ? 3 : (lane == 33 ? 6 : 0));
         const int nq = lane < 24 ? 1 : ((lane == 32 || lane == 33) ? 3 : 0);
         double dq[3] = {0.0, 0.0, 0.0};
+        {
+          const int q = lane < 24 ? lane : 0;
+          double s2 = 0.0;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          if (c < nq) {
-            const int q = q0 + c;
-            double s2 = 0.0;
-#pragma unroll
-            for (int k = 0; k < D; ++k) s2 = fma(L.G[q * D + k], y[k], s2);
-            dq[c] = s2 - L.dxn[q];
+          for (int k = 0; k < D; ++k) s2 = fma(L.G[q * D + k], y[k], s2);
+          dq[0] = s2 - L.dxn[q];
+        }
+        {
+          const int base = lane == 33 ? 6 : 3;  // (every lane shuffles; 32 / 33 keep theirs)
+          const double r0 = __shfl(dq[0], base, 64), r1 = __shfl(dq[0], base + 1, 64),
+                       r2 = __shfl(dq[0], base + 2, 64);
+          if (lane == 32 || lane == 33) {
+            dq[0] = r0;
+            dq[1] = r1;
+            dq[2] = r2;
           }
         }
         big = __ballot(lane < 24 && fabs(dq[0]) > 0.001) != 0;

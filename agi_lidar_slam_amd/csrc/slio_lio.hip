@@ -1952,33 +1952,50 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
   __syncthreads();
   CCSTAMP(1);
   // horizontal runs: a valid cell with no edge from its left neighbour
-  // starts a run; every cell of a run points at the run's first cell
+  // starts a run; every cell of a run points at the run's first cell.  A
+  // wavefront per row, each lane a contiguous segment of it: the segment's
+  // last run start, a prefix max over the lanes, then the segment's cells
+  // (a 64-cell chunk per step with a cross-lane carry was a chain of ~8
+  // dependent shuffles per step: 12 us)
   for (int r = w; r < g.N; r += kLegoCcThreads / 64) {
-    int carry = -1;
     const int rb = r * g.H;
-    for (int b0 = 0; b0 < g.H; b0 += 64) {
-      const int col = b0 + lane;
-      const int e = col < g.H ? edg[rb + col] : 0;
-      const bool from_left = col > 0 && col < g.H && (edg[rb + col - 1] & 1);
-      int v = ((e & 4) && !from_left) ? rb + col : -1;
+    const int seg = (g.H + 63) / 64;
+    const int c0 = min(lane * seg, g.H), c1 = min(c0 + seg, g.H);
+    auto starts_run = [&](int col) {
+      const int e = edg[rb + col];
+      return (e & 4) && !(col > 0 && (edg[rb + col - 1] & 1));
+    };
+    int last = -1;
+    for (int col = c0; col < c1; ++col)
+      if (starts_run(col)) last = rb + col;
+    int v = last;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(v, o, 64);
-        if (lane >= o) v = max(v, u);
-      }
-      v = max(v, carry);
-      if (col < g.H) par[rb + col] = (e & 4) ? v : -1;
-      carry = __shfl(v, 63, 64);
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o, 64);
+      if (lane >= o) v = max(v, u);
+    }
+    int cur = __shfl_up(v, 1, 64);  // the last run start before this segment
+    if (lane == 0) cur = -1;
+    for (int col = c0; col < c1; ++col) {
+      const int e = edg[rb + col];
+      if (starts_run(col)) cur = rb + col;
+      par[rb + col] = (e & 4) ? cur : -1;
     }
   }
   __syncthreads();
   CCSTAMP(2);
-  // vertical edges and the column wrap (col H - 1 -> 0)
-  for (int c = t; c < C; c += kLegoCcThreads) {
-    const int e = edg[c];
-    const int col = c % g.H;
-    if (e & 2) cc_unite(par, c, c + g.H);
-    if ((e & 1) && col == g.H - 1) cc_unite(par, c, c - (g.H - 1));
+  // vertical edges and the column wrap (col H - 1 -> 0).  A vertical edge
+  // whose left neighbours are linked the same way (both cells continue a run
+  // and the edge to the left exists) adds nothing: only the first of each
+  // stretch of parallel edges is united.
+  for (int r = 0; r < g.N; ++r) {
+    const int rb = r * g.H;
+    for (int col = t; col < g.H; col += kLegoCcThreads) {
+      const int c = rb + col;
+      const int e = edg[c];
+      if ((e & 2) && !(col > 0 && (edg[c - 1] & 3) == 3 && (edg[c + g.H - 1] & 1))) cc_unite(par, c, c + g.H);
+      if ((e & 1) && col == g.H - 1) cc_unite(par, c, c - (g.H - 1));
+    }
   }
   __syncthreads();
   CCSTAMP(3);
@@ -1991,20 +2008,28 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
   }
   __syncthreads();
   CCSTAMP(4);
-  // sizes: a root's entry becomes -(size + 1) (<= -2; -1 stays "no label")
+  // sizes: a root's entry becomes -(size + 1) (<= -2; -1 stays "no label"):
+  // it starts at -1 and every cell of the component subtracts 1, one atomic
+  // per stretch of lanes (consecutive cells) with the same root
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
     const int c = t + i * kLegoCcThreads;
     if (c < C) {
       parent[c] = root[i];
-      if (root[i] == c) par[c] = -2;
+      if (root[i] == c) par[c] = -1;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
-    const int c = t + i * kLegoCcThreads;
-    if (c < C && root[i] >= 0 && root[i] != c) atomicSub(par + root[i], 1);
+    const int r = root[i];
+    const int prev = __shfl_up(r, 1, 64);
+    const uint64_t heads = __ballot(lane == 0 || prev != r);
+    if (r >= 0 && (lane == 0 || prev != r)) {
+      const uint64_t after = heads & ~((2ull << lane) - 1ull);  // (lane 63: 2 << 63 wraps to 0)
+      const int end = after ? __ffsll((unsigned long long)after) - 1 : 64;
+      atomicSub(par + r, end - lane);
+    }
   }
   __syncthreads();
   CCSTAMP(5);
