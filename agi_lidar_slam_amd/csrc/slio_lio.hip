@@ -1745,12 +1745,13 @@ __global__ __launch_bounds__(256) void k_lego_ground(LGeo g, const int32_t* __re
       f[i] = (i <= g.gsi && own[i] >= 0) ? full[j + (int64_t)i * g.H] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < kLegoGroundRows; ++i) {
-      if (i >= g.gsi) break;
-      if (own[i] < 0 || own[i + 1] < 0) {
-        gr[i] = -1;
-      } else if (ground_test(f[i], f[i + 1])) {
-        gr[i] = 1;
-        gr[i + 1] = 1;
+      if (i < g.gsi) {
+        if (own[i] < 0 || own[i + 1] < 0) {
+          gr[i] = -1;
+        } else if (ground_test(f[i], f[i + 1])) {
+          gr[i] = 1;
+          gr[i + 1] = 1;
+        }
       }
     }
 #pragma unroll
