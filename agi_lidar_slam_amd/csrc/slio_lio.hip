@@ -1871,6 +1871,7 @@ __device__ unsigned long long g_ccstamp[8];
   } while (0)
 #endif
 constexpr int kLegoCcThreads = 1024;
+constexpr int kLegoCcSeg = 32;           // row cells per lane held in registers (rows <= 2048 cells)
 constexpr int kLegoCcCells = 31 * 1024;  // 5 B of LDS a cell: 155 KB
 __global__ __launch_bounds__(256) void k_lego_edges(LGeo g, const int32_t* __restrict__ owner,
                                                     const int8_t* __restrict__ ground,
@@ -1962,6 +1963,35 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
     const int rb = r * g.H;
     const int seg = (g.H + 63) / 64;
     const int c0 = min(lane * seg, g.H), c1 = min(c0 + seg, g.H);
+    if (seg <= kLegoCcSeg) {
+      // the segment's flags (and its left neighbour's) in registers, every
+      // LDS read in flight at once
+      uint8_t eb[kLegoCcSeg + 1];
+#pragma unroll
+      for (int k = 0; k <= kLegoCcSeg; ++k) {
+        const int col = c0 - 1 + k;
+        eb[k] = (col >= 0 && col < c1) ? edg[rb + col] : 0;
+      }
+      int last = -1;
+#pragma unroll
+      for (int k = 1; k <= kLegoCcSeg; ++k)
+        if ((eb[k] & 4) && !(eb[k - 1] & 1)) last = rb + c0 - 1 + k;
+      int v = last;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v = max(v, u);
+      }
+      int cur = __shfl_up(v, 1, 64);  // the last run start before this segment
+      if (lane == 0) cur = -1;
+#pragma unroll
+      for (int k = 1; k <= kLegoCcSeg; ++k) {
+        const int col = c0 - 1 + k;
+        if ((eb[k] & 4) && !(eb[k - 1] & 1)) cur = rb + col;
+        if (col < c1) par[rb + col] = (eb[k] & 4) ? cur : -1;
+      }
+      continue;
+    }
     auto starts_run = [&](int col) {
       const int e = edg[rb + col];
       return (e & 4) && !(col > 0 && (edg[rb + col - 1] & 1));
@@ -1975,7 +2005,7 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
       const int u = __shfl_up(v, o, 64);
       if (lane >= o) v = max(v, u);
     }
-    int cur = __shfl_up(v, 1, 64);  // the last run start before this segment
+    int cur = __shfl_up(v, 1, 64);
     if (lane == 0) cur = -1;
     for (int col = c0; col < c1; ++col) {
       const int e = edg[rb + col];
@@ -1989,13 +2019,32 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
   // whose left neighbours are linked the same way (both cells continue a run
   // and the edge to the left exists) adds nothing: only the first of each
   // stretch of parallel edges is united.
-  for (int r = 0; r < g.N; ++r) {
-    const int rb = r * g.H;
-    for (int col = t; col < g.H; col += kLegoCcThreads) {
-      const int c = rb + col;
-      const int e = edg[c];
-      if ((e & 2) && !(col > 0 && (edg[c - 1] & 3) == 3 && (edg[c + g.H - 1] & 1))) cc_unite(par, c, c + g.H);
-      if ((e & 1) && col == g.H - 1) cc_unite(par, c, c - (g.H - 1));
+  // (the thread's cells' tests first, every LDS read in flight, then the
+  // unions: each one a chain of dependent LDS reads)
+  {
+    uint64_t need = 0;  // bit 2i: vertical union of cell i, 2i + 1: wrap union
+    int col = t % g.H;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int c = t + i * kLegoCcThreads;
+      if (c < C) {
+        const int e = edg[c];
+        const bool vert = (e & 2) && !(col > 0 && (edg[c - 1] & 3) == 3 && (edg[c + g.H - 1] & 1));
+        const bool wrap = (e & 1) && col == g.H - 1;
+        need |= (vert ? 1ull : 0ull) << (2 * i);
+        need |= (wrap ? 2ull : 0ull) << (2 * i);
+      }
+      col += kLegoCcThreads;
+      while (col >= g.H) col -= g.H;
+    }
+    static_assert(2 * kPer <= 64, "need bits");
+    for (uint64_t m = need; m; m &= m - 1) {
+      const int b = __ffsll((unsigned long long)m) - 1, i = b >> 1;
+      const int c = t + i * kLegoCcThreads;
+      if (b & 1)
+        cc_unite(par, c, c - (g.H - 1));
+      else
+        cc_unite(par, c, c + g.H);
     }
   }
   __syncthreads();
@@ -2348,12 +2397,9 @@ __global__ __launch_bounds__(256) void k_lego_deskew(const float4* seg, const in
     st[3] = c0.vx;
     st[4] = c0.vy;
     st[5] = c0.vz;
-    st[6] = fcos(c0.r);
-    st[7] = fcos(c0.p);
-    st[8] = fcos(c0.y);
-    st[9] = fsin(c0.r);
-    st[10] = fsin(c0.p);
-    st[11] = fsin(c0.y);
+    fsincos(c0.r, st[9], st[6]);
+    fsincos(c0.p, st[10], st[7]);
+    fsincos(c0.y, st[11], st[8]);
     if (blockIdx.x == 0) {
       float a[3];
       if (c0.after) {
@@ -2409,16 +2455,22 @@ __global__ __launch_bounds__(256) void k_lego_deskew(const float4* seg, const in
         io->velo_from_start[1] = -sRs * x2 + cRs * y2;
         io->velo_from_start[2] = z2;
       }
-      // TransformToStartIMU (:429-458); imuShiftFromStartCur is 0
-      const float x1 = fcos(c.r) * px - fsin(c.r) * py;
-      const float y1 = fsin(c.r) * px + fcos(c.r) * py;
+      // TransformToStartIMU (:429-458); imuShiftFromStartCur is 0.  One
+      // double sincos per angle (six separate sin / cos calls were most of
+      // the kernel's time)
+      float sr, cr, sp_, cp, sy, cy;
+      fsincos(c.r, sr, cr);
+      fsincos(c.p, sp_, cp);
+      fsincos(c.y, sy, cy);
+      const float x1 = cr * px - sr * py;
+      const float y1 = sr * px + cr * py;
       const float z1 = pz;
       const float x2 = x1;
-      const float y2 = fcos(c.p) * y1 - fsin(c.p) * z1;
-      const float z2 = fsin(c.p) * y1 + fcos(c.p) * z1;
-      const float x3 = fcos(c.y) * x2 + fsin(c.y) * z2;
+      const float y2 = cp * y1 - sp_ * z1;
+      const float z2 = sp_ * y1 + cp * z1;
+      const float x3 = cy * x2 + sy * z2;
       const float y3 = y2;
-      const float z3 = -fsin(c.y) * x2 + fcos(c.y) * z2;
+      const float z3 = -sy * x2 + cy * z2;
       const float x4 = cYs * x3 - sYs * z3;
       const float y4 = y3;
       const float z4 = sYs * x3 + cYs * z3;
