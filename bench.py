@@ -103,6 +103,22 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def frontend_traffic(workload):
+    """HBM bytes of one feature-stage pass (k_fe_pick + k_fe_ring) from the
+    committed PMC summary (scripts/pmc_frontend.sh: rocprofv3 --pmc cannot run
+    inside this process), only when the library was built from the same
+    sources."""
+    path = os.path.join(ROOT, "profiles", f"{workload}_traffic.json")
+    try:
+        tj = json.load(open(path))
+        from agi_lidar_slam_amd import build
+        if tj.get("workload") == workload and tj.get("source_hash") == build.source_hash():
+            return tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def bench_c3(args, rank, world, dev, dist):
     """C3: LIO-SAM imageProjection + featureExtraction on a
     64 x 2048 Ouster scan (131 072 points).  One step = one scan through the
@@ -229,7 +245,7 @@ def bench_c3(args, rank, world, dev, dist):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": None,
+            "traffic": frontend_traffic("c3") if S == 1 else None,
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_us": avg_s * 1e6,
             "launches": int(nl.value),
@@ -357,7 +373,7 @@ def bench_lego(args, rank, world, dev, dist):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": None,
+            "traffic": frontend_traffic("lego"),
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_us": avg_s * 1e6,
             "launches": int(nl.value),

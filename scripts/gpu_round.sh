@@ -97,5 +97,8 @@ for step in "$@"; do
       grep -v amdgpu.ids gpurun_out/${tag}_ustamps.log ;;
     pmc)
       bash scripts/pmc_search.sh ${tag} || exit $? ;;
+    pmcfe)
+      bash scripts/pmc_frontend.sh ${tag} || exit $?
+      cat gpurun_out/${tag}_c3_traffic.json gpurun_out/${tag}_lego_traffic.json | cut -c1-400 ;;
   esac
 done

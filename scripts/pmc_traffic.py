@@ -12,28 +12,47 @@ from collections import defaultdict
 
 
 def main(out_json, *dirs):
-    vals = defaultdict(list)
+    """PMC_KERNELS (comma list of kernel-name substrings, default k_search_pass):
+    the per-launch means of every listed kernel are summed, i.e. the traffic of
+    one launch of each (the C3 / LeGO feature stage is k_fe_pick + k_fe_ring).
+    PMC_WORKLOAD names the workload the summary belongs to (bench.py checks it)."""
+    import os
+    kernels = os.environ.get("PMC_KERNELS", "k_search_pass").split(",")
+    workload = os.environ.get("PMC_WORKLOAD", "c2")
+    vals = defaultdict(lambda: defaultdict(list))
     for d in dirs:
         for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
-                if "k_search_pass" in r.get("Kernel_Name", ""):
-                    vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    mean = {k: sum(v) / len(v) for k, v in vals.items()}
+                for k in kernels:
+                    if k in r.get("Kernel_Name", ""):
+                        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    per_kernel = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+    mean = defaultdict(float)
+    for cs in per_kernel.values():
+        for c, v in cs.items():
+            mean[c] += v
+    mean = dict(mean)
     fetch = mean.get("FETCH_SIZE")
     write = mean.get("WRITE_SIZE")
-    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from agi_lidar_slam_amd import build
     res = {
-        "kernel": "k_search_pass",
+        "kernel": " + ".join(kernels),
+        "workload": workload,
         # bench.py attaches hbm_bytes_per_launch only to runs of the library
         # built from these sources
         "source_hash": build.source_hash(),
-        "map_points": 10_000_000,
-        "scan_points": 100_000,
         "counters_mean_per_launch": mean,
+        "counters_per_kernel": per_kernel,
         "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
         "note": "2*FETCH_SIZE+WRITE_SIZE (KiB) per launch, gfx950 FETCH_SIZE halving corrected",
     }
+    if workload == "c2":
+        res["map_points"] = 10_000_000
+        res["scan_points"] = 100_000
+    else:
+        res["note"] += ("; the feature kernels read mostly 4-B words, a width the halving rule is not "
+                        "calibrated for (MI355X_MICROARCH.md): 2*FETCH+WRITE is an upper estimate")
     if "TCC_HIT_sum" in mean and "TCC_MISS_sum" in mean:
         res["l2_hit_rate"] = mean["TCC_HIT_sum"] / (mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"])
     json.dump(res, open(out_json, "w"), indent=1)

@@ -1,0 +1,27 @@
+"""Time the LeGO-LOAM front-end on the VLP-16 sweep (inputs resident, IMU on)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
+
+L.load(os.environ.get("SLIO_LIB", L.LIB_PATH))
+from agi_lidar_slam_amd.lego import LegoFrontEnd, LegoImu, LegoParams  # noqa: E402
+
+reps = int(os.environ.get("REPS", "200"))
+sw = synth.make_vlp16_sweep()
+imu = LegoImu()
+imu.feed(sw["imu"], sw["time_scan_cur"] + 0.15)
+fe = LegoFrontEnd(LegoParams())
+fe.set_imu(imu, sw["time_scan_cur"])
+fe.upload(sw["x"], sw["y"], sw["z"])
+for _ in range(5):
+    fe.run()
+t0 = time.perf_counter()
+for _ in range(reps):
+    fe.lib.slio_lego_run_async(fe.h)
+c = fe.run()
+el = time.perf_counter() - t0
+print(f"{(reps + 1) / el:.1f} scans/s  {el / (reps + 1) * 1e6:.1f} us/scan")
+fe.close()
