@@ -49,6 +49,10 @@ def mapping(n_map, n_scan, frames_n=6):
         x = lm.kf.get_x()
         if k:
             x.pos = x.pos + (fr.gt_pos - frames[k - 1].gt_pos)
+            if os.environ.get("MAPPING_PRIOR") == "gtrot":
+                # diagnostic: the ground-truth rotation as well (the default
+                # prior carries the previous scan's rotation)
+                x.rot = fr.gt_rot.copy()
         lm.kf.change_x(x)
         lm.kf.change_P(np.eye(24) * 1e-2)
         body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
