@@ -226,6 +226,9 @@ SIGNATURES = {
     ),
     "slio_state_boxplus": (C.c_int, [C.POINTER(SlioState), _DP, C.POINTER(SlioState)]),
     "slio_state_boxminus": (C.c_int, [C.POINTER(SlioState), C.POINTER(SlioState), _DP]),
+    "slio_debug_reload_switches": (C.c_int, [_P]),
+    "slio_debug_host_stamps": (C.c_int, [_P, C.c_int, _I64P]),
+    "slio_debug_knn_cert": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
     # include/slio_frontend.h (LIO-SAM front-end)
     "slio_lio_params_default": (C.c_int, [C.POINTER(SlioLioParams)]),
     "slio_lio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioLioParams)]),
@@ -263,24 +266,28 @@ SIGNATURES = {
 _lib = None
 
 
-def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load libslio.so once and bind every declared signature."""
+def load() -> C.CDLL:
+    """Load the in-tree libslio.so once and bind every declared signature.
+    The library must carry the digest of the current sources (slio_build_id):
+    a stale or foreign build fails loudly.  (Diagnostic variants are bound by
+    scripts/variant.py, outside the product.)"""
     global _lib
     if _lib is not None:
         return _lib
-    override = os.environ.get("SLIO_LIB_OVERRIDE")  # diagnostic / A-B builds (scripts/build_abl.sh)
-    path = override or path
-    if not os.path.exists(path):
+    if not os.path.exists(LIB_PATH):
         raise RuntimeError(
-            f"{path} is missing: build it with `python -m agi_lidar_slam_amd.build` "
+            f"{LIB_PATH} is missing: build it with `python -m agi_lidar_slam_amd.build` "
             "(there is no CPU fallback for the device path)")
-    lib = C.CDLL(path)
+    lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        if override and not hasattr(lib, name):
-            continue  # an older build in an A/B run: entry points it predates stay unbound
         fn = getattr(lib, name)  # AttributeError if the library lacks a declared symbol
         fn.restype = res
         fn.argtypes = args
+    from . import build
+    got, want = lib.slio_build_id().decode(), build.source_hash()
+    if got != want:
+        raise RuntimeError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                           "rebuild with `python -m agi_lidar_slam_amd.build`")
     _lib = lib
     return lib
 

@@ -70,6 +70,9 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 constexpr int kBlock = 256;                      // threads per search workgroup
 constexpr int kDefaultLPQ = 2;                   // lanes per query (tuned on MI355X)
+#ifndef SLIO_KC_U
+#define SLIO_KC_U 2                              // the same, in a search that keeps 8 (kNN certificates)
+#endif
 #ifndef SLIO_SEARCH_U
 #define SLIO_SEARCH_U 3                          // candidate loads in flight per lane and step (A/B on MI355X, block rows: 3 < 4 < 2)
 #endif
@@ -737,6 +740,39 @@ __device__ __forceinline__ void top5_insert(Top5& t, uint64_t key) {
   t.k[0] = c[0] ? key : t.k[0];
 }
 
+// Sorted top-8 list with the smallest squared distance it has DROPPED (an
+// evicted entry or a rejected key): after a scan, every scanned candidate
+// outside the list lies at >= m.  The 6th-8th entries and m certify later
+// passes' searches (kNN certificate, k_search_pass): a query that has moved
+// by delta keeps its 5 nearest among these 8 while the 9th bound minus delta
+// stays beyond its new 5th distance.
+struct Top8 {
+  uint64_t k[8];
+  float m;
+};
+
+__device__ __forceinline__ void top8_clear(Top8& t) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t.k[j] = kInfKey;
+  t.m = __int_as_float(0x7f800000);
+}
+
+__device__ __forceinline__ void top8_insert(Top8& t, uint64_t key) {
+  // the element that leaves (or never enters) the list; an empty slot's key
+  // (all ones) reads as NaN, which fminf ignores
+  const uint64_t drop = key < t.k[7] ? t.k[7] : key;
+  t.m = fminf(t.m, __uint_as_float((uint32_t)(drop >> 32)));
+  bool c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = key < t.k[j];
+#pragma unroll
+  for (int j = 7; j > 0; --j) t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
+  t.k[0] = c[0] ? key : t.k[0];
+}
+
+__device__ __forceinline__ void list_insert(Top5& t, uint64_t key) { top5_insert(t, key); }
+__device__ __forceinline__ void list_insert(Top8& t, uint64_t key) { top8_insert(t, key); }
+
 __device__ __forceinline__ void consider(Top5& t, const float4 c, uint32_t pos, float qx, float qy,
                                          float qz) {
   const float ddx = qx - c.x, ddy = qy - c.y, ddz = qz - c.z;
@@ -760,6 +796,20 @@ __device__ __forceinline__ void merge_round_dpp(Top5& t) {
 #pragma unroll
   for (int j = 0; j < 5; ++j) top5_insert(t, ok[j]);
 }
+template <int CTRL>
+__device__ __forceinline__ void merge_round_dpp(Top8& t) {
+  uint64_t ok[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ok[j] = dpp64<CTRL>(t.k[j]);
+  const float om = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t.m), CTRL, 0xF, 0xF, false));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) top8_insert(t, ok[j]);
+  t.m = fminf(t.m, om);
+}
+
+// the 2-lane merge of a query pair's top-8 lists (both lanes end with the
+// merged list and the union's dropped minimum)
+__device__ __forceinline__ void group_merge2(Top8& t) { merge_round_dpp<0xB1>(t); }
 
 // butterfly merge of the LPQ per-lane lists of a query group (lanes of a
 // group are consecutive and aligned, and all active or all inactive).  Up to
@@ -1013,10 +1063,10 @@ __device__ __forceinline__ void scan_flat(const float4* __restrict__ pts, const 
 // The 3x3x3 block from the block rows: one contiguous range, so a flat
 // position is an address (no run lookup); keys carry the pts position (.w),
 // identical to the keys of the 9-run scan.  Same pipeline as scan_flat.
-template <int LPQ, int U>
+template <int LPQ, int U, class TL>
 __device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, uint32_t s,
                                                 uint32_t T, int sub, float qx, float qy, float qz,
-                                                Top5& t) {
+                                                TL& t) {
   uint32_t t0 = sub;
   if (t0 >= T) return;
   constexpr uint32_t kStep = U * LPQ;
@@ -1031,7 +1081,7 @@ __device__ __forceinline__ void scan_block_rows(const float4* __restrict__ blk, 
       const float ddx = qx - c[u].x, ddy = qy - c[u].y, ddz = qz - c[u].z;
       const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
       const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint64_t)__float_as_uint(c[u].w);
-      top5_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
+      list_insert(t, (tb + u * LPQ < T) ? key : kInfKey);
     }
   };
   for (;;) {
@@ -1185,6 +1235,14 @@ struct PassOut {
   uint32_t* far_ctr;   // [1]: deferred (far) queries of this pass, all chunks
   PoseDev* pose;       // the pass's pose (block 0), for nbr_settle
   uint32_t* chunk_cost;  // per chunk of the rank (relative index): candidates + refinement / far weights
+  // kNN certificates (device-resident passes after the first, see
+  // k_search_pass): per point the query of its last full search and the
+  // squared-distance bound G of every map point outside its 8 nearest; the
+  // 8 nearest positions; per chunk the update epoch the entries belong to
+  float4* kq;
+  uint4* kpos;          // n * 2: positions 0..3, 4..7
+  uint32_t* kepoch;     // per chunk (global index)
+  uint32_t* kc_count;   // [0] certified queries, [1] queries searched with a certificate written
 };
 
 // far_query_margin: squared distance from the query to the grid's bounding box
@@ -1210,6 +1268,7 @@ struct PassCfg {
   int knn_only;            // 1: neighbours only (nbr_*), no fit / rows / products
   int mfma;                // chunk sums on the matrix cores (chunk_products_mfma), else VALU
   const uint32_t* perm;    // block -> chunk order within each XCD's range (chunk_order), or null
+  uint32_t kc_epoch;       // kNN certificates of this update (0: off); see k_search_pass
 };
 
 // ---------------------------------------------------------------- far queries
@@ -2328,6 +2387,7 @@ struct FuseArgs {
 };
 constexpr int kSegCnt = 16;
 constexpr int kCountWords = kSegCnt + kNSeg;
+constexpr int kKcCount = 8;  // count[8..9]: certified / searched queries (slio_debug_knn_cert)
 
 // the segment row of chunk c (single rank) and its number of chunks
 __device__ __forceinline__ int seg_of_chunk(int64_t C, int64_t c, int64_t& lim) {
@@ -2458,6 +2518,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     return;
   const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
   constexpr int NT = search_block<LPQ>();
+  // kNN certificates (passes after the first of a device-resident update,
+  // 2 lanes per query, 3x3x3 block first): see the certificate below
+  constexpr bool KC = DEVPOSE && LPQ == 2 && !SPHERE;
   if (DEVPOSE) ikf_dx_new(cfg.ctl);
   constexpr int QPP = NT / LPQ;               // queries per kNN pass
   constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
@@ -2480,7 +2543,9 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     alignas(16) float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
     alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
     float nb_d5[SLIO_CHUNK];
-    float4 qw[SLIO_CHUNK];
+    float4 qw[SLIO_CHUNK];            // the query; .w: its certificate bound G (KC, -2: none written)
+    uint32_t kp3[SLIO_CHUNK][3];      // KC: positions of the 6th-8th nearest
+    uint32_t kc_n[2];                 // KC: certified queries, searched queries
     // deferred (far) queries of this chunk and the far workers' scratch
     int far_cnt, ref_cnt;
     uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
@@ -2540,11 +2605,16 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   const GridGeom g = map.g;
   const float4* __restrict__ pts = map.pts;
   const uint32_t* __restrict__ start = map.start;
+  // this chunk's certificates belong to this update (written by one of its
+  // earlier passes): a uniform load
+  bool cache_ok = false;
+  if constexpr (KC) cache_ok = cfg.kc_epoch != 0 && out.kepoch[chunk] == cfg.kc_epoch;
   if (tid == 0) STAMP(0);
   if (tid == 0) {
     far_cnt = 0;
     ref_cnt = 0;
     lds.s.cost = 0;
+    if (KC) lds.s.kc_n[0] = lds.s.kc_n[1] = 0;
     if (blockIdx.x == 0 && !cfg.knn_only) *out.pose = pose;
   }
   __syncthreads();
@@ -2556,6 +2626,14 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     const int64_t i = chunk * SLIO_CHUNK + slot;
     const bool live = i < scan.n;
     float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+    // KC: the point's certificate (earlier query + bound, and this lane's 4 of
+    // its 8 positions), loaded with the scan point: no dependent round trip
+    float4 ka = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+    uint4 kp = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (KC && cache_ok && live) {
+      ka = out.kq[i];
+      kp = out.kpos[2 * i + sub];
+    }
     if (live) {
       const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
       body_to_world(pose, bx, by, bz, qx, qy, qz);
@@ -2568,7 +2646,54 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     bool done = !finite;
     bool refine = false;   // exact 5x5x5 refinement wanted (lim = refine bound)
     float lim = 0.0f;
-    if (finite) {
+    // kNN certificate (KC).  A full search on the block rows keeps the 8
+    // nearest and the smallest squared distance it dropped (Top8), so every
+    // map point outside the 8 lies at squared distance >= G = min(dropped,
+    // b1^2) (b1: the block faces' bound) from that query, less a 2e-5
+    // relative margin for float rounding -- a bound on the TRUE squared
+    // distance.  A later pass of the same update, its query moved by
+    // delta <= |q - q_old|, evaluates the 8 at the new query; if
+    // (sqrt(G) - delta)^2 (1 - 1e-5) exceeds the new 5th squared distance,
+    // no point outside the 8 can enter the top 5 (its float distance is
+    // strictly larger), so the 5 smallest keys of the 8 ARE the exact search's
+    // result, tie order included (same keys).  Otherwise the query searches.
+    bool reused = false;
+    float kG = -1.0f;                      // this search's certificate bound (-1: none)
+    uint32_t kx5 = ~0u, kx6 = ~0u, kx7 = ~0u;  // its 6th-8th positions
+    if constexpr (KC) {
+      // (branch-free up to the gathers, so the certificate loads stay whole)
+      const double ex0 = (double)qx - (double)ka.x, ey0 = (double)qy - (double)ka.y,
+                   ez0 = (double)qz - (double)ka.z;
+      const double dl = sqrt(ex0 * ex0 + ey0 * ey0 + ez0 * ez0) * (1.0 + 1e-9) + 1e-9;
+      const double A = sqrt((double)fmaxf(ka.w, 0.0f)) - dl;
+      if (cache_ok && finite && ka.w > 0.0f) {
+        {
+          if (A > 0.0) {
+            // the pair's lanes take 4 of the 8 each, then merge (as a search)
+            const uint32_t ps[4] = {kp.x, kp.y, kp.z, kp.w};
+            float4 cc[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cc[j] = pts[ps[j] != ~0u ? ps[j] : 0u];
+            Top5 tr;
+            top5_clear(tr);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float ddx = qx - cc[j].x, ddy = qy - cc[j].y, ddz = qz - cc[j].z;
+              const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
+              top5_insert(tr, ps[j] != ~0u ? (((uint64_t)__float_as_uint(d) << 32) | (uint64_t)ps[j]) : kInfKey);
+            }
+            group_merge<2>(tr);
+            if (tr.k[4] != kInfKey &&
+                A * A * (1.0 - 1e-5) > (double)__uint_as_float((uint32_t)(tr.k[4] >> 32))) {
+              t = tr;
+              reused = true;
+              done = true;
+            }
+          }
+        }
+      }
+    }
+    if (finite && !reused) {
       cx = cell_coord(qx, g.ox, g.inv_h);
       cy = cell_coord(qy, g.oy, g.inv_h);
       cz = cell_coord(qz, g.oz, g.inv_h);
@@ -2591,17 +2716,35 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           if (b1 < b0 || (int64_t)b1 > map.nblk)
             printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
 #endif
-          scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+          if (KC && cfg.kc_epoch) {
+            Top8 t8;
+            top8_clear(t8);
+            // (2 loads in flight per set: the top-8 list takes the registers)
+            scan_block_rows<LPQ, SLIO_KC_U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t8);
+            group_merge2(t8);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) t.k[j] = t8.k[j];
+            kx5 = (uint32_t)t8.k[5];
+            kx6 = (uint32_t)t8.k[6];
+            kx7 = (uint32_t)t8.k[7];
+            kG = t8.m;
+          } else {
+            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+            group_merge<LPQ>(t);
+          }
           if (sub == 0 && out.chunk_cost) atomicAdd(&lds.s.cost, b1 - b0);
         } else {
           RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
           scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
+          group_merge<LPQ>(t);
         }
-        group_merge<LPQ>(t);
         bool covers;
         const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
         const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
         done = covers || (t.k[4] != kInfKey && b1 > 0.0f && d5 < (b1 * b1) * 0.99999f);
+        // the certificate bound: dropped block candidates and the block faces
+        // (+inf when the block covers the grid); none off the block rows
+        if (KC) kG = (done && kG >= 0.0f) ? fminf(kG, b1 * b1) * (1.0f - 2e-5f) : -1.0f;
         if (!done) {
           // (2) exact refinement (below): every cell of the 5x5x5 cube whose
           // conservative box gap is within the current 5th distance, minus
@@ -2703,7 +2846,20 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       // kNN gate (esekfom.hpp:144-147): 5 neighbours and d5 <= 5
       const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
       nb_d5[slot] = (t.k[4] != kInfKey) ? d5 : __int_as_float(0x7f800000);
-      qw[slot] = make_float4(qx, qy, qz, 0.0f);
+      // (KC: a certified query keeps the certificate it was certified by)
+      qw[slot] = make_float4(qx, qy, qz, KC ? (reused ? -2.0f : kG) : 0.0f);
+      if (KC) {
+        lds.s.kp3[slot][0] = kx5;
+        lds.s.kp3[slot][1] = kx6;
+        lds.s.kp3[slot][2] = kx7;
+      }
+    }
+    if constexpr (KC) {
+      const uint64_t br = __ballot(sub == 0 && live && reused), bs = __ballot(sub == 0 && live && !reused);
+      if ((tid & 63) == 0 && cfg.kc_epoch) {
+        atomicAdd(&lds.s.kc_n[0], (uint32_t)__popcll(br));
+        atomicAdd(&lds.s.kc_n[1], (uint32_t)__popcll(bs));
+      }
     }
   }
   if ((tid >> 6) < 4) STAMP(4 + (tid >> 6));  // per-wave end of the fast path
@@ -2878,6 +3034,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       out.plane[i] = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
       out.sel[i] = sel ? 1 : 0;
       out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
+      if constexpr (KC) {
+        // this search's certificate: the query, G, the 8 positions
+        if (cfg.kc_epoch && q.w != -2.0f) {
+          out.kq[i] = q;
+          out.kpos[2 * i] = make_uint4(nb_pos[slot][0], nb_pos[slot][1], nb_pos[slot][2], nb_pos[slot][3]);
+          out.kpos[2 * i + 1] =
+              make_uint4(nb_pos[slot][4], lds.s.kp3[slot][0], lds.s.kp3[slot][1], lds.s.kp3[slot][2]);
+        }
+      }
       if (sel) {
         double h[12];
         jacobian_row(pose, bx, by, bz, abcd[0], abcd[1], abcd[2], cfg.extrinsic != 0, h);
@@ -2894,6 +3059,17 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   if (tid == 0) STAMP(2);
   if (tid == 0 && out.chunk_cost)
     out.chunk_cost[chunk - cfg.c_begin] = lds.s.cost + 256u * (uint32_t)ref_cnt + 1024u * (uint32_t)nfar;
+  if constexpr (KC) {
+    if (tid == 0 && cfg.kc_epoch) {
+      // every live query of the chunk searched (and wrote its entry) when the
+      // chunk's entries were another update's
+      if (!cache_ok) out.kepoch[chunk] = cfg.kc_epoch;
+      if (out.kc_count) {
+        atomicAdd(out.kc_count, lds.s.kc_n[0]);
+        atomicAdd(out.kc_count + 1, lds.s.kc_n[1]);
+      }
+    }
+  }
   // the chunk's cell-sorted neighbour positions ([slot][5] in LDS, [i][5]
   // in HBM: one contiguous run of 5 * live words, 16-B stores).  Nearest_Points
   // ids and pointSearchSqDis are derived from them only when read
@@ -3183,6 +3359,16 @@ struct Ctx {
   float* resid = nullptr;
   double* chunk_part = nullptr;
   uint32_t* chunk_cost = nullptr;  // per chunk of the last search pass (chunk_order)
+  // kNN certificates of the device-resident update (k_search_pass): per point
+  // query + bound, 8 positions; per chunk the update epoch they belong to
+  float4* kq = nullptr;
+  uint4* kpos = nullptr;
+  uint32_t* kepoch = nullptr;
+  uint32_t kc_next = 0;       // last epoch handed out
+  uint32_t kc_epoch = 0;      // the running update's (0: certificates off)
+  uint64_t kc_version = 0;    // map version of the update's first pass
+  bool kc_stats = false;      // count certified / searched queries (slio_debug_knn_cert): two
+                              // same-address atomics per workgroup, off the product path
   uint32_t* chunk_perm = nullptr;  // search order for the next device-resident pass
   int cus_per_xcd = 0;             // CUs per XCD (0: chunk_order off)
   // far queue (deferred queries, see far_search)
@@ -3210,7 +3396,42 @@ struct Ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   double prof_ms[3] = {0, 0, 0};
   int64_t prof_n[3] = {0, 0, 0};
+  // diagnostic switches of the update path, read from the environment once
+  // per handle (slio_create, slio_debug_reload_switches): no getenv on the
+  // host turnaround between updates
+  struct Switches {
+    bool no_fuse = false;     // SLIO_NO_FUSE: two launches per pass
+    bool no_fuse0 = false;    // SLIO_NO_FUSE0: two launches for the first pass
+    bool no_mfma = false;     // SLIO_NO_MFMA: VALU chunk products
+    bool event_wait = false;  // SLIO_EVENT_WAIT: wait on a completion event
+    bool no_kc = false;       // SLIO_NO_KNN_CERT: every pass searches in full
+  } sw;
+  // host clock stamps (CLOCK_MONOTONIC ns) of the last device-resident update
+  // (slio_debug_host_stamps)
+  bool hstamp = false;
+  int64_t hst[8] = {};
 };
+
+static bool env_on(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] && e[0] != '0';
+}
+static void load_switches(Ctx& c) {
+  c.sw.no_fuse = env_on("SLIO_NO_FUSE");
+  c.sw.no_fuse0 = env_on("SLIO_NO_FUSE0");
+  c.sw.no_mfma = env_on("SLIO_NO_MFMA");
+  c.sw.event_wait = env_on("SLIO_EVENT_WAIT");
+  c.sw.no_kc = env_on("SLIO_NO_KNN_CERT");
+}
+static inline int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
+#define SLIO_HSTAMP(c, k) \
+  do {                    \
+    if ((c).hstamp) (c).hst[k] = mono_ns(); \
+  } while (0)
 
 static std::pair<hipEvent_t, hipEvent_t> prof_pair(Ctx& c) {
   if (!c.pool.empty()) {
@@ -3352,6 +3573,12 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->chunk_cost);
   (void)hipFree(c->chunk_perm);
   c->chunk_cost = c->chunk_perm = nullptr;
+  (void)hipFree(c->kq);
+  (void)hipFree(c->kpos);
+  (void)hipFree(c->kepoch);
+  c->kq = nullptr;
+  c->kpos = nullptr;
+  c->kepoch = nullptr;
   c->bx = c->by = c->bz = nullptr;
   c->nbr_idx = nullptr;
   c->nbr_sqd = nullptr;
@@ -3388,8 +3615,7 @@ static hipError_t wait_published(Ctx& c) {
   // the stream itself is queried now and then (a failed or early-exiting
   // launch still ends the wait): no completion-event packet behind the
   // update's kernels (SLIO_EVENT_WAIT=1: the round-2 event record + query)
-  const char* ev_env = std::getenv("SLIO_EVENT_WAIT");
-  const bool use_event = ev_env && ev_env[0] && ev_env[0] != '0';
+  const bool use_event = c.sw.event_wait;
   if (use_event) {
     if (!c.done_ev && (e = hipEventCreateWithFlags(&c.done_ev, hipEventDisableTiming))) return e;
     if ((e = hipEventRecord(c.done_ev, c.stream))) return e;
@@ -3464,10 +3690,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   cfg.c_end = c1;
   cfg.pass_idx = sa ? sa->pass_idx : 0;
   cfg.knn_only = knn_only ? 1 : 0;
-  {
-    const char* e = std::getenv("SLIO_NO_MFMA");
-    cfg.mfma = !(e && e[0] && e[0] != '0');
-  }
+  cfg.mfma = !c.sw.no_mfma;
   // later passes of a device-resident update take their chunks in the order
   // the previous pass's costs call for (chunk_order; pass 0 in index order)
   static const bool no_order = std::getenv("SLIO_NO_CHUNK_ORDER") != nullptr;
@@ -3486,8 +3709,14 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   // change by another handle waits for these launches (map_write_begin)
   std::shared_lock<std::shared_mutex> map_lock(c.map->mu);
   if (int rc = map_read_sync(c)) return rc;
-  PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,   c.sel,
-            c.resid,      c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost};
+  // kNN certificates: only a device-resident pass after the update's first,
+  // on the map that pass ran on (another handle sharing the map may have
+  // rebuilt it in between)
+  if (!devpose) c.kc_version = c.map->version;
+  cfg.kc_epoch = (devpose && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
+  PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,  c.sel,    c.resid,
+            c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq, c.kpos,
+            c.kepoch,     c.kc_stats ? c.count + kKcCount : nullptr};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
@@ -3745,6 +3974,7 @@ int slio_create(slio_handle* out, const slio_params* p) {
     return SLIO_EDEVICE;
   }
   h->c.stream = h->c.own_stream;
+  load_switches(h->c);
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess &&
@@ -3799,6 +4029,28 @@ int slio_destroy(slio_handle h) {
 int slio_set_stream(slio_handle h, void* s) {
   SLIO_CHECK_H(h);
   h->c.stream = s ? (hipStream_t)s : h->c.own_stream;
+  return SLIO_OK;
+}
+
+int slio_debug_reload_switches(slio_handle h) {
+  if (!h) return SLIO_EINVAL;
+  load_switches(h->c);
+  return SLIO_OK;
+}
+
+int slio_debug_knn_cert(slio_handle h, uint32_t out[2]) {
+  SLIO_CHECK_H(h);
+  if (!out) return SLIO_EINVAL;
+  h->c.kc_stats = true;  // counting starts with the first call
+  SLIO_HIP(hipStreamSynchronize(h->c.stream));
+  SLIO_HIP(hipMemcpy(out, h->c.count + kKcCount, 8, hipMemcpyDeviceToHost));
+  return SLIO_OK;
+}
+
+int slio_debug_host_stamps(slio_handle h, int enable, int64_t out[8]) {
+  if (!h) return SLIO_EINVAL;
+  if (out) std::memcpy(out, h->c.hst, sizeof(h->c.hst));
+  if (enable >= 0) h->c.hstamp = enable != 0;
   return SLIO_OK;
 }
 
@@ -4184,7 +4436,9 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.nbr_sqd, 4 * 5 * cap)) || (e = hipMalloc(&c.plane, 16 * cap)) ||
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
-        (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc))) {
+        (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc)) ||
+        (e = hipMalloc(&c.kq, 16 * cap)) || (e = hipMalloc(&c.kpos, 32 * cap)) ||
+        (e = hipMalloc(&c.kepoch, 4 * capc)) || (e = hipMemset(c.kepoch, 0, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));
       return SLIO_ENOMEM;
@@ -5826,8 +6080,6 @@ int slio_map_download(slio_handle h, float* x, float* y, float* z, uint32_t* ids
   return SLIO_OK;
 }
 
-// test support (not in include/slio.h): the index's points in their stored
-// (cell, id) order, x, y, z, bits(id) per point, after the pending rebuild
 // Test hook (not in the header): the last pass's per-chunk partials,
 // num_chunks(n) x 91 doubles (global chunk index; other ranks' chunks are
 // stale), so tests can rebuild the segment / super tree from them.
@@ -5844,6 +6096,8 @@ int slio_dbg_chunk_partials(slio_handle h, double* out, int64_t cap, int64_t* nc
   return SLIO_OK;
 }
 
+// test support (not in include/slio.h): the index's points in their stored
+// (cell, id) order, x, y, z, bits(id) per point, after the pending rebuild
 int slio_dbg_map_raw(slio_handle h, float* xyzw, int64_t cap, int64_t* n) {
   SLIO_CHECK_H(h);
   Ctx& c = h->c;
@@ -6753,6 +7007,12 @@ struct UpdateRun {
       SLIO_HIP(hipHostGetDevicePointer((void**)&c.d_hctl, c.h_ctl, 0));
     }
     first = (mode == SLIO_MODE_REFERENCE) ? -1 : 0;
+    // a fresh epoch: no certificate of an earlier update is ever used
+    if (++c.kc_next == 0) {
+      if (c.kepoch) SLIO_HIP(hipMemsetAsync(c.kepoch, 0, 4 * (num_chunks(c.prm.max_points) + 1), c.stream));
+      c.kc_next = 1;
+    }
+    c.kc_epoch = c.sw.no_kc ? 0 : c.kc_next;
     // H's columns 6..11 are zero without extrinsic estimation (esekfom.hpp:218-220):
     // the filter step works on the first 6 error-state components
     dim = ext ? 12 : 6;
@@ -6804,7 +7064,7 @@ struct UpdateRun {
     const SolveArgs sa = args(i);
     // pass 0 always searches (converge starts true, esekfom.hpp:282)
     const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
-    if (fusable() && !(p0 && getenv_on("SLIO_NO_FUSE0"))) {
+    if (fusable() && !(p0 && c.sw.no_fuse0)) {
       // one launch: search (or reuse) pass + sums + filter step.  The first
       // pass's launch copies the mapped host block into HBM, so the host
       // fills the block BEFORE that launch (measured: launching first and
@@ -6818,11 +7078,13 @@ struct UpdateRun {
           set_error("slio_ikf_update_device: singular covariance block P[:D, :D]");
           return SLIO_EINVAL;
         }
+        SLIO_HSTAMP(c, 2);
       }
       const FuseArgs fa{c.ctl, p0 ? (const IkfCtl*)c.d_hctl : nullptr, c.d_seg, c.d_super, c.ctl, c.d_hctl,
                         c.count, R, i, maxit, num_chunks(c.n)};
       int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
       if (rc) return rc;
+      if (p0) SLIO_HSTAMP(c, 3);
       SLIO_HIP(hipGetLastError());
       return SLIO_OK;
     }
@@ -6850,12 +7112,8 @@ struct UpdateRun {
   // its reuse passes) and with or without extrinsic estimation (D = 12 / 6),
   // given at least 8 chunks per super-chunk (every segment row has a chunk).
   // SLIO_NO_FUSE=1 keeps two launches per pass.
-  static bool getenv_on(const char* name) {
-    const char* e = std::getenv(name);
-    return e && e[0] && e[0] != '0';
-  }
   bool fusable() const {
-    const bool off = getenv_on("SLIO_NO_FUSE");
+    const bool off = c.sw.no_fuse;
     const int lpq = c.prm.lanes_per_query;
     return !off && !multi && c.prm.nranks == 1 &&
            (lpq != 1 && lpq != 4 && lpq != 8) && !(c.prm.search_radius > 0.0f) &&
@@ -6874,16 +7132,14 @@ struct UpdateRun {
   }
 
   int finish(slio_ikf_stats* stats) {
+    SLIO_HSTAMP(c, 4);
     SLIO_HIP(wait_published(c));
+    SLIO_HSTAMP(c, 5);
     const IkfCtl& hc = *c.h_ctl;
     if (!hc.done) {
       set_error("slio_ikf_update_device: the update did not complete (passes " + std::to_string(hc.passes) +
                 ", searches " + std::to_string(hc.searches) + ", converge " + std::to_string(hc.converge) +
                 ", published " + std::to_string(hc.published) + ")");
-      return SLIO_EDEVICE;
-    }
-    if (hc.singular == 2) {
-      set_error("slio_ikf_update_device: a fused pass's hand-off between workgroups timed out");
       return SLIO_EDEVICE;
     }
     if (hc.singular) {
@@ -6947,6 +7203,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     return SLIO_EINVAL;
   }
   Ctx& c = h->c;
+  SLIO_HSTAMP(c, 0);
   // the caller's reduce hook, else the handle's communicator (any number of
   // ranks, one included: the same path as several)
   const bool comm = !reduce && c.comm;
@@ -6956,6 +7213,7 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   }
   UpdateRun u(c, x, P, R, maximum_iter, extrinsic_est, mode, reduce || comm);
   if (int rc = u.begin()) return rc;
+  SLIO_HSTAMP(c, 1);
   for (int i = u.first; i < maximum_iter; ++i) {
     // single rank: the filter step runs in the super-sum kernel's last block
     // (or the search pass's tail); multi-rank: pass -> all-reduce of the
@@ -6972,7 +7230,9 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
     if (u.multi)
       if (int rc = u.solve(i)) return rc;
   }
-  return u.finish(stats);
+  const int rc = u.finish(stats);
+  SLIO_HSTAMP(c, 6);
+  return rc;
 }
 
 int slio_comm_unique_id(uint8_t id[SLIO_COMM_ID_BYTES]) {
@@ -7115,11 +7375,27 @@ static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], do
   gs.n = n;
   for (int r = 0; r < n; ++r) gs.sup[r] = hs[r]->c.d_super;
   Ctx& c0 = hs[0]->c;
+  // host stamps of the group update on rank 0's handle (slio_debug_host_stamps):
+  // [0] entry, [1] every pass enqueued, [2] every rank's result seen, [3] exit;
+  // [4] / [5] / [6] host ns spent enqueueing the ranks' pass launches / the
+  // reduce (events + k_group_reduce or the RCCL group) / the filter steps
+  const bool hs_on = c0.hstamp;
+  int64_t t_a = 0;
+  if (hs_on) {
+    c0.hst[0] = mono_ns();
+    c0.hst[4] = c0.hst[5] = c0.hst[6] = 0;
+  }
   for (int i = runs[0].first; i < maximum_iter; ++i) {
+    if (hs_on) t_a = mono_ns();
     for (int r = 0; r < n; ++r) {
       SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
       if (int rc = runs[r].pass(i)) return rc;
       if (kind == 2 && r > 0) SLIO_HIP(hipEventRecord(hs[r]->c.grp_ev, hs[r]->c.stream));
+    }
+    if (hs_on) {
+      const int64_t t = mono_ns();
+      c0.hst[4] += t - t_a;
+      t_a = t;
     }
     if (kind == 1) {
       // one RCCL all-reduce of the 8 x 91 super rows per pass, all ranks
@@ -7148,18 +7424,30 @@ static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], do
         SLIO_HIP(hipStreamWaitEvent(hs[r]->c.stream, c0.grp_ev, 0));
       }
     }
+    if (hs_on) {
+      const int64_t t = mono_ns();
+      c0.hst[5] += t - t_a;
+      t_a = t;
+    }
     for (int r = 0; r < n; ++r) {
       SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
       if (int rc2 = runs[r].solve(i)) return rc2;
     }
+    if (hs_on) c0.hst[6] += mono_ns() - t_a;
   }
+  if (hs_on) c0.hst[1] = mono_ns();
   slio_ikf_stats st0{};
   for (int r = 0; r < n; ++r) {
     SLIO_HIP(hipSetDevice(hs[r]->c.prm.device));
     slio_ikf_stats st{};
-    if (int rc = runs[r].finish(&st)) return rc;
+    const bool keep = hs[r]->c.hstamp;
+    hs[r]->c.hstamp = false;  // (finish's own stamps would overwrite the group's)
+    const int rc = runs[r].finish(&st);
+    hs[r]->c.hstamp = keep;
+    if (rc) return rc;
     if (r == 0) st0 = st;
   }
+  if (hs_on) c0.hst[2] = mono_ns();
   for (int r = 1; r < n; ++r)
     if (std::memcmp(&xs[r], &xs[0], sizeof(slio_state)) != 0 ||
         std::memcmp(Ps[r].data(), Ps[0].data(), sizeof(double) * 576) != 0) {
@@ -7169,6 +7457,7 @@ static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], do
   *x = xs[0];
   std::memcpy(P, Ps[0].data(), sizeof(double) * 576);
   if (stats) *stats = st0;
+  if (hs_on) c0.hst[3] = mono_ns();
   return SLIO_OK;
 }
 

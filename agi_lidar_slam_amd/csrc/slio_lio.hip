@@ -2770,9 +2770,18 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
     const char* cg = std::getenv("SLIO_LEGO_CC_GLOBAL");
     h->cc_global = cg && cg[0] && cg[0] != '0';
   }
-  if (h->cells <= kLegoCcCells)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lego_cc), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(5 * h->cells));
+  if (h->cells <= kLegoCcCells) {
+    // the attribute is the kernel's, for the whole process: set once to the
+    // largest image the kernel takes, not to this handle's size
+    static const hipError_t cc_attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k_lego_cc), hipFuncAttributeMaxDynamicSharedMemorySize, 5 * kLegoCcCells);
+    if (cc_attr != hipSuccess) {
+      set_error(std::string("slio_lego_create: k_lego_cc LDS attribute: ") + hipGetErrorString(cc_attr));
+      lego_free(h);
+      delete h;
+      return SLIO_EDEVICE;
+    }
+  }
   *out = h;
   return SLIO_OK;
 }

@@ -260,6 +260,100 @@ def bench_c3(args, rank, world, dev, dist):
         f.close()
 
 
+def bench_group(args, rank, world, dev, dist):
+    """C4 rehearsal on ONE GPU: the drop-in's multi-GPU form
+    (slio_create_group / slio_group_ikf_update) with
+    --group-ranks ranks sharing this device, so the group takes the in-device
+    reduce (k_group_reduce) instead of RCCL over xGMI.  The C2 scan is split
+    into the ranks' contiguous shards, the map is shared; one step = one group
+    update (--iters passes, fixed flow).  Not the C2 line and not a scaling
+    measurement: it times the group path's launches, event waits, reduce and
+    filter steps, and (host stamps) where the host spends its time per update."""
+    from agi_lidar_slam_amd import _lib as L, build, synth
+    build.build()
+    lib = L.load()
+    n = args.group_ranks
+    mp, fr = synth.make_problem(args.map_points, args.scan_points, pattern="avia", cache_dir=args.cache_dir)
+    fr.body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])
+    p = L.SlioParams()
+    lib.slio_params_default(C.byref(p))
+    p.max_points, p.grid_cell = args.scan_points, args.cell
+    hs = (C.c_void_p * n)()
+    dv = (C.c_int32 * n)(*([dev] * n))
+    L.check(lib.slio_create_group(hs, n, dv, C.byref(p)), "group")
+    kind = lib.slio_group_reduce_kind(hs[0])
+    x, y, z = (np.ascontiguousarray(mp[:, k]) for k in range(3))
+    L.check(lib.slio_map_upload(hs[0], L.fptr(x), L.fptr(y), L.fptr(z), mp.shape[0]), "map")
+    for r in range(1, n):
+        L.check(lib.slio_map_share(hs[r], hs[0]), "share")
+    bx, by, bz = (np.ascontiguousarray(fr.body[:, k]) for k in range(3))
+    for r in range(n):
+        L.check(lib.slio_scan_upload(hs[r], L.fptr(bx), L.fptr(by), L.fptr(bz), fr.body.shape[0]), "scan")
+    st0 = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9),
+                          [0, 0, -9.81]])
+    xs0 = L.SlioState()
+    xs0.pos[:] = list(st0[0:3])
+    xs0.rot[:] = list(st0[3:7])
+    xs0.rli[:] = list(st0[7:11])
+    xs0.tli[:] = list(st0[11:14])
+    xs0.grav[:] = list(st0[23:26])
+    xs = L.SlioState()
+    P0 = np.eye(24) * 1e-2
+    P = np.empty_like(P0)
+    stats = L.SlioIkfStats()
+
+    def step():
+        C.memmove(C.addressof(xs), C.addressof(xs0), C.sizeof(xs))
+        P[...] = P0
+        L.check(lib.slio_group_ikf_update(hs, n, C.byref(xs), L.dptr(P), 0.001, args.iters, 0,
+                                          L.SLIO_MODE_FIXED, C.byref(stats)), "group update")
+
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    el = time.perf_counter() - t0
+    # host stamps of further steps (rank 0's handle)
+    hst = np.zeros(8, np.int64)
+    lib.slio_debug_host_stamps(hs[0], 1, None)
+    rows = []
+    for _ in range(max(1, args.timing_steps)):
+        step()
+        lib.slio_debug_host_stamps(hs[0], -1, L.i64ptr(hst))
+        rows.append(hst.copy())
+    lib.slio_debug_host_stamps(hs[0], 0, None)
+    r = np.array(rows, np.float64) / 1e3
+    passes = int(stats.passes)
+    host = {"enqueue_all_us": float(np.median(r[:, 1] - r[:, 0])),
+            "rank_pass_launches_us": float(np.median(r[:, 4])),
+            "reduce_enqueue_us": float(np.median(r[:, 5])),
+            "filter_step_enqueue_us": float(np.median(r[:, 6])),
+            "wait_after_enqueue_us": float(np.median(r[:, 2] - r[:, 1])),
+            "update_us": float(np.median(r[:, 3] - r[:, 0]))}
+    out = {
+        "metric": "IKF iterations/sec, C4 group rehearsal on one GPU (not the C2 line)",
+        "value": args.steps * passes / el,
+        "unit": "IKF iterations/s",
+        "n_gpus": 1,
+        "group_ranks": n,
+        "reduce": {1: "RCCL", 2: "in-device (k_group_reduce)"}.get(kind, str(kind)),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "us_per_pass": el / args.steps / passes * 1e6,
+        "host_us_per_update": host,
+        "config": {"workload": (f"C4 rehearsal: slio_group_ikf_update, {n} ranks on one device, "
+                                f"{args.scan_points}-pt scan split {n} ways vs {args.map_points}-pt map, "
+                                f"{args.iters} IKF iterations (fixed flow)"),
+                   "map_points": args.map_points, "scan_points": args.scan_points},
+        "data": "synthetic (seeded urban scene, Avia-like rosette scan)",
+    }
+    print(json.dumps(out), flush=True)
+    for q in range(n):
+        lib.slio_destroy(hs[q])
+
+
 def bench_lego(args, rank, world, dev, dist):
     """LeGO-LOAM front-end: ImageProjection
     (projectPointCloud, groundRemoval, cloudSegmentation) + the front half of
@@ -525,12 +619,16 @@ def main():
     ap.add_argument("--host-loop", action="store_true",
                     help="run the 24x24 step on the host after every pass (slio_ikf_update)")
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
-    ap.add_argument("--workload", choices=["c2", "c3", "c5", "lego"], default="c2",
+    ap.add_argument("--group-ranks", type=int, default=8,
+                    help="group: ranks of the one-GPU C4 rehearsal (must divide 8)")
+    ap.add_argument("--workload", choices=["c2", "c3", "c5", "lego", "group"], default="c2",
                     help="c2: IKF iterations/s, 100k Avia scan vs 10M map (BASELINE.json metric); "
                          "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan; "
                          "c5: batched replay, --replicas concurrent distinct 100k scans per GPU vs a "
                          "shared 50M map (BASELINE config 5: 32 scans on 8 GPUs = 4 per GPU); "
-                         "lego: LeGO-LOAM front-end scans/s on a VLP-16 16 x 1800 sweep, IMU on")
+                         "lego: LeGO-LOAM front-end scans/s on a VLP-16 16 x 1800 sweep, IMU on; "
+                         "group: the C4 group path (slio_group_ikf_update) rehearsed with --group-ranks "
+                         "ranks on one GPU")
     ap.add_argument("--replicas", type=int, default=4, help="c5: concurrent scans per GPU")
     ap.add_argument("--cpu-scans-c5", type=int, default=4)
     ap.add_argument("--reduce-hook", action="store_true",
@@ -563,8 +661,9 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev)
         dist.init_process_group(args.dist_backend if args.workload == "c2" else "gloo")
-    if args.workload in ("c3", "c5", "lego"):
-        {"c3": bench_c3, "c5": bench_c5, "lego": bench_lego}[args.workload](args, rank, world, dev, dist)
+    if args.workload in ("c3", "c5", "lego", "group"):
+        {"c3": bench_c3, "c5": bench_c5, "lego": bench_lego, "group": bench_group}[args.workload](
+            args, rank, world, dev, dist)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -451,6 +451,28 @@ int slio_s2m_lm_step(const float AtA[36], const float AtB[6], int64_t nsel, int 
 int slio_state_boxplus(const slio_state* x, const double dx[24], slio_state* out);
 int slio_state_boxminus(const slio_state* x1, const slio_state* x2, double dx[24]);
 
+/* ---- diagnostics ----------------------------------------------------------- */
+/* Re-read the SLIO_NO_FUSE / SLIO_NO_FUSE0 / SLIO_NO_MFMA / SLIO_EVENT_WAIT
+ * switches of the update path (read once at slio_create). */
+int slio_debug_reload_switches(slio_handle h);
+/* Host clock stamps (CLOCK_MONOTONIC ns) of the last slio_ikf_update_device:
+ * [0] entry, [1] state set up, [2] control block + information-form constants
+ * ready (fused path), [3] first launch enqueued, [4] every launch enqueued,
+ * [5] result seen, [6] return.  After slio_group_ikf_update, rank 0's handle
+ * holds the group's: [0] entry, [1] every pass enqueued, [2] every rank's
+ * result seen, [3] return, [4] / [5] / [6] host ns spent enqueueing the
+ * ranks' pass launches / the reduce (events + in-device reduce, or the RCCL
+ * group) / the filter steps.  out may be NULL; enable 1 / 0 turns stamping
+ * on / off, -1 leaves it. */
+int slio_debug_host_stamps(slio_handle h, int enable, int64_t out[8]);
+/* kNN certificate counters (wrapping 32-bit; counting starts with the first
+ * call, which turns it on for the handle -- it costs two same-address atomics
+ * per workgroup):
+ * out[0] queries whose 5 nearest a later pass certified from its earlier
+ * search's 8 nearest, out[1] queries searched in full in passes that write
+ * certificates (device-resident passes after the first). */
+int slio_debug_knn_cert(slio_handle h, uint32_t out[2]);
+
 #ifdef __cplusplus
 }
 #endif

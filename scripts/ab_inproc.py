@@ -61,6 +61,7 @@ def main():
             for kv in cfg.split(","):
                 k, v = kv.split("=")
                 os.environ[k] = v
+        lib.slio_debug_reload_switches(h)
 
     def run(n):
         for _ in range(n):

@@ -10,7 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 from agi_lidar_slam_amd.lego import LegoFrontEnd, LegoParams  # noqa: E402
 
-lib = L.load(os.environ["SLIO_LIB"])
+from variant import use  # noqa: E402
+lib = use(os.environ["SLIO_LIB"])
 lib.slio_dbg_cc_stamps.argtypes = [C.POINTER(C.c_ulonglong)]
 sw = synth.make_vlp16_sweep()
 fe = LegoFrontEnd(LegoParams())

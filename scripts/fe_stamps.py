@@ -9,7 +9,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
-lib = L.load(os.environ["SLIO_LIB"])
+from variant import use  # noqa: E402
+lib = use(os.environ["SLIO_LIB"])
 from agi_lidar_slam_amd.frontend import LioSamFrontEnd, LioSamParams, imu_deskew_table  # noqa: E402
 
 lib.slio_dbg_fe_stamps.argtypes = [C.POINTER(C.c_ulonglong)]

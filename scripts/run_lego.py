@@ -6,7 +6,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
-L.load(os.environ.get("SLIO_LIB", L.LIB_PATH))
+from variant import use  # noqa: E402
+use(os.environ["SLIO_LIB"]) if "SLIO_LIB" in os.environ else L.load()
 from agi_lidar_slam_amd.lego import LegoFrontEnd, LegoImu, LegoParams  # noqa: E402
 
 reps = int(os.environ.get("REPS", "200"))

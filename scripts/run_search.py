@@ -15,7 +15,8 @@ from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
 
 def main():
-    lib = L.load(os.environ.get("SLIO_LIB", L.LIB_PATH))
+    from variant import use
+    lib = use(os.environ["SLIO_LIB"]) if "SLIO_LIB" in os.environ else L.load()
     lpq = int(os.environ.get("LPQ", "2"))
     cell = float(os.environ.get("CELL", "1.0"))
     reps = int(os.environ.get("REPS", "20"))

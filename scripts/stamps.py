@@ -8,7 +8,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
-lib = L.load(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
+from variant import use  # noqa: E402
+lib = use(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
 lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 for lpq in [int(v) for v in os.environ.get("LPQS", "102,2").split(",")]:
     for nscan in [100000]:

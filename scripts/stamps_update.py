@@ -12,7 +12,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from agi_lidar_slam_amd import _lib as L, synth  # noqa: E402
 
-lib = L.load(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
+from variant import use  # noqa: E402
+lib = use(os.environ.get("SLIO_LIB", os.path.join(os.path.dirname(L.LIB_PATH), "_abl", "libslio_STAMP.so")))
 lib.slio_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 mp, fr = synth.make_problem(10_000_000, 100_000, pattern="avia", cache_dir="/tmp/slio_cache")
 body = np.ascontiguousarray(fr.body[synth.voxel_order(fr.body)])

@@ -1,5 +1,5 @@
-"""Where the fused pass's tail goes (diagnostic build: bash scripts/build_abl.sh
-sstamp -DSLIO_SOLVE_STAMP, then SLIO_LIB_OVERRIDE=agi_lidar_slam_amd/_abl/libslio_sstamp.so).
+"""Where the fused pass's tail goes (diagnostic build: bash scripts/build_variant.sh
+sstamp -DSLIO_SOLVE_STAMP, then python scripts/variant.py <that .so> scripts/tail_stamps.py).
 C2 problem, fixed-mode device updates (every pass fused); the stamps of the
 update's last pass: launch start (block 0), then the final workgroup's
 partial issued / segment arrival / row stored / row arrival, the 64 rows

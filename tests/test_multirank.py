@@ -4,7 +4,7 @@ Each rank forms the super rows of its own super-chunks from the chunk
 partials of its own chunks (tests/tree_model.py: the device's segment-row
 tree, k_super_sums / fused_tail), zeros elsewhere; a SUM all-reduce must
 reproduce the single-rank tree bit for bit, which is what makes 1/2/4/8-GPU
-runs identical.  tests/test_gpu_parity.py::test_tree_model_matches_device
+runs identical.  tests/test_gpu_parity.py::test_sharded_handles_bitwise_equal
 pins the model to the device's own super rows."""
 import os
 import sys

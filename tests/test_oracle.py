@@ -116,3 +116,43 @@ def test_pass_gates(oracle_mod):
     out2 = oracle_mod.h_pass(T, st, fr.body, ps, False)
     np.testing.assert_array_equal(ps.sel, sel0)
     np.testing.assert_array_equal(out2, out)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("ext", [False, True])
+def test_reference_gain_equals_reduced_gain(oracle_mod, mode, ext):
+    """The reference's own gain formation (esekfom.hpp:311-319: K =
+    K_front[:, :12] H^T / R as a 24 x m matrix, then K h and K H) against
+    the H^T H / H^T h form the GPU path reduces to (reference_gain=0): the
+    same control flow and neighbours, x and P equal to rounding.  Without
+    extrinsic estimation within 1e-12 (x, absolute) and 1e-12 of max |P|; with
+    it the 12-column system's directions that only the prior observes make
+    S = P^-1 + E^T H^T H E / R ill-conditioned (kappa ~ 2e8 here), so the two
+    orderings of the same sums may differ by up to u * kappa (x) and
+    32 u kappa max|P| (P)."""
+    from agi_lidar_slam_amd import synth
+    mp, fr = synth.make_problem(200000, 20000, pattern="avia")
+    T = oracle_mod.Tree(mp)
+    st = np.concatenate([fr.init_pos, fr.init_rot, [1, 0, 0, 0], synth.AVIA_T_LI, np.zeros(9),
+                         [0, 0, -9.81]])
+    P0 = np.eye(24) * 1e-2
+    a = oracle_mod.ikf_update(T, fr.body, st, P0, maximum_iter=4, mode=mode, extrinsic=ext,
+                              reference_gain=1, threads=8)
+    b = oracle_mod.ikf_update(T, fr.body, st, P0, maximum_iter=4, mode=mode, extrinsic=ext,
+                              reference_gain=0, threads=8)
+    np.testing.assert_array_equal(a[2], b[2])   # passes, searches, valid, converged, m
+    np.testing.assert_array_equal(a[3], b[3])   # Nearest_Points of the last search
+    np.testing.assert_array_equal(a[5], b[5])   # point_selected_surf
+    dx, dP, pmax = np.abs(a[0] - b[0]).max(), np.abs(a[1] - b[1]).max(), np.abs(a[1]).max()
+    if not ext:
+        assert dx <= 1e-12, dx
+        assert dP <= 1e-12 * pmax, dP
+    else:
+        rows = np.zeros((fr.body.shape[0], 14))
+        oracle_mod.h_pass(T, st, fr.body, oracle_mod.PassState(fr.body.shape[0]), True, extrinsic=True,
+                          rows=rows)
+        S = np.linalg.inv(P0)
+        S[:12, :12] += rows[:, :12].T @ rows[:, :12] / 0.001
+        u, kappa = 2.0 ** -52, np.linalg.cond(S)
+        assert dx <= u * kappa, (dx, kappa)
+        assert dP <= 32 * u * kappa * pmax, (dP, kappa)
