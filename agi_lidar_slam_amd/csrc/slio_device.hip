@@ -70,9 +70,6 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 constexpr int kBlock = 256;                      // threads per search workgroup
 constexpr int kDefaultLPQ = 2;                   // lanes per query (tuned on MI355X)
-#ifndef SLIO_KC_U
-#define SLIO_KC_U 2                              // the same, in a search that keeps 8 (kNN certificates)
-#endif
 #ifndef SLIO_SEARCH_U
 #define SLIO_SEARCH_U 3                          // candidate loads in flight per lane and step (A/B on MI355X, block rows: 3 < 4 < 2)
 #endif
@@ -740,38 +737,25 @@ __device__ __forceinline__ void top5_insert(Top5& t, uint64_t key) {
   t.k[0] = c[0] ? key : t.k[0];
 }
 
-// Sorted top-8 list with the smallest squared distance it has DROPPED (an
+// A sorted top-5 list with the smallest squared distance it has DROPPED (an
 // evicted entry or a rejected key): after a scan, every scanned candidate
-// outside the list lies at >= m.  The 6th-8th entries and m certify later
-// passes' searches (kNN certificate, k_search_pass): a query that has moved
-// by delta keeps its 5 nearest among these 8 while the 9th bound minus delta
-// stays beyond its new 5th distance.
-struct Top8 {
-  uint64_t k[8];
+// outside the list lies at >= m (the 6th distance of the scanned set).  The
+// 5 and m certify later passes' searches (kNN certificate, k_search_pass).
+struct Top5M {
+  Top5 t;
   float m;
 };
 
-__device__ __forceinline__ void top8_clear(Top8& t) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) t.k[j] = kInfKey;
-  t.m = __int_as_float(0x7f800000);
-}
-
-__device__ __forceinline__ void top8_insert(Top8& t, uint64_t key) {
+__device__ __forceinline__ void top5m_insert(Top5M& a, uint64_t key) {
   // the element that leaves (or never enters) the list; an empty slot's key
   // (all ones) reads as NaN, which fminf ignores
-  const uint64_t drop = key < t.k[7] ? t.k[7] : key;
-  t.m = fminf(t.m, __uint_as_float((uint32_t)(drop >> 32)));
-  bool c[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = key < t.k[j];
-#pragma unroll
-  for (int j = 7; j > 0; --j) t.k[j] = c[j - 1] ? t.k[j - 1] : (c[j] ? key : t.k[j]);
-  t.k[0] = c[0] ? key : t.k[0];
+  const uint64_t drop = key < a.t.k[4] ? a.t.k[4] : key;
+  a.m = fminf(a.m, __uint_as_float((uint32_t)(drop >> 32)));
+  top5_insert(a.t, key);
 }
 
 __device__ __forceinline__ void list_insert(Top5& t, uint64_t key) { top5_insert(t, key); }
-__device__ __forceinline__ void list_insert(Top8& t, uint64_t key) { top8_insert(t, key); }
+__device__ __forceinline__ void list_insert(Top5M& t, uint64_t key) { top5m_insert(t, key); }
 
 __device__ __forceinline__ void consider(Top5& t, const float4 c, uint32_t pos, float qx, float qy,
                                          float qz) {
@@ -797,19 +781,19 @@ __device__ __forceinline__ void merge_round_dpp(Top5& t) {
   for (int j = 0; j < 5; ++j) top5_insert(t, ok[j]);
 }
 template <int CTRL>
-__device__ __forceinline__ void merge_round_dpp(Top8& t) {
-  uint64_t ok[8];
+__device__ __forceinline__ void merge_round_dpp(Top5M& a) {
+  uint64_t ok[5];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ok[j] = dpp64<CTRL>(t.k[j]);
-  const float om = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t.m), CTRL, 0xF, 0xF, false));
+  for (int j = 0; j < 5; ++j) ok[j] = dpp64<CTRL>(a.t.k[j]);
+  const float om = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a.m), CTRL, 0xF, 0xF, false));
 #pragma unroll
-  for (int j = 0; j < 8; ++j) top8_insert(t, ok[j]);
-  t.m = fminf(t.m, om);
+  for (int j = 0; j < 5; ++j) top5m_insert(a, ok[j]);
+  a.m = fminf(a.m, om);
 }
 
-// the 2-lane merge of a query pair's top-8 lists (both lanes end with the
-// merged list and the union's dropped minimum)
-__device__ __forceinline__ void group_merge2(Top8& t) { merge_round_dpp<0xB1>(t); }
+// the 2-lane merge of a query pair's lists (both lanes end with the merged
+// list and the union's dropped minimum)
+__device__ __forceinline__ void group_merge2(Top5M& a) { merge_round_dpp<0xB1>(a); }
 
 // butterfly merge of the LPQ per-lane lists of a query group (lanes of a
 // group are consecutive and aligned, and all active or all inactive).  Up to
@@ -1237,10 +1221,9 @@ struct PassOut {
   uint32_t* chunk_cost;  // per chunk of the rank (relative index): candidates + refinement / far weights
   // kNN certificates (device-resident passes after the first, see
   // k_search_pass): per point the query of its last full search and the
-  // squared-distance bound G of every map point outside its 8 nearest; the
-  // 8 nearest positions; per chunk the update epoch the entries belong to
+  // squared-distance bound G of every map point outside its 5 nearest (which
+  // nbr_pos holds); per chunk the update epoch the entries belong to
   float4* kq;
-  uint4* kpos;          // n * 2: positions 0..3, 4..7
   uint32_t* kepoch;     // per chunk (global index)
   uint32_t* kc_count;   // [0] certified queries, [1] queries searched with a certificate written
 };
@@ -2544,7 +2527,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];            // the query; .w: its certificate bound G (KC, -2: none written)
-    uint32_t kp3[SLIO_CHUNK][3];      // KC: positions of the 6th-8th nearest
     uint32_t kc_n[2];                 // KC: certified queries, searched queries
     // deferred (far) queries of this chunk and the far workers' scratch
     int far_cnt, ref_cnt;
@@ -2626,13 +2608,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     const int64_t i = chunk * SLIO_CHUNK + slot;
     const bool live = i < scan.n;
     float qx = 0.0f, qy = 0.0f, qz = 0.0f;
-    // KC: the point's certificate (earlier query + bound, and this lane's 4 of
-    // its 8 positions), loaded with the scan point: no dependent round trip
+    // KC: the point's certificate (earlier query + bound, and this lane's share
+    // of its 5 positions), loaded with the scan point: no dependent round trip
     float4 ka = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-    uint4 kp = make_uint4(~0u, ~0u, ~0u, ~0u);
+    uint32_t kp[3] = {~0u, ~0u, ~0u};  // this lane's share of the 5: 0..2 (sub 0), 3..4 (sub 1)
     if (KC && cache_ok && live) {
       ka = out.kq[i];
-      kp = out.kpos[2 * i + sub];
+      kp[0] = out.nbr_pos[5 * i + 3 * sub];
+      kp[1] = out.nbr_pos[5 * i + 3 * sub + 1];
+      if (sub == 0) kp[2] = out.nbr_pos[5 * i + 2];
     }
     if (live) {
       const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
@@ -2646,20 +2630,20 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     bool done = !finite;
     bool refine = false;   // exact 5x5x5 refinement wanted (lim = refine bound)
     float lim = 0.0f;
-    // kNN certificate (KC).  A full search on the block rows keeps the 8
-    // nearest and the smallest squared distance it dropped (Top8), so every
-    // map point outside the 8 lies at squared distance >= G = min(dropped,
-    // b1^2) (b1: the block faces' bound) from that query, less a 2e-5
-    // relative margin for float rounding -- a bound on the TRUE squared
-    // distance.  A later pass of the same update, its query moved by
-    // delta <= |q - q_old|, evaluates the 8 at the new query; if
-    // (sqrt(G) - delta)^2 (1 - 1e-5) exceeds the new 5th squared distance,
-    // no point outside the 8 can enter the top 5 (its float distance is
-    // strictly larger), so the 5 smallest keys of the 8 ARE the exact search's
-    // result, tie order included (same keys).  Otherwise the query searches.
+    // kNN certificate (KC).  A full search on the block rows keeps the 5
+    // nearest and the smallest squared distance it dropped (Top5M), so every
+    // other map point lies at squared distance >= G = min(dropped, b1^2)
+    // (b1: the block faces' bound) from that query, less a 2e-5 relative
+    // margin for float rounding -- a bound on the TRUE squared distance.  A
+    // later pass of the same update, its query moved by delta <= |q - q_old|,
+    // evaluates the 5 (nbr_pos: a certified pass rewrites the same set) at
+    // the new query; if (sqrt(G) - delta)^2 (1 - 1e-5) exceeds the new 5th
+    // squared distance, no other point can enter the top 5 (its float
+    // distance is strictly larger), so the 5 sorted by key ARE the exact
+    // search's result, tie order included (same keys).  Otherwise the query
+    // searches.
     bool reused = false;
-    float kG = -1.0f;                      // this search's certificate bound (-1: none)
-    uint32_t kx5 = ~0u, kx6 = ~0u, kx7 = ~0u;  // its 6th-8th positions
+    float kG = -1.0f;  // this search's certificate bound (-1: none)
     if constexpr (KC) {
       // (branch-free up to the gathers, so the certificate loads stay whole)
       const double ex0 = (double)qx - (double)ka.x, ey0 = (double)qy - (double)ka.y,
@@ -2669,18 +2653,17 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       if (cache_ok && finite && ka.w > 0.0f) {
         {
           if (A > 0.0) {
-            // the pair's lanes take 4 of the 8 each, then merge (as a search)
-            const uint32_t ps[4] = {kp.x, kp.y, kp.z, kp.w};
-            float4 cc[4];
+            // the pair's lanes take 3 + 2 of the 5, then merge (as a search)
+            float4 cc[3];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) cc[j] = pts[ps[j] != ~0u ? ps[j] : 0u];
+            for (int j = 0; j < 3; ++j) cc[j] = pts[kp[j] != ~0u ? kp[j] : 0u];
             Top5 tr;
             top5_clear(tr);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 3; ++j) {
               const float ddx = qx - cc[j].x, ddy = qy - cc[j].y, ddz = qz - cc[j].z;
               const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
-              top5_insert(tr, ps[j] != ~0u ? (((uint64_t)__float_as_uint(d) << 32) | (uint64_t)ps[j]) : kInfKey);
+              top5_insert(tr, kp[j] != ~0u ? (((uint64_t)__float_as_uint(d) << 32) | (uint64_t)kp[j]) : kInfKey);
             }
             group_merge<2>(tr);
             if (tr.k[4] != kInfKey &&
@@ -2717,17 +2700,11 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
             printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
 #endif
           if (KC && cfg.kc_epoch) {
-            Top8 t8;
-            top8_clear(t8);
-            // (2 loads in flight per set: the top-8 list takes the registers)
-            scan_block_rows<LPQ, SLIO_KC_U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t8);
-            group_merge2(t8);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) t.k[j] = t8.k[j];
-            kx5 = (uint32_t)t8.k[5];
-            kx6 = (uint32_t)t8.k[6];
-            kx7 = (uint32_t)t8.k[7];
-            kG = t8.m;
+            Top5M tm{t, __int_as_float(0x7f800000)};
+            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, tm);
+            group_merge2(tm);
+            t = tm.t;
+            kG = tm.m;
           } else {
             scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
             group_merge<LPQ>(t);
@@ -2848,11 +2825,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       nb_d5[slot] = (t.k[4] != kInfKey) ? d5 : __int_as_float(0x7f800000);
       // (KC: a certified query keeps the certificate it was certified by)
       qw[slot] = make_float4(qx, qy, qz, KC ? (reused ? -2.0f : kG) : 0.0f);
-      if (KC) {
-        lds.s.kp3[slot][0] = kx5;
-        lds.s.kp3[slot][1] = kx6;
-        lds.s.kp3[slot][2] = kx7;
-      }
     }
     if constexpr (KC) {
       const uint64_t br = __ballot(sub == 0 && live && reused), bs = __ballot(sub == 0 && live && !reused);
@@ -3035,13 +3007,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       out.sel[i] = sel ? 1 : 0;
       out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
       if constexpr (KC) {
-        // this search's certificate: the query, G, the 8 positions
-        if (cfg.kc_epoch && q.w != -2.0f) {
-          out.kq[i] = q;
-          out.kpos[2 * i] = make_uint4(nb_pos[slot][0], nb_pos[slot][1], nb_pos[slot][2], nb_pos[slot][3]);
-          out.kpos[2 * i + 1] =
-              make_uint4(nb_pos[slot][4], lds.s.kp3[slot][0], lds.s.kp3[slot][1], lds.s.kp3[slot][2]);
-        }
+        // this search's certificate: the query and G (its 5 go to nbr_pos)
+        if (cfg.kc_epoch && q.w != -2.0f) out.kq[i] = q;
       }
       if (sel) {
         double h[12];
@@ -3360,9 +3327,8 @@ struct Ctx {
   double* chunk_part = nullptr;
   uint32_t* chunk_cost = nullptr;  // per chunk of the last search pass (chunk_order)
   // kNN certificates of the device-resident update (k_search_pass): per point
-  // query + bound, 8 positions; per chunk the update epoch they belong to
+  // query + bound (the 5 positions are nbr_pos); per chunk the update epoch
   float4* kq = nullptr;
-  uint4* kpos = nullptr;
   uint32_t* kepoch = nullptr;
   uint32_t kc_next = 0;       // last epoch handed out
   uint32_t kc_epoch = 0;      // the running update's (0: certificates off)
@@ -3574,10 +3540,8 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->chunk_perm);
   c->chunk_cost = c->chunk_perm = nullptr;
   (void)hipFree(c->kq);
-  (void)hipFree(c->kpos);
   (void)hipFree(c->kepoch);
   c->kq = nullptr;
-  c->kpos = nullptr;
   c->kepoch = nullptr;
   c->bx = c->by = c->bz = nullptr;
   c->nbr_idx = nullptr;
@@ -3715,7 +3679,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   if (!devpose) c.kc_version = c.map->version;
   cfg.kc_epoch = (devpose && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
   PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,  c.sel,    c.resid,
-            c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq, c.kpos,
+            c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq,
             c.kepoch,     c.kc_stats ? c.count + kKcCount : nullptr};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
@@ -4437,7 +4401,7 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
         (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc)) ||
-        (e = hipMalloc(&c.kq, 16 * cap)) || (e = hipMalloc(&c.kpos, 32 * cap)) ||
+        (e = hipMalloc(&c.kq, 16 * cap)) ||
         (e = hipMalloc(&c.kepoch, 4 * capc)) || (e = hipMemset(c.kepoch, 0, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));

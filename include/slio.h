@@ -469,7 +469,7 @@ int slio_debug_host_stamps(slio_handle h, int enable, int64_t out[8]);
  * call, which turns it on for the handle -- it costs two same-address atomics
  * per workgroup):
  * out[0] queries whose 5 nearest a later pass certified from its earlier
- * search's 8 nearest, out[1] queries searched in full in passes that write
+ * search's 5 nearest and bound, out[1] queries searched in full in passes that write
  * certificates (device-resident passes after the first). */
 int slio_debug_knn_cert(slio_handle h, uint32_t out[2]);
 

@@ -374,9 +374,9 @@ def _cert_counts(L, h):
     (100_000, 1, 0, 4), (100_000, 0, 0, 3), (100_000, 0, 0, 4), (100_000, 1, 1, 4), (20_013, 1, 0, 4),
     (8_191, 1, 0, 4)])
 def test_knn_certificate_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
-    """kNN certificates: a device-resident pass after the update's first takes
-    a query's 5 nearest from its earlier search's 8 nearest when the bound on
-    every other map point proves none can enter (k_search_pass).  x, P, the
+    """kNN certificates: a device-resident pass after the update's first keeps
+    a query's 5 nearest from its earlier search when the bound on every other
+    map point proves none can enter (k_search_pass).  x, P, the
     flags, the super rows and the last search's Nearest_Points, distances and
     selection are bit-for-bit those of the same update with every pass
     searching in full (SLIO_NO_KNN_CERT=1): fused passes and (8191 points,
@@ -411,10 +411,11 @@ def test_knn_certificate_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
         assert per[0] == per[1] == per[2]
         if mode == 1:
             # fixed flow: pass 1 searches every query in full (new epoch);
-            # passes 2..maxit-1 certify nearly all of them
+            # passes 2..maxit-1 certify most of them (C2: ~86 % at pass 2,
+            # > 99 % at pass 3)
             cert, srch = per[0]
             assert srch >= npts
-            assert cert >= 0.9 * (maxit - 2) * npts
+            assert cert >= 0.75 * (maxit - 2) * npts
     finally:
         lib.slio_destroy(h)
 
