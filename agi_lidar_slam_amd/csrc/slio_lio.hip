@@ -1963,7 +1963,9 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
     const int rb = r * g.H;
     const int seg = (g.H + 63) / 64;
     const int c0 = min(lane * seg, g.H), c1 = min(c0 + seg, g.H);
-    if (seg <= kLegoCcSeg) {
+    // (rows hold <= 2048 cells: slio_lego_create refuses wider images for
+    // the feature kernels' LDS layout, so a segment is <= kLegoCcSeg cells)
+    {
       // the segment's flags (and its left neighbour's) in registers, every
       // LDS read in flight at once
       uint8_t eb[kLegoCcSeg + 1];
@@ -1990,27 +1992,6 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
         if ((eb[k] & 4) && !(eb[k - 1] & 1)) cur = rb + col;
         if (col < c1) par[rb + col] = (eb[k] & 4) ? cur : -1;
       }
-      continue;
-    }
-    auto starts_run = [&](int col) {
-      const int e = edg[rb + col];
-      return (e & 4) && !(col > 0 && (edg[rb + col - 1] & 1));
-    };
-    int last = -1;
-    for (int col = c0; col < c1; ++col)
-      if (starts_run(col)) last = rb + col;
-    int v = last;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(v, o, 64);
-      if (lane >= o) v = max(v, u);
-    }
-    int cur = __shfl_up(v, 1, 64);
-    if (lane == 0) cur = -1;
-    for (int col = c0; col < c1; ++col) {
-      const int e = edg[rb + col];
-      if (starts_run(col)) cur = rb + col;
-      par[rb + col] = (e & 4) ? cur : -1;
     }
   }
   __syncthreads();
@@ -2096,6 +2077,260 @@ __global__ __launch_bounds__(kLegoCcThreads) void k_lego_cc(LGeo g, const uint8_
     }
   }
   CCSTAMP(6);
+}
+
+// ---- labelComponents in column bands (round 5): the one-workgroup kernel
+// above runs the whole image on one CU (~34 us a VLP-16 sweep).  Here band b
+// (64 columns, all rows; one workgroup per band, grid ceil(H / 64)) forms its
+// cells' edge bits (k_lego_edges' tests), links its row runs (a prefix max
+// over the band's lanes), unites its vertical edges in LDS (union by the
+// smaller cell index, path halving) and counts each band-local component's
+// cells and row bits.  A band-local root is its component's smallest cell in
+// the band; parent[] of every cell points at it (a global cell index).  The
+// components a horizontal edge joins across a band seam (and across the
+// column wrap H - 1 -> 0) are merged by the LAST band workgroup to arrive: the
+// seam cells' local roots, sizes and row bits are handed over as records
+// (write-through stores, drained, one arrival add; the last arriver loads
+// them write-through, MI355X_MICROARCH.md inter-workgroup visibility), united
+// in an LDS hash table by the smaller cell index, and each absorbed local root
+// is linked below its component's root (parent[lr] = root, a smaller index:
+// uf_find in the later kernels follows it), whose size and row bits become the
+// component's.  The root of a component is its smallest cell index overall --
+// the reference's label order (first row-major cell) -- and sizes and row
+// sets (every cell's row but the seed's, :373) are the one-workgroup kernel's,
+// so every later kernel is unchanged.  Rows <= 64.
+constexpr int kLegoBandW = 64;
+constexpr int kLegoBandThreads = 256;
+constexpr int kLegoBandMaxRows = 64;
+struct LegoSeamRec {
+  int32_t root;   // the seam cell's band-local root (global cell index), -1: no cell
+  int32_t size;   // that local component's cells
+  uint64_t rows;  // its cells' rows, the local root's own row excluded
+};
+// the band kernel's limits: rows <= 64, the merge's hash at most half full
+inline bool lego_band_ok(const LGeo& g) {
+  const int64_t nb = (g.H + kLegoBandW - 1) / kLegoBandW;
+  return g.N >= 1 && g.N <= kLegoBandMaxRows && g.H >= 2 && 4 * nb * g.N <= (int64_t)kLegoBandMaxRows * kLegoBandW;
+}
+__device__ __forceinline__ bool lego_valid(const int32_t* owner, const int8_t* ground, int64_t c) {
+  return owner[c] >= 0 && ground[c] != 1;
+}
+
+__global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
+    LGeo g, const int32_t* __restrict__ owner, const int8_t* __restrict__ ground,
+    const float* __restrict__ range_mat, int32_t* __restrict__ parent, int32_t* __restrict__ csize,
+    unsigned long long* __restrict__ rows, LegoSeamRec* __restrict__ seam, uint32_t* __restrict__ arrive_ctr) {
+  constexpr int W = kLegoBandW;
+  constexpr int kRowsPerWave = kLegoBandMaxRows / (kLegoBandThreads / 64);
+  __shared__ int lpar[kLegoBandMaxRows * W];
+  __shared__ int lcnt[kLegoBandMaxRows * W];
+  __shared__ unsigned long long lrow[kLegoBandMaxRows * W];
+  __shared__ uint8_t le[kLegoBandMaxRows * W];
+  __shared__ int s_last;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int N = g.N, H = g.H;
+  const int nb = (H + W - 1) / W;
+  const int band = blockIdx.x;
+  const int col = band * W + lane;
+  const bool incol = col < H;
+  // 1. the band's edge bits: 4 valid, 1 right neighbour (column wrap), 2 below
+  for (int r = w; r < N; r += kLegoBandThreads / 64) {
+    const int64_t c = (int64_t)r * H + col;
+    uint8_t e = 0;
+    if (incol && lego_valid(owner, ground, c)) {
+      e = 4;
+      const float rc = range_mat[c];
+      const int64_t cr = (col + 1 < H ? col + 1 : 0) + (int64_t)r * H;
+      if (cr != c && lego_valid(owner, ground, cr) && lego_edge(g, rc, range_mat[cr], true)) e |= 1;
+      if (r + 1 < N && lego_valid(owner, ground, c + H) && lego_edge(g, rc, range_mat[c + H], false)) e |= 2;
+    }
+    le[r * W + lane] = e;
+    lcnt[r * W + lane] = 0;
+    lrow[r * W + lane] = 0ull;
+  }
+  __syncthreads();
+  // 2. row runs inside the band: every cell of a run points at its first cell
+  for (int r = w; r < N; r += kLegoBandThreads / 64) {
+    const int i = r * W + lane;
+    const int e = le[i];
+    const bool st = (e & 4) && !(lane > 0 && (le[i - 1] & 1));
+    int v = st ? lane : -1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o, 64);
+      if (lane >= o) v = max(v, u);
+    }
+    lpar[i] = (e & 4) ? r * W + v : -1;
+  }
+  __syncthreads();
+  // 3. vertical edges (only the first of a stretch of parallel ones)
+  for (int r = w; r < N; r += kLegoBandThreads / 64) {
+    const int i = r * W + lane;
+    const int e = le[i];
+    const bool vert = (e & 2) && !(lane > 0 && (le[i - 1] & 3) == 3 && (le[i - 1 + W] & 1));
+    if (vert) cc_unite(lpar, i, i + W);
+  }
+  __syncthreads();
+  // 4. band-local roots, sizes and row bits (the root's own row excluded)
+  int root[kRowsPerWave];
+#pragma unroll
+  for (int k = 0; k < kRowsPerWave; ++k) {
+    const int r = w + k * (kLegoBandThreads / 64);
+    const int i = r * W + lane;
+    root[k] = (r < N && lds_ld(lpar + i) >= 0) ? cc_find(lpar, i) : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRowsPerWave; ++k) {
+    const int r = w + k * (kLegoBandThreads / 64);
+    const int i = r * W + lane;
+    if (root[k] >= 0) {
+      atomicAdd(&lcnt[root[k]], 1);
+      if (root[k] != i) atomicOr(&lrow[root[k]], 1ull << r);
+    }
+  }
+  __syncthreads();
+  auto gidx = [&](int li) { return (int32_t)((li / W) * H + band * W + (li % W)); };
+#pragma unroll
+  for (int k = 0; k < kRowsPerWave; ++k) {
+    const int r = w + k * (kLegoBandThreads / 64);
+    if (r >= N || !incol) continue;
+    const int i = r * W + lane;
+    const int64_t c = (int64_t)r * H + col;
+    parent[c] = root[k] >= 0 ? gidx(root[k]) : -1;
+    if (root[k] == i) {
+      csize[c] = lcnt[i];
+      rows[2 * c] = lrow[i];
+      rows[2 * c + 1] = 0ull;
+    }
+    // the seam records: the band's first (side 0) and last (side 1) column,
+    // per row (a one-column band writes both)
+    const int last = min(W, H - band * W) - 1;
+    LegoSeamRec rec{-1, 0, 0ull};
+    if (root[k] >= 0) rec = LegoSeamRec{gidx(root[k]), lcnt[root[k]], lrow[root[k]]};
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      if (lane != (side == 0 ? 0 : last)) continue;
+      LegoSeamRec* dst = seam + ((int64_t)band * 2 + side) * N + r;
+      __hip_atomic_store(&dst->root, rec.root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dst->size, rec.size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dst->rows, rec.rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // 5. arrival (after every wave's stores have completed); the last band merges
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(arrive_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (t == 0) __hip_atomic_store(arrive_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  // merge: an LDS hash of the seam records' roots (key: cell index), union by
+  // the smaller key across the horizontal seam edges, then each absorbed local
+  // root below its component's root.  (The band arrays are reused.)
+  constexpr int kHash = kLegoBandMaxRows * W;  // >= 2 x N seam records per band for nb <= 32 bands
+  int* hkey = lcnt;                            // key or -1
+  int* hpar = lpar;                            // union-find over slots
+  unsigned long long* hrow = lrow;             // the slot's record rows; then the component's
+  __shared__ int hsize[kHash];
+  __shared__ int hacc[kHash];
+  const int nrec = nb * 2 * N;
+  for (int s = t; s < kHash; s += kLegoBandThreads) {
+    hkey[s] = -1;
+    hacc[s] = 0;
+  }
+  __syncthreads();
+  auto slot_of = [&](int32_t key, bool insert) {
+    uint32_t hsh = ((uint32_t)key * 2654435761u) & (kHash - 1);
+    while (true) {
+      const int k = lds_ld(hkey + hsh);
+      if (k == key) return (int)hsh;
+      if (k == -1) {
+        if (!insert) return -1;
+        const int old = atomicCAS(hkey + hsh, -1, key);
+        if (old == -1 || old == key) return (int)hsh;
+      }
+      hsh = (hsh + 1) & (kHash - 1);
+    }
+  };
+  for (int q = t; q < nrec; q += kLegoBandThreads) {
+    const LegoSeamRec* src = seam + q;
+    const int32_t key = __hip_atomic_load(&src->root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (key < 0) continue;
+    const int s = slot_of(key, true);
+    hsize[s] = __hip_atomic_load(&src->size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hrow[s] = __hip_atomic_load(&src->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hpar[s] = s;
+  }
+  __syncthreads();
+  // union-find over slots, the root slot keeps the smallest key
+  auto sfind = [&](int s) {
+    int p = lds_ld(hpar + s);
+    while (p != s) {
+      const int gp = lds_ld(hpar + p);
+      if (gp != p) __hip_atomic_store(hpar + s, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      s = p;
+      p = gp;
+    }
+    return s;
+  };
+  // seam k: band k's last column -> band (k + 1) % nb's first column, every row
+  for (int q = t; q < nb * N; q += kLegoBandThreads) {
+    const int k = q / N, r = q - k * N;
+    const int k2 = k + 1 < nb ? k + 1 : 0;
+    const int colL = min((k + 1) * W, H) - 1, colR = k2 * W;
+    const int64_t cL = (int64_t)r * H + colL, cR = (int64_t)r * H + colR;
+    if (cL == cR || !lego_valid(owner, ground, cL) || !lego_valid(owner, ground, cR) ||
+        !lego_edge(g, range_mat[cL], range_mat[cR], true))
+      continue;
+    const int32_t kl = __hip_atomic_load(&seam[((int64_t)k * 2 + 1) * N + r].root, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t kr = __hip_atomic_load(&seam[((int64_t)k2 * 2) * N + r].root, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    int a = slot_of(kl, false), b = slot_of(kr, false);
+    while (true) {
+      a = sfind(a);
+      b = sfind(b);
+      if (a == b) break;
+      if (hkey[a] > hkey[b]) {
+        const int tmp = a;
+        a = b;
+        b = tmp;
+      }
+      const int old = atomicCAS(hpar + b, b, a);  // the larger key's root below the smaller's
+      if (old == b) break;
+      b = old;
+    }
+  }
+  __syncthreads();
+  // each slot into its component's root: sizes, row bits (an absorbed local
+  // root's own row counts: it is not the component's seed), parent links
+  int rs[kHash / kLegoBandThreads];
+#pragma unroll
+  for (int u = 0; u < kHash / kLegoBandThreads; ++u) {
+    const int s = t + u * kLegoBandThreads;
+    rs[u] = hkey[s] >= 0 ? sfind(s) : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kHash / kLegoBandThreads; ++u) {
+    const int s = t + u * kLegoBandThreads;
+    if (rs[u] < 0 || rs[u] == s) continue;
+    const int32_t key = hkey[s], rk = hkey[rs[u]];
+    atomicAdd(&hacc[rs[u]], hsize[s]);
+    atomicOr(&hrow[rs[u]], hrow[s] | (1ull << (key / H)));
+    parent[key] = rk;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kHash / kLegoBandThreads; ++u) {
+    const int s = t + u * kLegoBandThreads;
+    if (rs[u] == s && hacc[s] > 0) {
+      const int32_t key = hkey[s];
+      csize[key] = hsize[s] + hacc[s];
+      rows[2 * (int64_t)key] = hrow[s];
+    }
+  }
 }
 
 __device__ __forceinline__ bool lego_feasible(const LGeo& g, const int32_t* csize,
@@ -2549,6 +2784,9 @@ struct slio_lego {
   LegoImuDev imu{};
   int imu_last_host = 0;
   bool cc_global = false;  // labelComponents by k_lego_union / k_lego_compress
+  bool cc_lds1 = false;    // labelComponents by the one-workgroup k_lego_cc (SLIO_LEGO_CC_LDS1)
+  LegoSeamRec* seam = nullptr;  // k_lego_cc_band's seam records
+  uint32_t* cc_arrive = nullptr;
   // image / segmentation
   int32_t* owner = nullptr;
   float* range_mat = nullptr;
@@ -2614,7 +2852,7 @@ void lego_free(slio_lego* h) {
                  h->slot, h->desk, h->io, h->curvature, h->picked0, h->flabel, h->corner_stage,
                  h->corner_sharp, h->corner_count, h->sharp_count, h->flat_count, h->surf_count,
                  h->flat_stage, h->surf_stage, h->c_sharp, h->c_less_sharp, h->c_flat,
-                 h->c_less_flat, h->counts};
+                 h->c_less_flat, h->counts, h->seam, h->cc_arrive};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   feat_work_free(h->fw);
@@ -2769,6 +3007,19 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   {
     const char* cg = std::getenv("SLIO_LEGO_CC_GLOBAL");
     h->cc_global = cg && cg[0] && cg[0] != '0';
+    const char* c1 = std::getenv("SLIO_LEGO_CC_LDS1");
+    h->cc_lds1 = c1 && c1[0] && c1[0] != '0';
+  }
+  if (lego_band_ok(h->g)) {
+    const int nb = (h->g.H + kLegoBandW - 1) / kLegoBandW;
+    if (hipMalloc(&h->seam, sizeof(LegoSeamRec) * 2 * (size_t)nb * h->g.N) != hipSuccess ||
+        hipMalloc(&h->cc_arrive, sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(h->cc_arrive, 0, sizeof(uint32_t)) != hipSuccess) {
+      set_error("slio_lego_create: out of device memory");
+      lego_free(h);
+      delete h;
+      return SLIO_ENOMEM;
+    }
   }
   if (h->cells <= kLegoCcCells) {
     // the attribute is the kernel's, for the whole process: set once to the
@@ -2885,9 +3136,12 @@ int slio_lego_run_async(slio_lego_handle h) {
   const LGeo& g = h->g;
   const int R = g.N;
   const unsigned cb = (unsigned)((g.cells + 255) / 256);
-  const bool cc_lds = g.cells <= kLegoCcCells && !h->cc_global;
+  // labelComponents: column bands (default), one workgroup's LDS, or global
+  // atomics (SLIO_LEGO_CC_LDS1 / SLIO_LEGO_CC_GLOBAL; all give the same labels)
+  const bool cc_band = h->seam && !h->cc_global && !h->cc_lds1;
+  const bool cc_lds = !cc_band && g.cells <= kLegoCcCells && !h->cc_global;
   LIO_HIP(hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream));
-  if (!cc_lds) {
+  if (!cc_lds && !cc_band) {
     LIO_HIP(hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream));
     LIO_HIP(hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream));
   }
@@ -2895,8 +3149,12 @@ int slio_lego_run_async(slio_lego_handle h) {
     k_lego_claim<<<(unsigned)((h->n + 255) / 256), 256, 0, h->stream>>>(h->x, h->y, h->z, h->n, g,
                                                                           h->owner);
   k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, h->owner, h->range_mat, h->full, h->ground);
-  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, h->owner, h->full, h->ground, h->parent, !cc_lds);
-  if (cc_lds) {
+  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, h->owner, h->full, h->ground, h->parent,
+                                                           !cc_lds && !cc_band);
+  if (cc_band) {
+    k_lego_cc_band<<<(g.H + kLegoBandW - 1) / kLegoBandW, kLegoBandThreads, 0, h->stream>>>(
+        g, h->owner, h->ground, h->range_mat, h->parent, h->csize, h->rows, h->seam, h->cc_arrive);
+  } else if (cc_lds) {
     k_lego_edges<<<cb, 256, 0, h->stream>>>(g, h->owner, h->ground, h->range_mat, h->edges, h->csize, h->rows);
     k_lego_cc<<<1, kLegoCcThreads, 5 * g.cells, h->stream>>>(g, h->edges, h->parent, h->csize, h->rows);
   } else {

@@ -73,12 +73,16 @@ def check_features(oracle_mod, fe, si, P, imu=None, t0=0.0):
     return got
 
 
-@pytest.mark.parametrize("with_imu,cc", [(False, "lds"), (True, "lds"), (False, "global")])
+@pytest.mark.parametrize("with_imu,cc", [(False, "band"), (True, "band"), (False, "lds1"), (False, "global")])
 def test_vlp16_sweep_bitexact(oracle_mod, with_imu, cc, monkeypatch):
-    """cc: labelComponents by the one-workgroup LDS union-find (k_lego_cc, the
-    default when the image fits) or the global-atomic kernels."""
+    """cc: labelComponents in 64-column bands with a last-arriver seam merge
+    (k_lego_cc_band, the default for <= 64 rows), by the one-workgroup LDS
+    union-find (k_lego_cc, SLIO_LEGO_CC_LDS1) or by the global-atomic kernels
+    (SLIO_LEGO_CC_GLOBAL): the same labels."""
     if cc == "global":
         monkeypatch.setenv("SLIO_LEGO_CC_GLOBAL", "1")
+    if cc == "lds1":
+        monkeypatch.setenv("SLIO_LEGO_CC_LDS1", "1")
     from agi_lidar_slam_amd import synth
     from agi_lidar_slam_amd.lego import LegoImu, LegoParams
     P = LegoParams()
@@ -97,10 +101,17 @@ def test_vlp16_sweep_bitexact(oracle_mod, with_imu, cc, monkeypatch):
         fe.close()
 
 
+@pytest.mark.parametrize("cc", ["band", "lds1"])
 @pytest.mark.parametrize("seed,n_scan,horizon,res_y,shuffle,dup", [
     (3, 16, 360, 2.0, False, 0.1), (4, 16, 240, 2.0, True, 0.3), (5, 32, 1024, 1.0, True, 0.05),
-    (6, 64, 2048, 0.5, False, 0.0), (7, 8, 97, 4.0, False, 0.2)])
-def test_small_sweeps(oracle_mod, seed, n_scan, horizon, res_y, shuffle, dup):
+    (6, 64, 2048, 0.5, False, 0.0), (7, 8, 97, 4.0, False, 0.2), (9, 4, 65, 8.0, True, 0.2)])
+def test_small_sweeps(oracle_mod, seed, n_scan, horizon, res_y, shuffle, dup, cc, monkeypatch):
+    """Geometries beside VLP-16's, each labelComponents path: bands (default
+    where it applies: <= 64 rows; 97 and 65 columns leave a narrow last band,
+    the column wrap crosses a seam; 64 x 2048 is past the bands' merge table
+    and takes the global kernels) or the one-workgroup LDS kernel."""
+    if cc == "lds1":
+        monkeypatch.setenv("SLIO_LEGO_CC_LDS1", "1")
     from agi_lidar_slam_amd.lego import LegoParams
     P = LegoParams(N_SCAN=n_scan, Horizon_SCAN=horizon, ang_res_x=360.0 / horizon, ang_res_y=res_y,
                    groundScanInd=min(7, n_scan - 1))
