@@ -754,7 +754,25 @@ __device__ __forceinline__ void top5m_insert(Top5M& a, uint64_t key) {
   top5_insert(a.t, key);
 }
 
+// the same with the 6th entry kept (kNN certificates: the writer's list)
+struct Top6M {
+  uint64_t k[6];
+  float m;
+};
+
+__device__ __forceinline__ void top6m_insert(Top6M& a, uint64_t key) {
+  const uint64_t drop = key < a.k[5] ? a.k[5] : key;
+  a.m = fminf(a.m, __uint_as_float((uint32_t)(drop >> 32)));
+  bool c[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) c[j] = key < a.k[j];
+#pragma unroll
+  for (int j = 5; j > 0; --j) a.k[j] = c[j - 1] ? a.k[j - 1] : (c[j] ? key : a.k[j]);
+  a.k[0] = c[0] ? key : a.k[0];
+}
+
 __device__ __forceinline__ void list_insert(Top5& t, uint64_t key) { top5_insert(t, key); }
+__device__ __forceinline__ void list_insert(Top6M& t, uint64_t key) { top6m_insert(t, key); }
 __device__ __forceinline__ void list_insert(Top5M& t, uint64_t key) { top5m_insert(t, key); }
 
 __device__ __forceinline__ void consider(Top5& t, const float4 c, uint32_t pos, float qx, float qy,
@@ -791,9 +809,21 @@ __device__ __forceinline__ void merge_round_dpp(Top5M& a) {
   a.m = fminf(a.m, om);
 }
 
+template <int CTRL>
+__device__ __forceinline__ void merge_round_dpp(Top6M& a) {
+  uint64_t ok[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) ok[j] = dpp64<CTRL>(a.k[j]);
+  const float om = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a.m), CTRL, 0xF, 0xF, false));
+#pragma unroll
+  for (int j = 0; j < 6; ++j) top6m_insert(a, ok[j]);
+  a.m = fminf(a.m, om);
+}
+
 // the 2-lane merge of a query pair's lists (both lanes end with the merged
 // list and the union's dropped minimum)
 __device__ __forceinline__ void group_merge2(Top5M& a) { merge_round_dpp<0xB1>(a); }
+__device__ __forceinline__ void group_merge2(Top6M& a) { merge_round_dpp<0xB1>(a); }
 
 // butterfly merge of the LPQ per-lane lists of a query group (lanes of a
 // group are consecutive and aligned, and all active or all inactive).  Up to
@@ -1224,6 +1254,7 @@ struct PassOut {
   // squared-distance bound G of every map point outside its 5 nearest (which
   // nbr_pos holds); per chunk the update epoch the entries belong to
   float4* kq;
+  uint32_t* k6;         // the 6th of the certified set (nbr_pos holds the other 5)
   uint32_t* kepoch;     // per chunk (global index)
   uint32_t* kc_count;   // [0] certified queries, [1] queries searched with a certificate written
 };
@@ -2528,6 +2559,8 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     float nb_d5[SLIO_CHUNK];
     float4 qw[SLIO_CHUNK];            // the query; .w: its certificate bound G (KC, -2: none written)
     uint32_t kc_n[2];                 // KC: certified queries, searched queries
+    uint32_t kx6[SLIO_CHUNK];         // KC: the 6th of the point's certified set
+    uint8_t ksame[SLIO_CHUNK];        // KC: certified in the last pass's order (plane reusable)
     // deferred (far) queries of this chunk and the far workers' scratch
     int far_cnt, ref_cnt;
     uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
@@ -2608,15 +2641,16 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     const int64_t i = chunk * SLIO_CHUNK + slot;
     const bool live = i < scan.n;
     float qx = 0.0f, qy = 0.0f, qz = 0.0f;
-    // KC: the point's certificate (earlier query + bound, and this lane's share
-    // of its 5 positions), loaded with the scan point: no dependent round trip
+    // KC: the point's certificate (earlier query + bound) and its 6 positions
+    // (the last pass's 5 in order, then the 6th), loaded with the scan point:
+    // no dependent round trip
     float4 ka = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-    uint32_t kp[3] = {~0u, ~0u, ~0u};  // this lane's share of the 5: 0..2 (sub 0), 3..4 (sub 1)
+    uint32_t kp[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
     if (KC && cache_ok && live) {
       ka = out.kq[i];
-      kp[0] = out.nbr_pos[5 * i + 3 * sub];
-      kp[1] = out.nbr_pos[5 * i + 3 * sub + 1];
-      if (sub == 0) kp[2] = out.nbr_pos[5 * i + 2];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) kp[j] = out.nbr_pos[5 * i + j];
+      kp[5] = out.k6[i];
     }
     if (live) {
       const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
@@ -2630,20 +2664,24 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     bool done = !finite;
     bool refine = false;   // exact 5x5x5 refinement wanted (lim = refine bound)
     float lim = 0.0f;
-    // kNN certificate (KC).  A full search on the block rows keeps the 5
-    // nearest and the smallest squared distance it dropped (Top5M), so every
-    // other map point lies at squared distance >= G = min(dropped, b1^2)
-    // (b1: the block faces' bound) from that query, less a 2e-5 relative
-    // margin for float rounding -- a bound on the TRUE squared distance.  A
-    // later pass of the same update, its query moved by delta <= |q - q_old|,
-    // evaluates the 5 (nbr_pos: a certified pass rewrites the same set) at
-    // the new query; if (sqrt(G) - delta)^2 (1 - 1e-5) exceeds the new 5th
-    // squared distance, no other point can enter the top 5 (its float
-    // distance is strictly larger), so the 5 sorted by key ARE the exact
-    // search's result, tie order included (same keys).  Otherwise the query
-    // searches.
+    // kNN certificate (KC).  A full search on the block rows keeps the 6
+    // nearest and the smallest squared distance it dropped (Top6M), so every
+    // map point outside the 6 lies at squared distance >= G = min(dropped,
+    // b1^2) (b1: the block faces' bound) from that query, less a 2e-5
+    // relative margin for float rounding -- a bound on the TRUE squared
+    // distance.  A later pass of the same update, its query moved by
+    // delta <= |q - q_old|, evaluates the 6 (nbr_pos + k6: a certified pass
+    // rewrites the same set) at the new query; if (sqrt(G) - delta)^2
+    // (1 - 1e-5) exceeds the new 5th squared distance, no point outside the 6
+    // can enter the top 5 (its float distance is strictly larger), so the 5
+    // smallest keys of the 6 ARE the exact search's result, tie order
+    // included (same keys).  Otherwise the query searches.  When the 5 come
+    // out in the last pass's order, esti_plane's input is the same and its
+    // plane is reused (the fit phase).
     bool reused = false;
-    float kG = -1.0f;  // this search's certificate bound (-1: none)
+    bool same5 = false;    // certified, in the last pass's order
+    float kG = -1.0f;      // this search's certificate bound (-1: none)
+    uint32_t kx6 = ~0u;    // the 6th position this pass leaves
     if constexpr (KC) {
       // (branch-free up to the gathers, so the certificate loads stay whole)
       const double ex0 = (double)qx - (double)ka.x, ey0 = (double)qy - (double)ka.y,
@@ -2653,17 +2691,20 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       if (cache_ok && finite && ka.w > 0.0f) {
         {
           if (A > 0.0) {
-            // the pair's lanes take 3 + 2 of the 5, then merge (as a search)
+            // the pair's lanes take 3 of the 6 each, then merge (as a search)
+            uint32_t ps[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) ps[j] = sub == 0 ? kp[j] : kp[3 + j];
             float4 cc[3];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) cc[j] = pts[kp[j] != ~0u ? kp[j] : 0u];
+            for (int j = 0; j < 3; ++j) cc[j] = pts[ps[j] != ~0u ? ps[j] : 0u];
             Top5 tr;
             top5_clear(tr);
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               const float ddx = qx - cc[j].x, ddy = qy - cc[j].y, ddz = qz - cc[j].z;
               const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;  // calc_dist, ikd_Tree.cpp:1539-1544
-              top5_insert(tr, kp[j] != ~0u ? (((uint64_t)__float_as_uint(d) << 32) | (uint64_t)kp[j]) : kInfKey);
+              top5_insert(tr, ps[j] != ~0u ? (((uint64_t)__float_as_uint(d) << 32) | (uint64_t)ps[j]) : kInfKey);
             }
             group_merge<2>(tr);
             if (tr.k[4] != kInfKey &&
@@ -2671,6 +2712,17 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
               t = tr;
               reused = true;
               done = true;
+              same5 = true;
+#pragma unroll
+              for (int j = 0; j < 5; ++j) same5 = same5 && (uint32_t)tr.k[j] == kp[j];
+              // the one of the 6 left out of the 5 (the set stays the same)
+#pragma unroll
+              for (int j = 0; j < 6; ++j) {
+                bool in5 = false;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) in5 = in5 || (uint32_t)tr.k[q] == kp[j];
+                if (!in5) kx6 = kp[j];
+              }
             }
           }
         }
@@ -2700,10 +2752,15 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
             printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
 #endif
           if (KC && cfg.kc_epoch) {
-            Top5M tm{t, __int_as_float(0x7f800000)};
+            Top6M tm;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) tm.k[j] = kInfKey;
+            tm.m = __int_as_float(0x7f800000);
             scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, tm);
             group_merge2(tm);
-            t = tm.t;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) t.k[j] = tm.k[j];
+            kx6 = (uint32_t)tm.k[5];
             kG = tm.m;
           } else {
             scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
@@ -2825,6 +2882,10 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       nb_d5[slot] = (t.k[4] != kInfKey) ? d5 : __int_as_float(0x7f800000);
       // (KC: a certified query keeps the certificate it was certified by)
       qw[slot] = make_float4(qx, qy, qz, KC ? (reused ? -2.0f : kG) : 0.0f);
+      if (KC) {
+        lds.s.kx6[slot] = kx6;
+        lds.s.ksame[slot] = same5 ? 1 : 0;
+      }
     }
     if constexpr (KC) {
       const uint64_t br = __ballot(sub == 0 && live && reused), bs = __ballot(sub == 0 && live && !reused);
@@ -2973,11 +3034,21 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       float pd2 = __int_as_float(0x7fc00000);
       const float4 q = qw[slot];
       const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
+      // KC: certified with the last pass's 5 in the same order -- the same
+      // esti_plane input, so its plane (when it had one) is reused
+      bool rp = false;
+      float4 cpl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if constexpr (KC) {
+        if (lds.s.ksame[slot]) {
+          cpl = out.plane[i];
+          rp = isfinite(cpl.x) && isfinite(cpl.y) && isfinite(cpl.z) && isfinite(cpl.w);
+        }
+      }
       // the 5 neighbours: coordinates for the fit, map index for
       // Nearest_Points (-1 when the map has fewer than 5 points)
       float nb[5][3];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
+      for (int j = 0; j < 5 && !rp; ++j) {
         const uint32_t ps = nb_pos[slot][j];
         float4 c = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
 #ifdef SLIO_BOUNDS_CHECK
@@ -2994,7 +3065,13 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb_idx[slot][j] = (int32_t)__float_as_uint(c.w);
       }
       if (cfg.knn_only) sel = false;
-      if (sel) {
+      if (sel && rp) {
+        abcd[0] = cpl.x;
+        abcd[1] = cpl.y;
+        abcd[2] = cpl.z;
+        abcd[3] = cpl.w;
+        sel = residual_gate(abcd, q.x, q.y, q.z, bx, by, bz, pd2);
+      } else if (sel) {
         float pl[4];
         sel = esti_plane_dev(nb, cfg.plane_thr, pl);
         if (sel) {
@@ -3007,8 +3084,12 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
       out.sel[i] = sel ? 1 : 0;
       out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
       if constexpr (KC) {
-        // this search's certificate: the query and G (its 5 go to nbr_pos)
-        if (cfg.kc_epoch && q.w != -2.0f) out.kq[i] = q;
+        // this search's certificate: the query and G (its 5 go to nbr_pos),
+        // and the 6th (a certified pass's: the one of the 6 left out)
+        if (cfg.kc_epoch) {
+          if (q.w != -2.0f) out.kq[i] = q;
+          out.k6[i] = lds.s.kx6[slot];
+        }
       }
       if (sel) {
         double h[12];
@@ -3329,6 +3410,7 @@ struct Ctx {
   // kNN certificates of the device-resident update (k_search_pass): per point
   // query + bound (the 5 positions are nbr_pos); per chunk the update epoch
   float4* kq = nullptr;
+  uint32_t* k6 = nullptr;
   uint32_t* kepoch = nullptr;
   uint32_t kc_next = 0;       // last epoch handed out
   uint32_t kc_epoch = 0;      // the running update's (0: certificates off)
@@ -3540,8 +3622,10 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->chunk_perm);
   c->chunk_cost = c->chunk_perm = nullptr;
   (void)hipFree(c->kq);
+  (void)hipFree(c->k6);
   (void)hipFree(c->kepoch);
   c->kq = nullptr;
+  c->k6 = nullptr;
   c->kepoch = nullptr;
   c->bx = c->by = c->bz = nullptr;
   c->nbr_idx = nullptr;
@@ -3679,7 +3763,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   if (!devpose) c.kc_version = c.map->version;
   cfg.kc_epoch = (devpose && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
   PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,  c.sel,    c.resid,
-            c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq,
+            c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq, c.k6,
             c.kepoch,     c.kc_stats ? c.count + kKcCount : nullptr};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
@@ -4401,7 +4485,7 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.sel, cap)) || (e = hipMalloc(&c.resid, 4 * cap)) ||
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
         (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc)) ||
-        (e = hipMalloc(&c.kq, 16 * cap)) ||
+        (e = hipMalloc(&c.kq, 16 * cap)) || (e = hipMalloc(&c.k6, 4 * cap)) ||
         (e = hipMalloc(&c.kepoch, 4 * capc)) || (e = hipMemset(c.kepoch, 0, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));

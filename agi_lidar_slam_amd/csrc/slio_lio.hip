@@ -1865,7 +1865,23 @@ __device__ unsigned long long g_ccstamp[8];
   do {                                                                         \
     if (threadIdx.x == 0) g_ccstamp[k] = __builtin_amdgcn_s_memrealtime();     \
   } while (0)
+__device__ unsigned long long g_bstamp[64][8];  // k_lego_cc_band: per band
+__device__ unsigned long long g_mstamp[8];      // k_lego_cc_band: the merge
+#define BSTAMP(k)                                                                          \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && blockIdx.x < 64) g_bstamp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define MSTAMP(k)                                                              \
+  do {                                                                         \
+    if (threadIdx.x == 0) g_mstamp[k] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
 #else
+#define BSTAMP(k) \
+  do {            \
+  } while (0)
+#define MSTAMP(k) \
+  do {            \
+  } while (0)
 #define CCSTAMP(k) \
   do {             \
   } while (0)
@@ -2133,22 +2149,71 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
   const int band = blockIdx.x;
   const int col = band * W + lane;
   const bool incol = col < H;
-  // 1. the band's edge bits: 4 valid, 1 right neighbour (column wrap), 2 below
-  for (int r = w; r < N; r += kLegoBandThreads / 64) {
-    const int64_t c = (int64_t)r * H + col;
-    uint8_t e = 0;
-    if (incol && lego_valid(owner, ground, c)) {
-      e = 4;
-      const float rc = range_mat[c];
-      const int64_t cr = (col + 1 < H ? col + 1 : 0) + (int64_t)r * H;
-      if (cr != c && lego_valid(owner, ground, cr) && lego_edge(g, rc, range_mat[cr], true)) e |= 1;
-      if (r + 1 < N && lego_valid(owner, ground, c + H) && lego_edge(g, rc, range_mat[c + H], false)) e |= 2;
+  BSTAMP(0);
+  // 1. the band's cells and the next column (its right neighbours, the
+  // column wrap for the last band) staged in LDS: validity and range, every
+  // global load of the thread in flight at once (a row-by-row loop with
+  // branches on validity was a chain of dependent round trips: ~20 us)
+  {
+    constexpr int kSW = W + 1;
+    constexpr int kPer = (kLegoBandMaxRows * kSW + kLegoBandThreads - 1) / kLegoBandThreads;
+    const int width = min(W, H - band * W);  // the band's columns; column `width` is the next one
+    int32_t ov[kPer];
+    int8_t gv[kPer];
+    float rv[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int q = t + u * kLegoBandThreads;
+      const int r = q / kSW, j = q - r * kSW;
+      const bool in = r < N && j <= width;
+      int cj = band * W + j;
+      if (cj >= H) cj -= H;
+      const int64_t c = in ? (int64_t)r * H + cj : 0;
+      ov[u] = in ? owner[c] : -1;
+      gv[u] = in ? ground[c] : (int8_t)1;
+      rv[u] = in ? range_mat[c] : 0.0f;
     }
-    le[r * W + lane] = e;
-    lcnt[r * W + lane] = 0;
-    lrow[r * W + lane] = 0ull;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int q = t + u * kLegoBandThreads;
+      if (q < kLegoBandMaxRows * kSW) {
+        reinterpret_cast<float*>(lrow)[q] = rv[u];                       // (lrow: free until step 4)
+        reinterpret_cast<uint8_t*>(lcnt)[q] = ov[u] >= 0 && gv[u] != 1;  // (lcnt: likewise)
+      }
+    }
+    __syncthreads();
+    BSTAMP(1);
+    const float* srng = reinterpret_cast<const float*>(lrow);
+    const uint8_t* sval = reinterpret_cast<const uint8_t*>(lcnt);
+    // edge bits: 4 valid, 1 right neighbour (column wrap), 2 below
+    uint8_t ev[kLegoBandMaxRows / (kLegoBandThreads / 64)];
+#pragma unroll
+    for (int k = 0; k < kLegoBandMaxRows / (kLegoBandThreads / 64); ++k) {
+      const int r = w + k * (kLegoBandThreads / 64);
+      uint8_t e = 0;
+      if (r < N && lane < width && sval[r * kSW + lane]) {
+        e = 4;
+        const float rc = srng[r * kSW + lane];
+        // (one column: the right neighbour is the cell itself, no edge)
+        if (H > 1 && sval[r * kSW + lane + 1] && lego_edge(g, rc, srng[r * kSW + lane + 1], true)) e |= 1;
+        if (r + 1 < N && sval[(r + 1) * kSW + lane] && lego_edge(g, rc, srng[(r + 1) * kSW + lane], false))
+          e |= 2;
+      }
+      ev[k] = e;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLegoBandMaxRows / (kLegoBandThreads / 64); ++k) {
+      const int r = w + k * (kLegoBandThreads / 64);
+      if (r < N) {
+        le[r * W + lane] = ev[k];
+        lcnt[r * W + lane] = 0;
+        lrow[r * W + lane] = 0ull;
+      }
+    }
   }
   __syncthreads();
+  BSTAMP(2);
   // 2. row runs inside the band: every cell of a run points at its first cell
   for (int r = w; r < N; r += kLegoBandThreads / 64) {
     const int i = r * W + lane;
@@ -2163,6 +2228,7 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
     lpar[i] = (e & 4) ? r * W + v : -1;
   }
   __syncthreads();
+  BSTAMP(3);
   // 3. vertical edges (only the first of a stretch of parallel ones)
   for (int r = w; r < N; r += kLegoBandThreads / 64) {
     const int i = r * W + lane;
@@ -2171,6 +2237,7 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
     if (vert) cc_unite(lpar, i, i + W);
   }
   __syncthreads();
+  BSTAMP(4);
   // 4. band-local roots, sizes and row bits (the root's own row excluded)
   int root[kRowsPerWave];
 #pragma unroll
@@ -2217,13 +2284,16 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
       __hip_atomic_store(&dst->rows, rec.rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  BSTAMP(5);
   // 5. arrival (after every wave's stores have completed); the last band merges
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0)
     s_last = __hip_atomic_fetch_add(arrive_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1;
   __syncthreads();
+  BSTAMP(6);
   if (!s_last) return;
+  MSTAMP(0);
   if (t == 0) __hip_atomic_store(arrive_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
   // merge: an LDS hash of the seam records' roots (key: cell index), union by
   // the smaller key across the horizontal seam edges, then each absorbed local
@@ -2253,14 +2323,29 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
       hsh = (hsh + 1) & (kHash - 1);
     }
   };
-  for (int q = t; q < nrec; q += kLegoBandThreads) {
-    const LegoSeamRec* src = seam + q;
-    const int32_t key = __hip_atomic_load(&src->root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (key < 0) continue;
-    const int s = slot_of(key, true);
-    hsize[s] = __hip_atomic_load(&src->size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    hrow[s] = __hip_atomic_load(&src->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    hpar[s] = s;
+  MSTAMP(1);
+  // (the thread's records first, every load in flight, then the inserts)
+  constexpr int kRecPer = kHash / 2 / kLegoBandThreads;  // nrec <= kHash / 2 (lego_band_ok)
+  {
+    int32_t rk[kRecPer], rsz[kRecPer];
+    uint64_t rrw[kRecPer];
+#pragma unroll
+    for (int u = 0; u < kRecPer; ++u) {
+      const int q = t + u * kLegoBandThreads;
+      const LegoSeamRec* src = seam + (q < nrec ? q : 0);
+      rk[u] = __hip_atomic_load(&src->root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      rsz[u] = __hip_atomic_load(&src->size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      rrw[u] = __hip_atomic_load(&src->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (q >= nrec) rk[u] = -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kRecPer; ++u) {
+      if (rk[u] < 0) continue;
+      const int s = slot_of(rk[u], true);
+      hsize[s] = rsz[u];
+      hrow[s] = rrw[u];
+      hpar[s] = s;
+    }
   }
   __syncthreads();
   // union-find over slots, the root slot keeps the smallest key
@@ -2274,20 +2359,46 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
     }
     return s;
   };
-  // seam k: band k's last column -> band (k + 1) % nb's first column, every row
-  for (int q = t; q < nb * N; q += kLegoBandThreads) {
-    const int k = q / N, r = q - k * N;
-    const int k2 = k + 1 < nb ? k + 1 : 0;
-    const int colL = min((k + 1) * W, H) - 1, colR = k2 * W;
-    const int64_t cL = (int64_t)r * H + colL, cR = (int64_t)r * H + colR;
-    if (cL == cR || !lego_valid(owner, ground, cL) || !lego_valid(owner, ground, cR) ||
-        !lego_edge(g, range_mat[cL], range_mat[cR], true))
-      continue;
-    const int32_t kl = __hip_atomic_load(&seam[((int64_t)k * 2 + 1) * N + r].root, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    const int32_t kr = __hip_atomic_load(&seam[((int64_t)k2 * 2) * N + r].root, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    int a = slot_of(kl, false), b = slot_of(kr, false);
+  MSTAMP(2);
+  // seam k: band k's last column -> band (k + 1) % nb's first column, every
+  // row (a seam cell's edge to the right is a band's own test: the seam
+  // cells' loads, all in flight, then the unions)
+  constexpr int kSeamPer = kHash / 4 / kLegoBandThreads;  // nb * N <= kHash / 4 (lego_band_ok)
+  bool sedge[kSeamPer];
+  int32_t skl[kSeamPer], skr[kSeamPer];
+  {
+    int32_t oL[kSeamPer], oR[kSeamPer];
+    int8_t gL[kSeamPer], gR[kSeamPer];
+    float rL[kSeamPer], rR[kSeamPer];
+#pragma unroll
+    for (int u = 0; u < kSeamPer; ++u) {
+      const int q = t + u * kLegoBandThreads;
+      const bool in = q < nb * N;
+      const int k = in ? q / N : 0, r = in ? q - k * N : 0;
+      const int k2 = k + 1 < nb ? k + 1 : 0;
+      const int colL = min((k + 1) * W, H) - 1, colR = k2 * W;
+      const int64_t cL = (int64_t)r * H + colL, cR = (int64_t)r * H + colR;
+      oL[u] = owner[cL];
+      oR[u] = owner[cR];
+      gL[u] = ground[cL];
+      gR[u] = ground[cR];
+      rL[u] = range_mat[cL];
+      rR[u] = range_mat[cR];
+      skl[u] = __hip_atomic_load(&seam[((int64_t)k * 2 + 1) * N + r].root, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      skr[u] = __hip_atomic_load(&seam[((int64_t)k2 * 2) * N + r].root, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      sedge[u] = in && cL != cR;
+    }
+#pragma unroll
+    for (int u = 0; u < kSeamPer; ++u)
+      sedge[u] = sedge[u] && oL[u] >= 0 && gL[u] != 1 && oR[u] >= 0 && gR[u] != 1 &&
+                 lego_edge(g, rL[u], rR[u], true);
+  }
+#pragma unroll
+  for (int u = 0; u < kSeamPer; ++u) {
+    if (!sedge[u]) continue;
+    int a = slot_of(skl[u], false), b = slot_of(skr[u], false);
     while (true) {
       a = sfind(a);
       b = sfind(b);
@@ -2303,6 +2414,7 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
     }
   }
   __syncthreads();
+  MSTAMP(3);
   // each slot into its component's root: sizes, row bits (an absorbed local
   // root's own row counts: it is not the component's seed), parent links
   int rs[kHash / kLegoBandThreads];
@@ -2331,6 +2443,7 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
       rows[2 * (int64_t)key] = hrow[s];
     }
   }
+  MSTAMP(4);
 }
 
 __device__ __forceinline__ bool lego_feasible(const LGeo& g, const int32_t* csize,
@@ -2764,6 +2877,12 @@ __global__ __launch_bounds__(256) void k_lego_concat(int n_scan, const int32_t* 
 using namespace slio::lego;
 
 #ifdef SLIO_FE_STAMP
+extern "C" int slio_dbg_band_stamps(unsigned long long* band, unsigned long long* merge) {
+  return hipMemcpyFromSymbol(band, HIP_SYMBOL(g_bstamp), sizeof(g_bstamp)) == hipSuccess &&
+                 hipMemcpyFromSymbol(merge, HIP_SYMBOL(g_mstamp), sizeof(g_mstamp)) == hipSuccess
+             ? 0
+             : -1;
+}
 extern "C" int slio_dbg_cc_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ccstamp), sizeof(g_ccstamp)) == hipSuccess ? 0 : -1;
 }

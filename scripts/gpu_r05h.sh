@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 tag=${1:-r05h}
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_lego.py > gpurun_out/${tag}_lego_tests.log 2>&1 || { tail -40 gpurun_out/${tag}_lego_tests.log; exit 3; }
 grep -E "passed|failed" gpurun_out/${tag}_lego_tests.log | tail -3
-for cc in band lds1; do
+for cc in band; do
   if [ $cc = lds1 ]; then export SLIO_LEGO_CC_LDS1=1; else unset SLIO_LEGO_CC_LDS1; fi
   timeout -k 10 300 python bench.py --workload lego --steps 300 --warmup 20 --no-cpu-baseline > gpurun_out/${tag}_lego_$cc.json 2>gpurun_out/${tag}_lego_$cc.err || { tail gpurun_out/${tag}_lego_$cc.err; exit 4; }
   python -c "import json; d=json.load(open('gpurun_out/${tag}_lego_$cc.json')); print('$cc', round(d['value']), d['ms_per_step'])"
