@@ -73,6 +73,8 @@ struct IkfCtl {
   int64_t last_m;
   int32_t singular;
   int32_t published;  // mapped host block: set (release, system scope) after x, P and the flags
+  int32_t seq;        // the update's sequence number (a fused group's passes and gates check it)
+  int32_t pad_;
   double pose[32];   // PoseDev of x (rotation matrices formed): the next pass's pose (device only)
   double LM[300];    // Cholesky factor of S = P11i + H^T H / R (D x D), H^T H / R
                      // (upper triangle, 78) and 1 / diag of the factor, of the

@@ -1283,6 +1283,7 @@ struct PassCfg {
   int mfma;                // chunk sums on the matrix cores (chunk_products_mfma), else VALU
   const uint32_t* perm;    // block -> chunk order within each XCD's range (chunk_order), or null
   uint32_t kc_epoch;       // kNN certificates of this update (0: off); see k_search_pass
+  int32_t seq;             // fused group pass: run only if ctl->seq == seq (0: no check)
 };
 
 // ---------------------------------------------------------------- far queries
@@ -1532,6 +1533,7 @@ constexpr int kNSeg = SLIO_NSUPER * kSuperSeg;   // segment rows per pass: one w
 // global-address-space views for the in-launch hand-off (sc1 accesses)
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) uint32_t guint;
+typedef __attribute__((address_space(1))) uint64_t guint64;
 
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2243,21 +2245,28 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
 // staging of the rows).  CTL_SC1: parts of the block were written in this
 // launch (dx_new by block 0 of a fused pass; the whole block by the first
 // fused pass's prefetch), so every control load goes past the L2 (sc1).
-template <int NT, int D, bool CTL_SC1>
+template <int NT, int D, bool CTL_SC1, bool GROUP = false>
 __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, double* super_out, IkfCtl* ctl,
                                            const IkfCtl* src, IkfCtl* hblk, double R, int iter, int maxit) {
   const int t = threadIdx.x;
   if (t < SLIO_NPROD) {
-    double v[kNSeg];
-#pragma unroll
-    for (int e = 0; e < kNSeg; ++e) v[e] = ld_sc1(seg_out + e * SLIO_NPROD + t);
+    // the 8 super rows: from the 64 segment rows, or (GROUP) the ranks' super
+    // rows themselves, formed by the same loop
     double sp[SLIO_NSUPER];
+    if constexpr (GROUP) {
 #pragma unroll
-    for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
-      double a = v[ss * kSuperSeg];
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) sp[ss] = ld_sc1(seg_out + ss * SLIO_NPROD + t);
+    } else {
+      double v[kNSeg];
 #pragma unroll
-      for (int q = 1; q < kSuperSeg; ++q) a = a + v[ss * kSuperSeg + q];
-      sp[ss] = a;
+      for (int e = 0; e < kNSeg; ++e) v[e] = ld_sc1(seg_out + e * SLIO_NPROD + t);
+#pragma unroll
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
+        double a = v[ss * kSuperSeg];
+#pragma unroll
+        for (int q = 1; q < kSuperSeg; ++q) a = a + v[ss * kSuperSeg + q];
+        sp[ss] = a;
+      }
     }
     double a = sp[0];
 #pragma unroll
@@ -2267,8 +2276,9 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
       L.Mt[t] = a / R;
     else if (t < SLIO_NHTH + 12)
       L.hR[t - SLIO_NHTH] = a / R;
+    if (!GROUP)
 #pragma unroll
-    for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
   } else {
     constexpr int NC = NT - SLIO_NPROD, nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
     const int tt = t - SLIO_NPROD;
@@ -2398,6 +2408,13 @@ struct FuseArgs {
   double R;
   int iter, maxit;
   int64_t C;          // chunks of the scan
+  // fused group pass (slio_group_ikf_update, ranks sharing a device): this
+  // rank's segment rows (64 / ranks) and first super-chunk; the group's super
+  // rows and arrival counter (rank 0's); null gsup: a single rank
+  int nrows, s0, granks;
+  double* gsup;
+  uint32_t* garrive;     // [0] the ranks' arrivals; [2..3] gflag (u64): (seq << 32) | done << 31 | passes
+  int32_t gseq;          // the update's sequence number
 };
 constexpr int kSegCnt = 16;
 constexpr int kCountWords = kSegCnt + kNSeg;
@@ -2433,6 +2450,8 @@ __device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, Ik
     st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->converge) + threadIdx.x,
                ld_sys_u32(reinterpret_cast<const uint32_t*>(&hsrc->converge) + threadIdx.x));
   if (threadIdx.x == 8) st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->singular), 0u);
+  if (threadIdx.x == 9)
+    st_sc1_u32(reinterpret_cast<uint32_t*>(&ctl->seq), ld_sys_u32(reinterpret_cast<const uint32_t*>(&hsrc->seq)));
 }
 
 // After the chunk partial is stored (sc1): arrival on the chunk's segment row;
@@ -2480,7 +2499,7 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
 #endif
   if (t == 0) bcast = (int)arrive(fa.cnt);
   __syncthreads();
-  if (bcast != kNSeg - 1) return;
+  if (bcast != fa.nrows - 1) return;
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) {
     ts[3] = wall_clock64();
@@ -2494,7 +2513,45 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     st_sc1_u32(fa.cnt + 4, 0u);
     st_sc1_u32(fa.cnt + 5, 0u);
   }
-  final_step<NT, D, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+  if (!fa.gsup) {
+    final_step<NT, D, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+  } else {
+    // fused group pass: this rank's super rows (its 8 / ranks super-chunks,
+    // each the sum of its 8 segment rows in order: k_super_sums' tree) into
+    // the group's buffer, write-through and drained, then one arrival on the
+    // group's counter; the rank that arrives last runs the filter step on
+    // the 8 super rows (the same sums, the same bits as one rank) for the
+    // whole group: the ranks' next passes read the group's control block
+    const int nsup = SLIO_NSUPER / fa.granks;
+    if (t < SLIO_NPROD) {
+      for (int k = 0; k < nsup; ++k) {
+        const int ss = fa.s0 + k;
+        double a = ld_sc1(fa.seg_out + (ss * kSuperSeg) * SLIO_NPROD + t);
+#pragma unroll
+        for (int q = 1; q < kSuperSeg; ++q) a = a + ld_sc1(fa.seg_out + (ss * kSuperSeg + q) * SLIO_NPROD + t);
+        st_sc1(fa.gsup + ss * SLIO_NPROD + t, a);
+      }
+    }
+    drain_stores();
+    __syncthreads();
+    if (t == 0) bcast = (int)arrive(fa.garrive);
+    __syncthreads();
+    if (bcast != fa.granks - 1) return;
+    if (t == 0) reset_counter(fa.garrive);
+    final_step<NT, D, true, true>(L, fa.gsup, nullptr, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+    // the step's control block (plain stores, possibly on another XCD than
+    // the next passes' readers) out to memory, then the flag the ranks'
+    // gates poll: (seq, done, passes)
+    drain_stores();
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t fl = ((uint64_t)(uint32_t)fa.gseq << 32) | (L.fl[F_DONE] ? 0x80000000ull : 0ull) |
+                          (uint64_t)(uint32_t)L.fl[F_PASSES];
+      __hip_atomic_store((guint64*)(uint64_t*)(fa.garrive + 2), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 #ifdef SLIO_SOLVE_STAMP
   if (t == 0) g_sstamp[25 + ((fa.iter + 1) & 3)] = wall_clock64();  // per pass: the filter step's end
 #endif
@@ -2528,7 +2585,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   // ctl->search_now = converge, esekfom.hpp:138): one launch per pass in the
   // reference control flow too.
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
-                  (!FUSE && cfg.ctl->search_now != cfg.want_search)))
+                  (!FUSE && cfg.ctl->search_now != cfg.want_search) || (cfg.seq && cfg.ctl->seq != cfg.seq)))
     return;
   const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
   constexpr int NT = search_block<LPQ>();
@@ -3426,6 +3483,10 @@ struct Ctx {
   void* comm = nullptr;        // RCCL communicator of the rank group (slio_comm_init / slio_create_group)
   int group_reduce = 0;        // slio_create_group: 1 RCCL communicator, 2 in-device reduce (k_group_reduce)
   hipEvent_t grp_ev = nullptr; // in-device reduce: end of this rank's pass / of the reduce (rank 0)
+  double* gsup = nullptr;      // fused group pass (rank 0): the group's 8 super rows
+  uint32_t* garrive = nullptr; // ... and the ranks' arrival counter
+  int32_t group_seq = 0;       // fused group pass: the running update's sequence number (0: none)
+  int32_t upd_seq = 0;         // (rank 0) last sequence number handed out
   uint32_t* count = nullptr;  // [0] k_super_sums arrival counter, [4..5] far-queue head / tail,
   MapDev::Buf inc[7];         // map_incremental temporaries, kept across scans
                               // (zero between launches)
@@ -3762,6 +3823,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   // rebuilt it in between)
   if (!devpose) c.kc_version = c.map->version;
   cfg.kc_epoch = (devpose && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
+  cfg.seq = fuse ? c.group_seq : 0;
   PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,  c.sel,    c.resid,
             c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq, c.k6,
             c.kepoch,     c.kc_stats ? c.count + kKcCount : nullptr};
@@ -4063,6 +4125,8 @@ int slio_destroy(slio_handle h) {
     if (b.p) (void)hipFree(b.p);
   if (h->c.comm) (void)ncclCommDestroy((ncclComm_t)h->c.comm);
   if (h->c.grp_ev) (void)hipEventDestroy(h->c.grp_ev);
+  (void)hipFree(h->c.gsup);
+  (void)hipFree(h->c.garrive);
   (void)hipFree(h->c.ctl);
   (void)hipHostFree(h->c.h_ctl);
   if (h->c.done_ev) (void)hipEventDestroy(h->c.done_ev);
@@ -7128,8 +7192,15 @@ struct UpdateRun {
         }
         SLIO_HSTAMP(c, 2);
       }
-      const FuseArgs fa{c.ctl, p0 ? (const IkfCtl*)c.d_hctl : nullptr, c.d_seg, c.d_super, c.ctl, c.d_hctl,
-                        c.count, R, i, maxit, num_chunks(c.n)};
+      const FuseArgs fa{c.ctl,   p0 ? (const IkfCtl*)c.d_hctl : nullptr,
+                        c.d_seg, c.d_super,
+                        c.ctl,   c.d_hctl,
+                        c.count, R,
+                        i,       maxit,
+                        num_chunks(c.n), kNSeg,
+                        0,       1,
+                        nullptr, nullptr,
+                        0};
       int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
       if (rc) return rc;
       if (p0) SLIO_HSTAMP(c, 3);
@@ -7160,6 +7231,13 @@ struct UpdateRun {
   // its reuse passes) and with or without extrinsic estimation (D = 12 / 6),
   // given at least 8 chunks per super-chunk (every segment row has a chunk).
   // SLIO_NO_FUSE=1 keeps two launches per pass.
+  // the fused pass's configuration (2 lanes per query, no sphere-first
+  // search, every segment row holds a chunk), whatever the rank count
+  bool fused_ok() const {
+    const int lpq = c.prm.lanes_per_query;
+    return !c.sw.no_fuse && (lpq != 1 && lpq != 4 && lpq != 8) && !(c.prm.search_radius > 0.0f) &&
+           num_chunks(c.n) >= (int64_t)kNSeg;
+  }
   bool fusable() const {
     const bool off = c.sw.no_fuse;
     const int lpq = c.prm.lanes_per_query;
@@ -7223,6 +7301,32 @@ __global__ __launch_bounds__(256) void k_group_reduce(GroupSupers g) {
     double v = g.sup[0][e];
     for (int r = 1; r < g.n; ++r) v = v + g.sup[r][e];
     for (int r = 0; r < g.n; ++r) g.sup[r][e] = v;
+  }
+}
+
+// Fused group pass: between a rank's pass i and i + 1 on its stream, one
+// thread waits until the group's filter step of pass i has run (the group's
+// control block counts the pass, or ends the update, or a newer update owns
+// it: seq).  The last rank to arrive runs that step inside its pass launch
+// (fused_tail), so the wait is for a workgroup that is already running: no
+// workgroup of the next pass occupies the device meanwhile, and the ranks'
+// pass workgroups (<= the scan's chunks) always fit beside the N gates.  A
+// wait past ~1 s gives up (the next pass then exits and the update reports
+// that it did not complete) instead of hanging.
+__global__ __launch_bounds__(64) void k_group_gate(const uint32_t* __restrict__ garrive, int pass_idx, int32_t seq) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (true) {
+    const uint64_t fl = __hip_atomic_load((const guint64*)(const uint64_t*)(garrive + 2), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t fseq = (int32_t)(fl >> 32);
+    const bool done = (fl & 0x80000000ull) != 0;
+    const int32_t passes = (int32_t)(fl & 0x7fffffffull);
+    // this update's step has counted the pass or ended the update, or a newer
+    // update owns the group (a stale gate)
+    if ((fseq == seq && (done || passes >= pass_idx)) || (int32_t)(fseq - seq) > 0) return;
+    if (wall_clock64() - t0 > 100000000ull) return;  // 100 MHz: 1 s
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -7383,6 +7487,17 @@ int slio_create_group(slio_handle* out, int ndev, const int* devices, const slio
         rc = SLIO_EDEVICE;
       }
     }
+    if (!rc) {
+      // the fused group pass's buffers, on rank 0's device
+      (void)hipSetDevice(devices[0]);
+      Ctx& c0 = out[0]->c;
+      if (hipMalloc(&c0.gsup, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
+          hipMalloc(&c0.garrive, 4 * sizeof(uint32_t)) != hipSuccess ||
+          hipMemset(c0.garrive, 0, 4 * sizeof(uint32_t)) != hipSuccess) {
+        set_error("slio_create_group: allocation failed");
+        rc = SLIO_ENOMEM;
+      }
+    }
   }
   if (rc) {
     for (int r = 0; r < ndev; ++r) {
@@ -7423,6 +7538,96 @@ static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], do
   gs.n = n;
   for (int r = 0; r < n; ++r) gs.sup[r] = hs[r]->c.d_super;
   Ctx& c0 = hs[0]->c;
+  // Fused group pass (ranks sharing one device): per pass ONE launch per rank
+  // (search or reuse pass + segment and super rows into the group's buffer +,
+  // in the rank that arrives last, the filter step on the group's control
+  // block, fused_tail) and, before every pass but the first, one gate launch
+  // that waits for the previous pass's filter step; no events, no reduce or
+  // filter-step launches, no host round trip until the end
+  bool gfused = kind == 2 && c0.gsup && n > 1 && runs[0].fused_ok();
+  for (int r = 1; r < n && gfused; ++r) gfused = hs[r]->c.prm.device == c0.prm.device;
+  if (gfused) {
+    const int64_t C = num_chunks(c0.n);
+    const bool hs_on = c0.hstamp;
+    if (hs_on) {
+      c0.hst[0] = mono_ns();
+      c0.hst[4] = c0.hst[5] = c0.hst[6] = 0;
+    }
+    if (++c0.upd_seq <= 0) c0.upd_seq = 1;
+    const int32_t seq = c0.upd_seq;
+    for (int r = 0; r < n; ++r) hs[r]->c.group_seq = seq;
+    int rc = SLIO_OK;
+    for (int i = runs[0].first; i < maximum_iter && !rc; ++i) {
+      const bool p0 = i == runs[0].first;
+      if (p0) {
+        // the group's control block is rank 0's: its mapped host block in,
+        // its pass-0 launch copies it to HBM
+        runs[0].fill_block();
+        c0.h_ctl->seq = seq;
+        if (!info_constants(P, runs[0].dim, c0.h_ctl->P11i, c0.h_ctl->G)) {
+          set_error("slio_group_ikf_update: singular covariance block P[:D, :D]");
+          rc = SLIO_EINVAL;
+          break;
+        }
+      }
+      const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
+      for (int r = 0; r < n && !rc; ++r) {
+        Ctx& cr = hs[r]->c;
+        if (!p0) k_group_gate<<<1, 64, 0, cr.stream>>>(c0.garrive, i - runs[0].first, seq);
+        const SolveArgs sa = runs[r].args(i);
+        const FuseArgs fa{c0.ctl,  (p0 && r == 0) ? (const IkfCtl*)c0.d_hctl : nullptr,
+                          cr.d_seg, c0.gsup,
+                          c0.ctl,  c0.d_hctl,
+                          cr.count, R,
+                          i,       maximum_iter,
+                          C,       kNSeg / n,
+                          r * (SLIO_NSUPER / n), n,
+                          c0.gsup, c0.garrive,
+                          seq};
+        rc = enqueue_pass(cr, p0 ? &runs[r].pose0 : nullptr, c0.ctl, which, extrinsic_est, &sa, true, false,
+                          nullptr, &fa);
+        if (!rc && hipGetLastError() != hipSuccess) {
+          set_error("slio_group_ikf_update: launch failed");
+          rc = SLIO_EDEVICE;
+        }
+      }
+    }
+    for (int r = 0; r < n; ++r) hs[r]->c.group_seq = 0;
+    if (rc) return rc;
+    if (hs_on) {
+      c0.hst[1] = mono_ns();
+      c0.hst[4] = c0.hst[1] - c0.hst[0];  // every launch (passes and gates)
+    }
+    // the step that ends the update runs in whichever rank arrives last:
+    // wait for rank 0's published word while any rank's stream still has work
+    {
+      volatile int32_t* pub = &c0.h_ctl->published;
+      for (uint32_t it = 1; !*pub; ++it) {
+        if ((it & 255) == 0) {
+          bool idle = true;
+          for (int r = 0; r < n && idle; ++r) {
+            const hipError_t e = hipStreamQuery(hs[r]->c.stream);
+            if (e != hipSuccess && e != hipErrorNotReady) return SLIO_EDEVICE;
+            idle = e == hipSuccess;
+          }
+          if (idle) break;  // every launch has ended: the flags tell whether it published
+        }
+        __builtin_ia32_pause();
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (hs_on) c0.hst[2] = mono_ns();
+    slio_ikf_stats st0{};
+    c0.hstamp = false;  // (finish's own stamps would overwrite the group's)
+    const int rc2 = runs[0].finish(&st0);
+    c0.hstamp = hs_on;
+    if (rc2) return rc2;
+    *x = xs[0];
+    std::memcpy(P, Ps[0].data(), sizeof(double) * 576);
+    if (stats) *stats = st0;
+    if (hs_on) c0.hst[3] = mono_ns();
+    return SLIO_OK;
+  }
   // host stamps of the group update on rank 0's handle (slio_debug_host_stamps):
   // [0] entry, [1] every pass enqueued, [2] every rank's result seen, [3] exit;
   // [4] / [5] / [6] host ns spent enqueueing the ranks' pass launches / the

@@ -325,6 +325,7 @@ def bench_group(args, rank, world, dev, dist):
     lib.slio_debug_host_stamps(hs[0], 0, None)
     r = np.array(rows, np.float64) / 1e3
     passes = int(stats.passes)
+    # (the fused group path has one launch kind per pass: [4] is all its launches)
     host = {"enqueue_all_us": float(np.median(r[:, 1] - r[:, 0])),
             "rank_pass_launches_us": float(np.median(r[:, 4])),
             "reduce_enqueue_us": float(np.median(r[:, 5])),

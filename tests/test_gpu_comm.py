@@ -104,12 +104,19 @@ def test_group_one_rank_bitwise(L, oracle_mod, c2, mode):
     assert rot_err(xg[3:7], s_ref[3:7]) < TOL_ROT
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("mode,ext", [(1, 0), (0, 0), (0, 1)])
-def test_group_ranks_one_device_bitwise(L, oracle_mod, c2, mode, ext):
+def test_group_ranks_one_device_bitwise(L, oracle_mod, c2, mode, ext, fused, monkeypatch):
     """C4's in-library sequence at N = 2, 4, 8 ranks on this one GPU (the
     in-device reduce backend): bitwise equal to one rank, in the FIXED and the
     REFERENCE control flow, with and without extrinsic estimation; the group
-    is updated twice (its counters and events are reused)."""
+    is updated twice (its counters, gates and events are reused).  fused: one
+    launch per rank per pass (the ranks' super rows into the group's buffer,
+    the filter step in the rank that arrives last) plus a gate launch between
+    passes; else (SLIO_NO_FUSE=1) search + super-sum launches, events,
+    k_group_reduce and a filter-step launch per rank."""
+    if not fused:
+        monkeypatch.setenv("SLIO_NO_FUSE", "1")
     mp, fr, T = c2
     st = state_of(fr)
     x1, P1, s1 = single_update(L, mp, fr, st, mode=mode, ext=ext)
