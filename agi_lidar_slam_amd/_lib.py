@@ -227,6 +227,7 @@ SIGNATURES = {
     "slio_state_boxplus": (C.c_int, [C.POINTER(SlioState), _DP, C.POINTER(SlioState)]),
     "slio_state_boxminus": (C.c_int, [C.POINTER(SlioState), C.POINTER(SlioState), _DP]),
     "slio_debug_reload_switches": (C.c_int, [_P]),
+    "slio_debug_update_path": (C.c_int, [_P]),
     "slio_debug_host_stamps": (C.c_int, [_P, C.c_int, _I64P]),
     "slio_debug_knn_cert": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
     # include/slio_frontend.h (LIO-SAM front-end)

@@ -75,7 +75,11 @@ struct IkfCtl {
   int32_t published;  // mapped host block: set (release, system scope) after x, P and the flags
   int32_t seq;        // the update's sequence number (a fused group's passes and gates check it)
   int32_t pad_;
-  double pose[32];   // PoseDev of x (rotation matrices formed): the next pass's pose (device only)
+  // PoseDev of x (rotation matrices formed) for the pass that follows, in slot
+  // (passes completed) % kPoseSlots (device only): a slot is first read by a
+  // pass after its writer's step, so a persistent update's scalar-cache loads
+  // of it are never stale within the launch
+  alignas(128) double pose[16][32];  // (each slot on cache lines of its own)
   double LM[300];    // Cholesky factor of S = P11i + H^T H / R (D x D), H^T H / R
                      // (upper triangle, 78) and 1 / diag of the factor, of the
                      // last valid pass (device only)

@@ -41,7 +41,7 @@
 // -DSLIO_SOLVE_STAMP: wall-clock stamps of the filter-step phases (diagnostic
 // builds only; read with slio_dbg_solve_stamps).
 #ifdef SLIO_SOLVE_STAMP
-__device__ unsigned long long g_sstamp[32];
+__device__ unsigned long long g_sstamp[64];
 #define SSTAMP(k)                                       \
   do {                                                  \
     __builtin_amdgcn_sched_barrier(0);                  \
@@ -85,11 +85,29 @@ __device__ unsigned long long g_wstamps[8192][4][4];  // per wave: refine start/
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192)                              \
       g_wstamps[blockIdx.x][threadIdx.x >> 6][k] = (v);                            \
   } while (0)
-__device__ unsigned long long g_rstamps[8192][4];  // thread 0's first wide refinement
+__device__ unsigned long long g_rstamps[8192][6];  // thread 0's last wide refinement
 #define RSTAMP(k)                                                                  \
   do {                                                                             \
     if (threadIdx.x == 0 && blockIdx.x < 8192)                                     \
       g_rstamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                 \
+  } while (0)
+// ... and its candidates, runs, lanes and whether its bound was finite
+#define RINFO(T, nr, RL, fin)                                                      \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {                                   \
+      g_rstamps[blockIdx.x][4] = (T);                                              \
+      g_rstamps[blockIdx.x][5] = (nr) | ((RL) << 8) | ((fin) ? 0x10000 : 0);       \
+    }                                                                              \
+  } while (0)
+// fit phase of thread 0 (wave 0): entry, loads landed, plane + gate, row formed, end
+__device__ unsigned long long g_fstamps[8192][6];
+#define FSTAMP(k, wait)                                                            \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                     \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                     \
+      g_fstamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                 \
+    __builtin_amdgcn_sched_barrier(0);                                             \
   } while (0)
 #define STAMP(slot)                                                                \
   do {                                                                             \
@@ -110,6 +128,12 @@ __device__ unsigned long long g_rstamps[8192][4];  // thread 0's first wide refi
   } while (0)
 #define RSTAMP(k) \
   do {            \
+  } while (0)
+#define RINFO(T, nr, RL, fin) \
+  do {                        \
+  } while (0)
+#define FSTAMP(k, wait) \
+  do {                  \
   } while (0)
 #endif
 
@@ -561,7 +585,7 @@ struct PoseDev {
 };
 
 static_assert(sizeof(PoseDev) == 32 * sizeof(double), "PoseDev: 32 doubles (IkfCtl::pose)");
-static_assert(sizeof(IkfCtl::pose) == sizeof(PoseDev), "IkfCtl::pose holds a PoseDev");
+static_assert(sizeof(IkfCtl::pose[0]) == sizeof(PoseDev), "IkfCtl::pose slots hold a PoseDev");
 
 // double e of pose_from_state(x) (the PoseDev layout), for the filter step
 // to store the next pass's pose: the pass kernels then read it with scalar
@@ -583,9 +607,11 @@ __device__ __forceinline__ double pose_elem(const slio_state& x, int e) {
   return v;
 }
 typedef __attribute__((address_space(4))) const double cdouble;  // constant: scalar loads
-__device__ __forceinline__ PoseDev pose_of_ctl(const IkfCtl* ctl) {
+constexpr int kPoseSlots = 16;  // IkfCtl::pose
+static_assert(offsetof(IkfCtl, pose) % 128 == 0 && sizeof(IkfCtl::pose) == kPoseSlots * 256, "IkfCtl: pose slots");
+__device__ __forceinline__ PoseDev pose_of_ctl(const IkfCtl* ctl, int slot) {
   PoseDev P;
-  cdouble* src = (cdouble*)(const void*)ctl->pose;
+  cdouble* src = (cdouble*)(const void*)ctl->pose[slot & (kPoseSlots - 1)];
   double* dst = reinterpret_cast<double*>(&P);
 #pragma unroll
   for (int e = 0; e < 32; ++e) dst[e] = src[e];
@@ -1752,9 +1778,23 @@ __device__ __forceinline__ Quat so3_boxplus_dev(const Quat& q, const double om[3
 // block; ctl (HBM) receives the new iterate and flags, hblk (the caller's
 // mapped host block) x, P and the flags when the update ends.  All threads
 // of the workgroup call this.
-template <int NT, int D>
+template <int NT, int D, bool WT = false>
 __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, int i, int maxit,
                                          StepLds& L) {
+  // WT (persistent update): the control block is written through -- the
+  // launch's next pass reads it from any XCD -- and LM read back the same way
+  auto stD = [](double* p, double v) {
+    if (WT)
+      st_sc1(p, v);
+    else
+      *p = v;
+  };
+  auto stU = [](void* p, uint32_t v) {
+    if (WT)
+      st_sc1_u32(reinterpret_cast<uint32_t*>(p), v);
+    else
+      *reinterpret_cast<uint32_t*>(p) = v;
+  };
   static_assert(NT >= 256, "filter step: at least four wavefronts");
   static_assert(D == 6 || D == 12, "filter step: D is 6 or 12");
   const int t = threadIdx.x;
@@ -1899,14 +1939,14 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
   } else if (valid) {
     // waves 1..3, beside wave 0's chain: keep this pass's M for a final pass
     // without effective points (its factor is formed again from P_DD^-1 + M)
-    for (int e = t - 64; e < SLIO_NHTH; e += NT - 64) ctl->LM[144 + e] = L.Mt[e];
+    for (int e = t - 64; e < SLIO_NHTH; e += NT - 64) stD(&ctl->LM[144 + e], L.Mt[e]);
   }
   __syncthreads();
   SSTAMP(6);
   if (!L.ok) {
     if (t == 0) {
-      ctl->singular = 1;
-      ctl->done = 1;
+      stU(&ctl->singular, 1u);
+      stU(&ctl->done, 1u);
       hblk->singular = 1;
       hblk->done = 1;
       __threadfence_system();
@@ -1923,7 +1963,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
       if (!valid) {
         // the last valid pass's M (fixed mode: one exists, or the update
         // would not end here with a P update); its factor, formed again
-        for (int e = t; e < SLIO_NHTH; e += 64) L.Mt[e] = ctl->LM[144 + e];
+        for (int e = t; e < SLIO_NHTH; e += 64) L.Mt[e] = WT ? ld_sc1(&ctl->LM[144 + e]) : ctl->LM[144 + e];
         wave_fence();
 #pragma unroll
         for (int r = 0; r < D; ++r)
@@ -1983,7 +2023,7 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
 #pragma unroll
         for (int k = 0; k < D; ++k) s2 = fma(L.zk.K[r * D + k], L.P[k * 24 + cc], s2);
         pn[u] = L.P[e] - s2;
-        ctl->P[e] = pn[u];
+        stD(&ctl->P[e], pn[u]);
       }
     }
   }
@@ -1991,11 +2031,19 @@ __device__ __forceinline__ void ikf_step(IkfCtl* ctl, IkfCtl* hblk, double R, in
   {
     const double* xs = reinterpret_cast<const double*>(&L.x);
     double* xd = reinterpret_cast<double*>(&ctl->x);
-    for (int e = t; e < kStateD; e += NT) xd[e] = xs[e];
-    if (t >= 64 && t < 96) ctl->pose[t - 64] = pose_elem(L.x, t - 64);  // the next pass's pose
+    for (int e = t; e < kStateD; e += NT) stD(xd + e, xs[e]);
+    // the next pass's pose, in the slot of the passes completed (L.fl: after
+    // this step)
+    if (t >= 64 && t < 96) stD(&ctl->pose[L.fl[F_PASSES] & (kPoseSlots - 1)][t - 64], pose_elem(L.x, t - 64));
   }
-  if (t < 8) (&ctl->converge)[t] = L.fl[t];
-  if (t == 0) ctl->last_m = m;
+  if (t < 8) stU(reinterpret_cast<uint32_t*>(&ctl->converge) + t, (uint32_t)L.fl[t]);
+  if (t == 0) {
+    if (WT)
+      __hip_atomic_store((guint64*)(uint64_t*)&ctl->last_m, (uint64_t)m, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      ctl->last_m = m;
+  }
   if (L.fl[F_DONE]) {
     // the update ends: x, P and the flags to the caller's mapped host block
 #pragma unroll
@@ -2182,6 +2230,7 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
     T += __shfl(inc, RL - 1, RL);
   }
   RSTAMP(1);
+  RINFO(T, nr, RL, rc.lim < __int_as_float(0x7f800000));
   static_assert(RL * W >= kTab, "every table entry has an owner lane");
 #pragma unroll
   for (int w = 0; w < W; ++w) {
@@ -2245,7 +2294,7 @@ __device__ __forceinline__ void scan_runs_wide(const float4* __restrict__ pts,
 // staging of the rows).  CTL_SC1: parts of the block were written in this
 // launch (dx_new by block 0 of a fused pass; the whole block by the first
 // fused pass's prefetch), so every control load goes past the L2 (sc1).
-template <int NT, int D, bool CTL_SC1, bool GROUP = false>
+template <int NT, int D, bool CTL_SC1, bool GROUP = false, bool WT = false>
 __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, double* super_out, IkfCtl* ctl,
                                            const IkfCtl* src, IkfCtl* hblk, double R, int iter, int maxit) {
   const int t = threadIdx.x;
@@ -2276,9 +2325,17 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
       L.Mt[t] = a / R;
     else if (t < SLIO_NHTH + 12)
       L.hR[t - SLIO_NHTH] = a / R;
+    // (WT: write-through -- a persistent update's passes write them from
+    // different XCDs, whose L2s would write their dirty copies back in any
+    // order)
     if (!GROUP)
 #pragma unroll
-      for (int ss = 0; ss < SLIO_NSUPER; ++ss) super_out[ss * SLIO_NPROD + t] = sp[ss];
+      for (int ss = 0; ss < SLIO_NSUPER; ++ss) {
+        if (WT)
+          st_sc1(super_out + ss * SLIO_NPROD + t, sp[ss]);
+        else
+          super_out[ss * SLIO_NPROD + t] = sp[ss];
+      }
   } else {
     constexpr int NC = NT - SLIO_NPROD, nC = CtlList<D>::total, kC = (nC + NC - 1) / NC;
     const int tt = t - SLIO_NPROD;
@@ -2315,7 +2372,7 @@ __device__ __forceinline__ void final_step(StepLds& L, const double* seg_out, do
   __syncthreads();
   SSTAMP(4);
   if (src == ctl && L.fl[F_DONE]) return;  // the first pass of an update always runs
-  ikf_step<NT, D>(ctl, hblk, R, iter, maxit, L);
+  ikf_step<NT, D, WT>(ctl, hblk, R, iter, maxit, L);
 }
 
 template <int LPQ>
@@ -2366,23 +2423,27 @@ __device__ __forceinline__ double chunk_sums_256(double (*rows)[kRow], double (*
 // two rotations, on different wavefronts) while the pass itself runs, off
 // the filter step's critical path.  Needs >= 128 threads.  Stored
 // write-through (sc1): a fused pass's filter step reads it in the same launch,
-// possibly from another XCD.
+// possibly from another XCD.  SC1: the iterate is read write-through too (a
+// persistent update's earlier pass wrote it in the same launch).
+template <bool SC1>
 __device__ __forceinline__ void ikf_dx_new(IkfCtl* ctl) {
   if (blockIdx.x != 0) return;
   const int t = threadIdx.x;
+  auto ld = [](const double* p) { return SC1 ? ld_sc1(p) : *p; };
   if (t < 24) {
     const int k = t;
     if (k < 3 || k >= 9) {
       const double* xs = reinterpret_cast<const double*>(&ctl->x);
       const double* ps = reinterpret_cast<const double*>(&ctl->xprop);
-      st_sc1(&ctl->dxn[k], xs[state_off(k)] - ps[state_off(k)]);
+      st_sc1(&ctl->dxn[k], ld(xs + state_off(k)) - ld(ps + state_off(k)));
     }
   } else if (t == 32 || t == 64) {
     const int u = t == 32;
     const double* q1 = u ? ctl->x.rli : ctl->x.rot;
     const double* q2 = u ? ctl->xprop.rli : ctl->xprop.rot;
     double d[3];
-    so3_boxminus(Quat{q1[0], q1[1], q1[2], q1[3]}, Quat{q2[0], q2[1], q2[2], q2[3]}, d);
+    so3_boxminus(Quat{ld(q1), ld(q1 + 1), ld(q1 + 2), ld(q1 + 3)}, Quat{ld(q2), ld(q2 + 1), ld(q2 + 2), ld(q2 + 3)},
+                 d);
     st_sc1(&ctl->dxn[3 + 3 * u], d[0]);
     st_sc1(&ctl->dxn[4 + 3 * u], d[1]);
     st_sc1(&ctl->dxn[5 + 3 * u], d[2]);
@@ -2415,7 +2476,12 @@ struct FuseArgs {
   double* gsup;
   uint32_t* garrive;     // [0] the ranks' arrivals; [2..3] gflag (u64): (seq << 32) | done << 31 | passes
   int32_t gseq;          // the update's sequence number
+  // persistent update (k_update_persist): 8 replicas (one per XCD, 128 B
+  // apart) of the flag (gseq << 32) | done << 31 | passes its filter step
+  // publishes after each pass; null otherwise
+  uint64_t* goflag;
 };
+constexpr int kGoFlagStride = 16;  // uint64 words between the replicas
 constexpr int kSegCnt = 16;
 constexpr int kCountWords = kSegCnt + kNSeg;
 constexpr int kKcCount = 8;  // count[8..9]: certified / searched queries (slio_debug_knn_cert)
@@ -2457,9 +2523,9 @@ __device__ __forceinline__ void prefetch_ctl(const IkfCtl* __restrict__ hsrc, Ik
 // After the chunk partial is stored (sc1): arrival on the chunk's segment row;
 // the last arrival sums the row, and the last row runs the filter step.
 // Every thread of the workgroup calls it.
-template <int NT, int D>
+template <int NT, int D, bool WT = false>
 __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArgs& fa, IkfCtl* ctl,
-                                           const double* chunk_part, int64_t chunk) {
+                                           const double* chunk_part, int64_t chunk, int iter) {
   const int t = threadIdx.x;
   int64_t lim;
   const int b = seg_of_chunk(fa.C, chunk, lim);
@@ -2504,6 +2570,9 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
   if (t == 0) {
     ts[3] = wall_clock64();
     for (int k = 0; k < 4; ++k) g_sstamp[16 + k] = ts[k];
+    // per pass: the final workgroup's partial issued / last row arrival
+    g_sstamp[36 + ((iter + 1) & 3)] = ts[0];
+    g_sstamp[32 + ((iter + 1) & 3)] = ts[3];
   }
 #endif
   if (t == 0) {
@@ -2514,7 +2583,20 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     st_sc1_u32(fa.cnt + 5, 0u);
   }
   if (!fa.gsup) {
-    final_step<NT, D, true>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+    final_step<NT, D, true, false, WT>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, iter, fa.maxit);
+    if (WT && fa.goflag) {
+      // persistent update: the step's control block went out write-through
+      // (ikf_step); every wave's stores drained, then the flag the waiting
+      // workgroups poll, one replica per XCD
+      drain_stores();
+      __syncthreads();
+      if (t < 8) {
+        const uint64_t fl = ((uint64_t)(uint32_t)fa.gseq << 32) | (L.fl[F_DONE] ? 0x80000000ull : 0ull) |
+                            (uint64_t)(uint32_t)L.fl[F_PASSES];
+        __hip_atomic_store((guint64*)(fa.goflag + t * kGoFlagStride), fl, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   } else {
     // fused group pass: this rank's super rows (its 8 / ranks super-chunks,
     // each the sum of its 8 segment rows in order: k_super_sums' tree) into
@@ -2538,7 +2620,7 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     __syncthreads();
     if (bcast != fa.granks - 1) return;
     if (t == 0) reset_counter(fa.garrive);
-    final_step<NT, D, true, true>(L, fa.gsup, nullptr, ctl, fa.src, fa.hblk, fa.R, fa.iter, fa.maxit);
+    final_step<NT, D, true, true>(L, fa.gsup, nullptr, ctl, fa.src, fa.hblk, fa.R, iter, fa.maxit);
     // the step's control block (plain stores, possibly on another XCD than
     // the next passes' readers) out to memory, then the flag the ranks'
     // gates poll: (seq, done, passes)
@@ -2553,7 +2635,7 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     }
   }
 #ifdef SLIO_SOLVE_STAMP
-  if (t == 0) g_sstamp[25 + ((fa.iter + 1) & 3)] = wall_clock64();  // per pass: the filter step's end
+  if (t == 0) g_sstamp[25 + ((iter + 1) & 3)] = wall_clock64();  // per pass: the filter step's end
 #endif
 }
 
@@ -2567,71 +2649,63 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
 #ifndef SLIO_RL8_MAX
 #define SLIO_RL8_MAX 8
 #endif
-template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE = false, int FD = 6>
-__global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
-    const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
-    const PassOut out, const FuseArgs fa) {
-  static_assert(!FUSE || search_block<LPQ>() == kSolveThreads, "fused pass: 256 threads");
-#ifdef SLIO_SOLVE_STAMP
-  if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) {
-    g_sstamp[20] = wall_clock64();
-    g_sstamp[21 + ((fa.iter + 1) & 3)] = g_sstamp[20];  // per pass: block 0's start
-  }
-#endif
-  if constexpr (FUSE && !DEVPOSE)
-    if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
-  // DEVPOSE: pose and pass selection come from the device-resident update.
-  // A fused pass runs whichever pass the update wants (search or reuse,
-  // ctl->search_now = converge, esekfom.hpp:138): one launch per pass in the
-  // reference control flow too.
-  if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
-                  (!FUSE && cfg.ctl->search_now != cfg.want_search) || (cfg.seq && cfg.ctl->seq != cfg.seq)))
-    return;
-  const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
+// refinement records of a chunk (alias the Jacobian rows, which the fit phase
+// writes only after the refinement)
+struct RefLds {
+  uint64_t top[SLIO_CHUNK][5];
+  float4 q[SLIO_CHUNK];
+  uint8_t slot[SLIO_CHUNK];
+};
+template <int NT>
+struct SearchLds {
+  union {
+    double rows[SLIO_CHUNK][kRow];
+    RefLds ref;
+  } rr;
+  double part[NT / 128][SLIO_NPROD];
+  alignas(16) uint32_t nb_pos[SLIO_CHUNK][5];
+  alignas(16) float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
+  alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
+  float nb_d5[SLIO_CHUNK];
+  float4 qw[SLIO_CHUNK];            // the query; .w: its certificate bound G (KC, -2: none written)
+  uint32_t kc_n[2];                 // KC: certified queries, searched queries
+  uint32_t kx6[SLIO_CHUNK];         // KC: the 6th of the point's certified set
+  uint8_t ksame[SLIO_CHUNK];        // KC: certified in the last pass's order (plane reusable)
+  // deferred (far) queries of this chunk and the far workers' scratch
+  int far_cnt, ref_cnt;
+  uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
+  uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
+  int32_t tab_dl[NT / 16][kTab];
+  float4 far_q[SLIO_CHUNK];
+  uint8_t far_slot[SLIO_CHUNK];
+  uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
+};
+// a pass's LDS: the search, then (fused pass) the filter step
+template <int NT>
+union PassLds {
+  SearchLds<NT> s;
+  StepLds L;
+};
+
+// The pass body: the search (or, reuse, the reuse pass's rows), the chunk's
+// products and (FUSE) the fused tail.  pose: the pass's pose; DEVPOSE: a
+// pass after the first of a device-resident update (certificates, dx_new);
+// PERS: a pass of the persistent update, whose control-block reads are
+// write-through (the launch's earlier passes wrote it).
+template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE, int FD, bool PERS>
+__device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& lds, int& fuse_bcast,
+                                                 const MapView& map, const ScanDev& scan, const PoseDev& pose,
+                                                 const PassCfg& cfg, const PassOut& out, const FuseArgs& fa,
+                                                 bool reuse, int iter) {
   constexpr int NT = search_block<LPQ>();
   // kNN certificates (passes after the first of a device-resident update,
   // 2 lanes per query, 3x3x3 block first): see the certificate below
   constexpr bool KC = DEVPOSE && LPQ == 2 && !SPHERE;
-  if (DEVPOSE) ikf_dx_new(cfg.ctl);
+  if (DEVPOSE) ikf_dx_new<PERS>(cfg.ctl);
   constexpr int QPP = NT / LPQ;               // queries per kNN pass
   constexpr int PASSES = SLIO_CHUNK / QPP;    // kNN passes per chunk
   static_assert(SLIO_CHUNK % QPP == 0, "chunk must be a multiple of queries/pass");
   static_assert(NT >= SLIO_CHUNK, "fit phase needs one lane per point");
-  // refinement records of the chunk (alias the Jacobian rows, which the fit
-  // phase writes only after the refinement)
-  struct RefLds {
-    uint64_t top[SLIO_CHUNK][5];
-    float4 q[SLIO_CHUNK];
-    uint8_t slot[SLIO_CHUNK];
-  };
-  struct SearchLds {
-    union {
-      double rows[SLIO_CHUNK][kRow];
-      RefLds ref;
-    } rr;
-    double part[NT / 128][SLIO_NPROD];
-    alignas(16) uint32_t nb_pos[SLIO_CHUNK][5];
-    alignas(16) float nb_sqd[SLIO_CHUNK][5];  // pointSearchSqDis, stored by the fit phase
-    alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
-    float nb_d5[SLIO_CHUNK];
-    float4 qw[SLIO_CHUNK];            // the query; .w: its certificate bound G (KC, -2: none written)
-    uint32_t kc_n[2];                 // KC: certified queries, searched queries
-    uint32_t kx6[SLIO_CHUNK];         // KC: the 6th of the point's certified set
-    uint8_t ksame[SLIO_CHUNK];        // KC: certified in the last pass's order (plane reusable)
-    // deferred (far) queries of this chunk and the far workers' scratch
-    int far_cnt, ref_cnt;
-    uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
-    uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
-    int32_t tab_dl[NT / 16][kTab];
-    float4 far_q[SLIO_CHUNK];
-    uint8_t far_slot[SLIO_CHUNK];
-    uint32_t far_pre[NT / 64][64], far_beg[NT / 64][64];
-  };
-  __shared__ union {
-    SearchLds s;
-    StepLds L;  // a fused pass's filter step, after the search is done
-  } lds;
-  __shared__ int fuse_bcast;
   auto& rows = lds.s.rr.rows;
   auto& ref = lds.s.rr.ref;
   auto& part = lds.s.part;
@@ -2655,8 +2729,6 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   // its rows here and shares the products and the tail below with the search
   // pass (one copy of the tail in the kernel: a second one, in a branch of
   // its own, cost ~2.5 % of the search pass's time)
-  bool reuse = false;
-  if constexpr (FUSE && DEVPOSE) reuse = !cfg.ctl->search_now;
   if (reuse) {
     if (tid < SLIO_CHUNK) {
       double row[kRow];
@@ -2680,7 +2752,12 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
   // this chunk's certificates belong to this update (written by one of its
   // earlier passes): a uniform load
   bool cache_ok = false;
-  if constexpr (KC) cache_ok = cfg.kc_epoch != 0 && out.kepoch[chunk] == cfg.kc_epoch;
+  if constexpr (KC) {
+    // (PERS: this workgroup wrote the entry in an earlier pass of the launch;
+    // a vector load, not the scalar cache)
+    const uint32_t ke = PERS ? __builtin_amdgcn_readfirstlane(ld_sc1_u32(&out.kepoch[chunk])) : out.kepoch[chunk];
+    cache_ok = cfg.kc_epoch != 0 && ke == cfg.kc_epoch;
+  }
   if (tid == 0) STAMP(0);
   if (tid == 0) {
     far_cnt = 0;
@@ -3090,6 +3167,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
                        __int_as_float(0x7fc00000), __int_as_float(0x7fc00000)};
       float pd2 = __int_as_float(0x7fc00000);
       const float4 q = qw[slot];
+      FSTAMP(0, false);
       const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
       // KC: certified with the last pass's 5 in the same order -- the same
       // esti_plane input, so its plane (when it had one) is reused
@@ -3121,6 +3199,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         nb[j][2] = c.z;
         nb_idx[slot][j] = (int32_t)__float_as_uint(c.w);
       }
+      FSTAMP(1, true);
       if (cfg.knn_only) sel = false;
       if (sel && rp) {
         abcd[0] = cpl.x;
@@ -3137,6 +3216,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
           sel = residual_gate(abcd, q.x, q.y, q.z, bx, by, bz, pd2);
         }
       }
+      FSTAMP(2, false);
       out.plane[i] = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
       out.sel[i] = sel ? 1 : 0;
       out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
@@ -3157,8 +3237,10 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
         row[13] = 1.0;
       }
     }
+    FSTAMP(3, false);
 #pragma unroll
     for (int j = 0; j < kRow; ++j) rows[slot][j] = row[j];
+    FSTAMP(4, true);
   }
   __syncthreads();
   if (tid == 0) STAMP(2);
@@ -3214,7 +3296,7 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     const double pv = chunk_sums_256(rows, part, cfg.mfma);
     if (tid < SLIO_NPROD) st_sc1(out.chunk_part + chunk * SLIO_NPROD + tid, pv);  // read by another workgroup
     if (tid == 0) STAMP(3);
-    fused_tail<NT, FD>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk);
+    fused_tail<NT, FD, PERS>(lds.L, fuse_bcast, fa, fa.ctl, out.chunk_part, chunk, iter);
   } else {
     if constexpr (NT == 256) {
       const double pv = chunk_sums_256(rows, part, cfg.mfma);
@@ -3224,6 +3306,111 @@ __global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_
     }
     if (tid == 0) STAMP(3);
   }
+}
+
+template <int LPQ, int U, bool SPHERE, bool DEVPOSE, bool FUSE = false, int FD = 6>
+__global__ __launch_bounds__(search_block<LPQ>(), SPHERE ? 2 : 4) void k_search_pass(
+    const MapView map, const ScanDev scan, const PoseDev pose_arg, const PassCfg cfg,
+    const PassOut out, const FuseArgs fa) {
+  static_assert(!FUSE || search_block<LPQ>() == kSolveThreads, "fused pass: 256 threads");
+#ifdef SLIO_SOLVE_STAMP
+  if (FUSE && blockIdx.x == 0 && threadIdx.x == 0) {
+    g_sstamp[20] = wall_clock64();
+    g_sstamp[21 + ((fa.iter + 1) & 3)] = g_sstamp[20];  // per pass: block 0's start
+  }
+#endif
+  if constexpr (FUSE && !DEVPOSE)
+    if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
+  // DEVPOSE: pose and pass selection come from the device-resident update.
+  // A fused pass runs whichever pass the update wants (search or reuse,
+  // ctl->search_now = converge, esekfom.hpp:138): one launch per pass in the
+  // reference control flow too.
+  if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
+                  (!FUSE && cfg.ctl->search_now != cfg.want_search) || (cfg.seq && cfg.ctl->seq != cfg.seq)))
+    return;
+  __shared__ PassLds<search_block<LPQ>()> lds;
+  __shared__ int fuse_bcast;
+  const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl, cfg.pass_idx) : pose_arg;
+  bool reuse = false;
+  if constexpr (FUSE && DEVPOSE) reuse = !cfg.ctl->search_now;
+  search_pass_body<LPQ, U, SPHERE, DEVPOSE, FUSE, FD, false>(lds, fuse_bcast, map, scan, pose, cfg, out, fa,
+                                                            reuse, fa.iter);
+}
+
+// The persistent update (single rank, fused passes): ONE launch runs every
+// pass of slio_ikf_update_device.  Each workgroup owns one chunk for the whole
+// update; after a pass it waits (one lane, write-through polls with s_sleep)
+// for the flag the pass's filter step publishes (fused_tail: the control
+// block written through, drained, then (seq, done, passes)), reads the next
+// pose and whether the pass searches (converge, esekfom.hpp:138) write-through,
+// and runs the pass; done ends every workgroup.  No kernel boundary between
+// passes (their end-of-kernel write-back and the next launch's start).  The
+// host launches it only when every workgroup is resident at once (occupancy
+// check) -- a pass's filter step needs all its chunks; a wait past ~1 s gives
+// up (the update then reports that it did not complete) instead of hanging.
+template <int U, int FD>
+__global__ __launch_bounds__(kSolveThreads, 4) void k_update_persist(const MapView map, const ScanDev scan,
+                                                                     const PoseDev pose0, const PassCfg cfg,
+                                                                     const PassOut out, const FuseArgs fa,
+                                                                     const int npasses) {
+  __shared__ PassLds<kSolveThreads> lds;
+  __shared__ int fuse_bcast;
+  __shared__ int s_go;
+#ifdef SLIO_SOLVE_STAMP
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    g_sstamp[20] = wall_clock64();
+    g_sstamp[21 + ((fa.iter + 1) & 3)] = g_sstamp[20];  // per pass: block 0's start
+  }
+#endif
+  if (blockIdx.x == 0 && fa.pre) prefetch_ctl<FD>(fa.pre, fa.ctl);
+  search_pass_body<2, U, false, false, true, FD, true>(lds, fuse_bcast, map, scan, pose0, cfg, out, fa, false,
+                                                       fa.iter);
+  const uint64_t* flag = fa.goflag + (blockIdx.x & 7) * kGoFlagStride;
+  // The pass cycle is entered at two points (the second never taken: npasses
+  // >= 1): an irreducible cycle is no natural loop to the optimizer, which
+  // would otherwise hoist the body's loop-invariant address arithmetic out of
+  // it and keep those values live in scratch across every pass.
+  int p = 1;
+  if (npasses < 0) goto run;
+wait:
+  if (p >= npasses) return;
+  if (threadIdx.x == 0) {
+    int go = 0;
+    const unsigned long long t0 = wall_clock64();
+#ifdef SLIO_SOLVE_STAMP
+    if (blockIdx.x == 0) g_sstamp[40 + ((fa.iter + p + 1) & 3)] = t0;  // per pass: block 0 waits
+#endif
+    while (true) {
+      const uint64_t fl = __hip_atomic_load((const guint64*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int32_t)(fl >> 32) == fa.gseq) {
+        if (fl & 0x80000000ull) break;  // the update ended
+        if ((int32_t)(fl & 0x7fffffffull) >= p) {
+          go = (int)(fl & 0x7fffffffull);
+          break;
+        }
+      }
+      if (wall_clock64() - t0 > 100000000ull) break;  // 100 MHz: 1 s
+      __builtin_amdgcn_s_sleep(4);  // (1 / 16 / 64: the same pass times, profiles/r05_persist_stamps.log)
+    }
+    s_go = go;
+#ifdef SLIO_SOLVE_STAMP
+    if (blockIdx.x == 0) g_sstamp[21 + ((fa.iter + p + 1) & 3)] = wall_clock64();
+#endif
+  }
+  __syncthreads();
+  if (!s_go) return;
+run:
+  {
+    // the pose slot of the passes counted (== p), taken from the flag, so the
+    // scalar loads cannot move above the wait
+    const PoseDev pose = pose_of_ctl(fa.ctl, __builtin_amdgcn_readfirstlane(s_go));
+    const bool reuse =
+        __builtin_amdgcn_readfirstlane(ld_sc1_u32(reinterpret_cast<const uint32_t*>(&fa.ctl->search_now))) == 0;
+    search_pass_body<2, U, false, true, true, FD, true>(lds, fuse_bcast, map, scan, pose, cfg, out, fa, reuse,
+                                                        fa.iter + p);
+  }
+  ++p;
+  goto wait;
 }
 
 // Nearest_Points ids and pointSearchSqDis of the last search pass, derived
@@ -3266,8 +3453,8 @@ __global__ __launch_bounds__(256) void k_reuse_pass(const ScanDev scan,
   if (DEVPOSE && (cfg.ctl->done || cfg.ctl->passes != cfg.pass_idx ||
                   cfg.ctl->search_now != cfg.want_search))
     return;
-  const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl) : pose_arg;
-  if (DEVPOSE) ikf_dx_new(cfg.ctl);
+  const PoseDev pose = DEVPOSE ? pose_of_ctl(cfg.ctl, cfg.pass_idx) : pose_arg;
+  if (DEVPOSE) ikf_dx_new<false>(cfg.ctl);
   __shared__ double rows[SLIO_CHUNK][kRow];
   __shared__ double part[2][SLIO_NPROD];
   const int64_t chunk = xcd_chunk(cfg.c_begin, cfg.c_end - cfg.c_begin);
@@ -3514,7 +3701,14 @@ struct Ctx {
     bool no_mfma = false;     // SLIO_NO_MFMA: VALU chunk products
     bool event_wait = false;  // SLIO_EVENT_WAIT: wait on a completion event
     bool no_kc = false;       // SLIO_NO_KNN_CERT: every pass searches in full
+    bool persist = false;     // SLIO_PERSIST: one persistent launch per update (k_update_persist)
   } sw;
+  // persistent update (k_update_persist): the flag replicas, the CU count and
+  // the workgroups the device holds at once (-1: not yet queried)
+  uint64_t* goflag = nullptr;
+  int ncu = 0;
+  int64_t persist_cap = -1;
+  int last_path = 0;  // the last device-resident update: 1 persistent launch, 0 a launch per pass
   // host clock stamps (CLOCK_MONOTONIC ns) of the last device-resident update
   // (slio_debug_host_stamps)
   bool hstamp = false;
@@ -3531,6 +3725,7 @@ static void load_switches(Ctx& c) {
   c.sw.no_mfma = env_on("SLIO_NO_MFMA");
   c.sw.event_wait = env_on("SLIO_EVENT_WAIT");
   c.sw.no_kc = env_on("SLIO_NO_KNN_CERT");
+  c.sw.persist = env_on("SLIO_PERSIST");
 }
 static inline int64_t mono_ns() {
   timespec ts;
@@ -3765,7 +3960,7 @@ static int build_blk(MapDev& m, hipStream_t st, const char* who);
 static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
                         int extrinsic_est, const SolveArgs* sa = nullptr,
                         bool with_super = true, bool knn_only = false, const ScanDev* sd = nullptr,
-                        const FuseArgs* fuse = nullptr) {
+                        const FuseArgs* fuse = nullptr, int persist = 0) {
   if (!c.map) {
     set_error("slio pass: no map uploaded");
     return SLIO_ESTATE;
@@ -3784,7 +3979,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   // update) or from the control block in HBM (later device-resident passes)
   const bool devpose = ctl && !Parg;
   PassCfg cfg;
-  cfg.ctl = devpose ? ctl : nullptr;
+  cfg.ctl = (devpose || persist) ? ctl : nullptr;
   cfg.want_search = 1;
   cfg.plane_thr = c.prm.plane_threshold;
   cfg.max_sqd = c.prm.max_match_sqd;
@@ -3808,7 +4003,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   if (int rc = map_refresh(c); rc) return rc;
   if (which != 0 && c.map->blk_deferred) {
     std::unique_lock<std::shared_mutex> lk(c.map->mu);
-    if (c.map->blk_deferred && ++c.map->stable_passes > kBlkAfterPasses) {
+    if (c.map->blk_deferred && (c.map->stable_passes += (persist > 0 ? persist : 1)) > kBlkAfterPasses) {
       if (int rc = map_write_begin(c)) return rc;
       if (int rc = build_blk(*c.map, c.stream, "slio map"); rc) return rc;
       if (int rc = map_write_end(c)) return rc;
@@ -3822,7 +4017,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   // on the map that pass ran on (another handle sharing the map may have
   // rebuilt it in between)
   if (!devpose) c.kc_version = c.map->version;
-  cfg.kc_epoch = (devpose && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
+  cfg.kc_epoch = ((devpose || persist) && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
   cfg.seq = fuse ? c.group_seq : 0;
   PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,  c.sel,    c.resid,
             c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq, c.k6,
@@ -3870,7 +4065,15 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
 #define SLIO_LAUNCH_FUSED(DEV, D)                                                                           \
   hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, DEV, true, D>, nb, dim3(kSolveThreads), 0, \
                         c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse)
-      if (sa && sa->dim == 12) {
+#define SLIO_LAUNCH_PERSIST(D)                                                                    \
+  hipExtLaunchKernelGGL(k_update_persist<SLIO_SEARCH_U, D>, nb, dim3(kSolveThreads), 0, c.stream, ev.first, \
+                        ev.second, 0, mv, s, P, cfg, o, *fuse, persist)
+      if (persist > 0) {
+        if (sa && sa->dim == 12)
+          SLIO_LAUNCH_PERSIST(12);
+        else
+          SLIO_LAUNCH_PERSIST(6);
+      } else if (sa && sa->dim == 12) {
         if (devpose)
           SLIO_LAUNCH_FUSED(true, 12);
         else
@@ -3882,6 +4085,7 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
           SLIO_LAUNCH_FUSED(false, 6);
       }
 #undef SLIO_LAUNCH_FUSED
+#undef SLIO_LAUNCH_PERSIST
     } else
     switch (c.prm.lanes_per_query * 2 + (sph ? 1 : 0)) {
       case 2: SLIO_LAUNCH2(1, false); break;
@@ -3999,6 +4203,11 @@ void* internal_stream(slio_handle h) { return h ? (void*)h->c.stream : nullptr; 
 extern "C" {
 
 #ifdef SLIO_ABL_STAMP
+int slio_debug_clear_stamps(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_rstamps)) != hipSuccess) return -3;
+  return hipMemset(p, 0, sizeof(g_rstamps)) == hipSuccess ? 0 : -3;
+}
 int slio_debug_stamps(unsigned long long* out, int nblocks) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * nblocks) ==
                  hipSuccess
@@ -4011,8 +4220,14 @@ int slio_debug_wstamps(unsigned long long* out, int nblocks) {
              ? 0
              : -3;
 }
+int slio_debug_fstamps(unsigned long long* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fstamps), sizeof(unsigned long long) * 6 * nblocks) ==
+                 hipSuccess
+             ? 0
+             : -3;
+}
 int slio_debug_rstamps(unsigned long long* out, int nblocks) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 4 * nblocks) ==
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 6 * nblocks) ==
                  hipSuccess
              ? 0
              : -3;
@@ -4090,12 +4305,15 @@ int slio_create(slio_handle* out, const slio_params* p) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess &&
         ncu > 0 && ncu % 8 == 0)
       h->c.cus_per_xcd = ncu / 8;
+    h->c.ncu = ncu;
   }
   if (hipMalloc(&h->c.d_super_own, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.d_seg, sizeof(double) * kNSeg * SLIO_NPROD) != hipSuccess ||
       hipHostMalloc(&h->c.h_super, sizeof(double) * SLIO_NSUPER * SLIO_NPROD) != hipSuccess ||
       hipMalloc(&h->c.count, sizeof(uint32_t) * kCountWords) != hipSuccess ||
       hipMemset(h->c.count, 0, sizeof(uint32_t) * kCountWords) != hipSuccess ||
+      hipMalloc(&h->c.goflag, sizeof(uint64_t) * 8 * kGoFlagStride) != hipSuccess ||
+      hipMemset(h->c.goflag, 0, sizeof(uint64_t) * 8 * kGoFlagStride) != hipSuccess ||
       false) {
     set_error("slio_create: allocation failed");
     slio_destroy(h);
@@ -4119,6 +4337,7 @@ int slio_destroy(slio_handle h) {
   (void)hipFree(h->c.d_super_own);
   (void)hipFree(h->c.d_seg);
   (void)hipFree(h->c.count);
+  (void)hipFree(h->c.goflag);
   for (auto& b : h->c.inc)
     if (b.p) (void)hipFree(b.p);
   for (auto& b : h->c.pre)
@@ -4164,6 +4383,11 @@ int slio_debug_host_stamps(slio_handle h, int enable, int64_t out[8]) {
   if (out) std::memcpy(out, h->c.hst, sizeof(h->c.hst));
   if (enable >= 0) h->c.hstamp = enable != 0;
   return SLIO_OK;
+}
+
+int slio_debug_update_path(slio_handle h) {
+  if (!h) return SLIO_EINVAL;
+  return h->c.last_path;
 }
 
 }  // extern "C"
@@ -7246,6 +7470,50 @@ struct UpdateRun {
            num_chunks(c.n) >= (int64_t)kNSeg;
   }
 
+  // The whole update as one persistent launch (k_update_persist): the fused
+  // configuration, and every chunk's workgroup resident at once (the
+  // occupancy the device reports for the kernel, times its CUs).
+  bool persist_ok() {
+    if (!c.sw.persist || c.sw.no_fuse0 || !fusable() || !c.goflag || c.ncu <= 0) return false;
+    if (c.persist_cap < 0) {
+      int b6 = 0, b12 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b6, k_update_persist<SLIO_SEARCH_U, 6>,
+                                                       kSolveThreads, 0) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&b12, k_update_persist<SLIO_SEARCH_U, 12>,
+                                                       kSolveThreads, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        b6 = b12 = 0;
+      }
+      c.persist_cap = (int64_t)std::min(b6, b12) * c.ncu;
+    }
+    return num_chunks(c.n) <= c.persist_cap;
+  }
+  int persist() {
+    fill_block();
+    if (!info_constants(P, dim, c.h_ctl->P11i, c.h_ctl->G)) {
+      set_error("slio_ikf_update_device: singular covariance block P[:D, :D]");
+      return SLIO_EINVAL;
+    }
+    if (++c.upd_seq <= 0) c.upd_seq = 1;
+    c.h_ctl->seq = c.upd_seq;
+    SLIO_HSTAMP(c, 2);
+    const SolveArgs sa = args(first);
+    FuseArgs fa{c.ctl,   (const IkfCtl*)c.d_hctl,
+                c.d_seg, c.d_super,
+                c.ctl,   c.d_hctl,
+                c.count, R,
+                first,   maxit,
+                num_chunks(c.n), kNSeg,
+                0,       1,
+                nullptr, nullptr,
+                c.upd_seq};
+    fa.goflag = c.goflag;
+    if (int rc = enqueue_pass(c, &pose0, c.ctl, 1, ext, &sa, true, false, nullptr, &fa, maxit - first)) return rc;
+    SLIO_HSTAMP(c, 3);
+    SLIO_HIP(hipGetLastError());
+    return SLIO_OK;
+  }
+
   // multi-rank: the filter step of pass i after the all-reduce, on every rank
   int solve(int i) {
     const SolveArgs sa = args(i);
@@ -7366,6 +7634,10 @@ int slio_ikf_update_device(slio_handle h, slio_state* x, double P[576], double R
   UpdateRun u(c, x, P, R, maximum_iter, extrinsic_est, mode, reduce || comm);
   if (int rc = u.begin()) return rc;
   SLIO_HSTAMP(c, 1);
+  c.last_path = (!u.multi && u.persist_ok()) ? 1 : 0;
+  if (c.last_path) {
+    if (int rc = u.persist()) return rc;
+  } else
   for (int i = u.first; i < maximum_iter; ++i) {
     // single rank: the filter step runs in the super-sum kernel's last block
     // (or the search pass's tail); multi-rank: pass -> all-reduce of the

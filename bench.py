@@ -801,9 +801,14 @@ def main():
     iters_total = args.steps * passes
     value = iters_total / el
     avg_kernel_s = (ms.value / max(nl.value, 1)) * 1e-3
-    # algorithmic bytes per launch: every launch of the fused kernel is one
-    # pass, a search (109 B/pt) or, in the reference flow, a reuse (30 B/pt)
-    alg_bytes = (searches * BYTES_PER_SEARCH_PT + (passes - searches) * BYTES_PER_REUSE_PT) * shard_pts / passes
+    # algorithmic bytes per launch: a pass is a search (109 B/pt) or, in the
+    # reference flow, a reuse (30 B/pt); the persistent update runs every pass
+    # of an update in one launch, the per-pass path one pass per launch
+    persistent = (world == 1 and not args.host_loop and hasattr(lib, "slio_debug_update_path")
+                  and lib.slio_debug_update_path(h) == 1)
+    alg_bytes = (searches * BYTES_PER_SEARCH_PT + (passes - searches) * BYTES_PER_REUSE_PT) * shard_pts
+    if not persistent:
+        alg_bytes /= passes
     achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else None
     # x and P of the last update (every rank holds the same bits): lets a
     # multi-rank run be compared with a single-rank one
@@ -825,7 +830,7 @@ def main():
 
     l2 = None
     if rank == 0 and avg_kernel_s > 0 and args.mode == "fixed":
-        dem = l2_demand_bytes(mp, fr.body[b.value:e.value], st0, cell_m)
+        dem = l2_demand_bytes(mp, fr.body[b.value:e.value], st0, cell_m) * (passes if persistent else 1)
         l2 = {"demand_bytes_per_launch": dem, "achieved": dem / avg_kernel_s / 1e9,
               "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": dem / avg_kernel_s / 1e9 / L2_PEAK_GBS,
               "note": "L2-level roofline of the same launches: block-row candidates + "
@@ -902,9 +907,13 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_search_pass (fused: each launch also sums the pass and runs its filter step"
+            "kernel": (("k_update_persist (one launch per update: every pass, each summed and followed "
+                        "by its filter step inside the launch"
+                        if persistent else
+                        "k_search_pass (fused: each launch also sums the pass and runs its filter step")
                        + ("" if args.mode == "fixed" else "; search or reuse pass as the update decides")
                        + ")"),
+            "launch_covers": f"{passes} passes" if persistent else "1 pass",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

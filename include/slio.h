@@ -452,9 +452,14 @@ int slio_state_boxplus(const slio_state* x, const double dx[24], slio_state* out
 int slio_state_boxminus(const slio_state* x1, const slio_state* x2, double dx[24]);
 
 /* ---- diagnostics ----------------------------------------------------------- */
-/* Re-read the SLIO_NO_FUSE / SLIO_NO_FUSE0 / SLIO_NO_MFMA / SLIO_EVENT_WAIT
- * switches of the update path (read once at slio_create). */
+/* Re-read the SLIO_NO_FUSE / SLIO_NO_FUSE0 / SLIO_PERSIST / SLIO_NO_MFMA /
+ * SLIO_EVENT_WAIT / SLIO_NO_KNN_CERT switches of the update path (read once at
+ * slio_create). */
 int slio_debug_reload_switches(slio_handle h);
+/* How the last slio_ikf_update_device ran: 1 one persistent launch for all
+ * its passes (SLIO_PERSIST=1, single rank, fused configuration, every chunk's
+ * workgroup resident at once), 0 a launch (or two) per pass. */
+int slio_debug_update_path(slio_handle h);
 /* Host clock stamps (CLOCK_MONOTONIC ns) of the last slio_ikf_update_device:
  * [0] entry, [1] state set up, [2] control block + information-form constants
  * ready (fused path), [3] first launch enqueued, [4] every launch enqueued,

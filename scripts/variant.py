@@ -22,6 +22,13 @@ if ROOT not in sys.path:
 
 
 def use(path: str) -> C.CDLL:
+    # torch first, as in the product scripts: its HIP runtime must be the one
+    # loaded when the library's dependency resolves (the other order leaves
+    # torch with "No HIP GPUs are available")
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     from agi_lidar_slam_amd import _lib as L
     if L._lib is not None:
         raise RuntimeError("a library is already bound in this process")

@@ -310,6 +310,48 @@ def test_fused_fresh_handle_repeated(L, c2, mode, maxit):
         lib.slio_destroy(h)
 
 
+@pytest.mark.parametrize("npts,mode,ext,maxit", [
+    (100_000, 1, 0, 4), (100_000, 0, 0, 3), (100_000, 0, 0, 4), (8_320, 1, 0, 4),
+    (20_013, 0, 0, 4), (100_000, 1, 1, 4), (8_191, 0, 1, 3), (100_000, 1, 0, 1), (20_013, 1, 0, 9)])
+def test_persistent_update_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
+    """The persistent update (SLIO_PERSIST=1, k_update_persist: one launch,
+    every workgroup owns its chunk for all passes and waits between them for
+    the flag the pass's filter step publishes) against a fused launch per
+    pass (the default): x, P, the flags, the super rows and Nearest_Points
+    bit-for-bit, in both control flows (the reference flow ends early and
+    runs reuse passes), D = 6 / 12, one pass and more passes than before.  The
+    two paths alternate on one handle (pose slots, flags and certificates
+    carry over between updates of either kind)."""
+    mp, fr, _ = c2
+    st = state_of(fr)
+    body = np.ascontiguousarray(fr.body[:npts])
+    lib = L.load()
+    h = mk(L, cell=C2_CELL)
+
+    def persist(on):
+        if on:
+            monkeypatch.setenv("SLIO_PERSIST", "1")
+        else:
+            monkeypatch.delenv("SLIO_PERSIST", raising=False)
+        lib.slio_debug_reload_switches(h)
+
+    try:
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, body) == 0
+        persist(False)
+        per = _update_once(L, h, st, maxit=maxit, mode=mode, ext=ext)
+        assert lib.slio_debug_update_path(h) == 0
+        for rep in range(4):
+            persist(rep != 2)   # a per-pass update in between
+            got = _update_once(L, h, st, maxit=maxit, mode=mode, ext=ext)
+            assert lib.slio_debug_update_path(h) == (0 if rep == 2 else 1)
+            for a, b in zip(got, per):
+                np.testing.assert_array_equal(a, b)
+    finally:
+        persist(False)
+        lib.slio_destroy(h)
+
+
 @pytest.mark.parametrize("size", ["c1", "c2"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_device_update_vs_reference_gain(L, oracle_mod, c2, size, mode):
