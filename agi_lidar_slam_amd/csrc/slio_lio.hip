@@ -534,7 +534,10 @@ struct FeatCfg {
 };
 
 constexpr int kFeatThreads = 1024;
-constexpr int kPickThreads = 384;  // per (ring, sector): one wavefront per variant
+// per (ring, sector): one wavefront per variant (waves 6-7 join the shared
+// sector sort and reach phase only; all 8 sort the ring's VoxelGrid order in
+// the 7th workgroup of a ring, ring_vsort)
+constexpr int kPickThreads = 512;
 
 // Scratch of the feature stage, per ring r, sector j, variant v.
 // Sectors of a ring interact only through the suppression marks a sector's
@@ -558,7 +561,13 @@ struct FeatWork {
   int32_t* spos;      // [R][6][sort_cap]: sector positions in std::sort order
   PickVar* var;       // [R][6][6]
   int8_t* lab;        // [R][6][6][sort_cap]: labels of positions sp..ep
+  // the ring's VoxelGrid order, sorted beside the picks (ring_vsort):
+  // [R][kVsortN] (voxel << 32 | position) over every position of the ring's
+  // live sectors, and per ring their number (-1: k_fe_ring sorts itself)
+  uint64_t* vkey;
+  int32_t* vinfo;
 };
+constexpr int kVsortN = 2048;  // ring_vsort: rings of up to this many positions
 
 // sector j of a ring (featureExtraction.cpp:191-192)
 __device__ __forceinline__ void sector_bounds(int start, int end, int j, int& sp, int& ep) {
@@ -571,7 +580,7 @@ __device__ __forceinline__ void sector_bounds(int start, int end, int j, int& sp
 __device__ unsigned long long g_fstamp[256 * 36][6];
 #define FSTAMP(k)                                                                  \
   do {                                                                             \
-    if ((threadIdx.x & 63) == 0 && blockIdx.y < 256)                               \
+    if ((threadIdx.x & 63) == 0 && blockIdx.y < 256 && (threadIdx.x >> 6) < 6)     \
       g_fstamp[blockIdx.y * 36 + blockIdx.x * 6 + (threadIdx.x >> 6)][k] =         \
           __builtin_amdgcn_s_memrealtime();                                        \
   } while (0)
@@ -589,6 +598,146 @@ __device__ unsigned long long g_rstamp[256][8];
   do {             \
   } while (0)
 #endif
+
+// ---- ring_vsort: the 7th workgroup of ring r in k_fe_pick's grid, running
+// beside the ring's six sector picks.  k_fe_ring's VoxelGrid (pcl::VoxelGrid
+// on surfaceCloudScan, featureExtraction.cpp:265-269) sorts the ring's surface
+// list -- the live sectors' positions whose label is <= 0 -- by voxel index
+// (then list = position order).  That order does not depend on the picks:
+// the voxel index over any bounding box holding the points is a mixed-radix
+// number of (floor(z / leaf), floor(y / leaf), floor(x / leaf)), so its order
+// and its equal runs are those of the triple, whatever the box; and removing
+// the corner picks (label 1) from the sorted full list leaves the surface
+// list sorted.  So the full list is sorted here, over its own bounding box,
+// and k_fe_ring keeps the entries whose label is <= 0.  When this box would
+// overflow PCL's index check (the surface list's box is no larger, so a pass
+// here is a pass there) or the ring has more than kVsortN positions, vinfo is
+// -1 and k_fe_ring sorts the surface list itself.
+__device__ __forceinline__ void ring_vsort(const CloudInfo& ci, const FeatCfg& cfg, const FeatWork& fw,
+                                           unsigned char* smem) {
+  constexpr int kW = kPickThreads / 64, kE = kVsortN / (64 * kW), kQBits = __builtin_ctz(kVsortN);
+  constexpr int kHeld = kVsortN / kPickThreads;  // points per thread, kept in registers
+  static_assert(kVsortN % kPickThreads == 0 && (kW & (kW - 1)) == 0, "ring_vsort layout");
+  const int r = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int start = ci.start_ring[r], end = ci.end_ring[r];
+  __shared__ int s_lo[6], s_cnt[7];
+  __shared__ float wmn[kPickThreads / 64][3], wmx[kPickThreads / 64][3];
+  __shared__ int s_ok, s_minb[3], s_mul[3], s_narrow;
+  if (t == 0) {
+    int c = 0;
+    for (int j = 0; j < 6; ++j) {
+      int sp, ep;
+      sector_bounds(start, end, j, sp, ep);
+      s_lo[j] = sp;
+      s_cnt[j] = c;
+      if (sp < ep) c += ep - sp + 1;  // a live sector: positions sp..ep
+    }
+    s_cnt[6] = c;
+  }
+  __syncthreads();
+  const int m = s_cnt[6];
+  auto pos_of = [&](int i) {  // the i-th position of the live sectors, in order
+    int j = 0;
+#pragma unroll
+    for (int jj = 1; jj < 6; ++jj) j = i >= s_cnt[jj] ? jj : j;
+    return s_lo[j] + (i - s_cnt[j]);
+  };
+  if (end - start > kVsortN) {
+    if (t == 0) fw.vinfo[r] = -1;
+    return;
+  }
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  float4 held[kHeld];
+  int hq[kHeld];
+#pragma unroll
+  for (int k = 0; k < kHeld; ++k) {
+    const int i = t + k * kPickThreads;
+    hq[k] = i < m ? pos_of(i) : -1;
+    held[k] = i < m ? ci.xyzi[hq[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < kHeld; ++k) {
+    if (hq[k] < 0) continue;
+    const float4 p = held[k];
+    mn[0] = fminf(mn[0], p.x);
+    mn[1] = fminf(mn[1], p.y);
+    mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x);
+    mx[1] = fmaxf(mx[1], p.y);
+    mx[2] = fmaxf(mx[2], p.z);
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+    }
+  }
+  if (lane == 0)
+    for (int a = 0; a < 3; ++a) {
+      wmn[w][a] = mn[a];
+      wmx[w][a] = mx[a];
+    }
+  __syncthreads();
+  const float inv = 1.0f / cfg.leaf;
+  if (t == 0) {
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = wmn[0][a];
+      hi[a] = wmx[0][a];
+      for (int q = 1; q < kPickThreads / 64; ++q) {
+        lo[a] = fminf(lo[a], wmn[q][a]);
+        hi[a] = fmaxf(hi[a], wmx[q][a]);
+      }
+    }
+    // k_fe_ring's check on this box (PCL applyFilter's overflow test)
+    const int64_t dx = (int64_t)((hi[0] - lo[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((hi[1] - lo[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((hi[2] - lo[2]) * inv) + 1;
+    int64_t divb[3];
+    for (int a = 0; a < 3; ++a) {
+      s_minb[a] = (int)floorf(lo[a] * inv);
+      divb[a] = (int64_t)((int)floorf(hi[a] * inv) - s_minb[a] + 1);
+    }
+    const int64_t cells = divb[0] * divb[1] * divb[2];
+    s_ok = m > 0 && dx * dy * dz <= (int64_t)2147483647 && cells <= (int64_t)2147483647;
+    s_mul[0] = 1;
+    s_mul[1] = (int)divb[0];
+    s_mul[2] = (int)(divb[0] * divb[1]);
+    const uint32_t top = s_ok ? (uint32_t)(cells - 1) : 0u;
+    s_narrow = (top ? 32 - __clz((int)top) : 1) + kQBits <= 32;
+  }
+  __syncthreads();
+  if (!s_ok) {
+    if (t == 0) fw.vinfo[r] = m > 0 ? -1 : 0;
+    return;
+  }
+  auto voxel_of = [&](const float4& p) {
+    const int i0 = (int)(floorf(p.x * inv) - (float)s_minb[0]);
+    const int i1 = (int)(floorf(p.y * inv) - (float)s_minb[1]);
+    const int i2 = (int)(floorf(p.z * inv) - (float)s_minb[2]);
+    return (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
+  };
+  uint64_t* out = fw.vkey + (int64_t)r * kVsortN;
+  if (s_narrow) {
+    uint32_t* k32 = reinterpret_cast<uint32_t*>(smem);
+#pragma unroll
+    for (int k = 0; k < kHeld; ++k)
+      k32[t + k * kPickThreads] = hq[k] >= 0 ? (voxel_of(held[k]) << kQBits) | (uint32_t)(hq[k] - start) : ~0u;
+    sort_keys_lds<kW, kE, uint32_t>(k32);
+    for (int i = t; i < m; i += kPickThreads)
+      out[i] = ((uint64_t)(k32[i] >> kQBits) << 32) | (uint32_t)(start + (int)(k32[i] & (kVsortN - 1)));
+  } else {
+    uint64_t* k64 = reinterpret_cast<uint64_t*>(smem);
+#pragma unroll
+    for (int k = 0; k < kHeld; ++k)
+      k64[t + k * kPickThreads] = hq[k] >= 0 ? ((uint64_t)voxel_of(held[k]) << 32) | (uint32_t)hq[k] : ~0ull;
+    sort_keys_lds<kW, kE>(k64);
+    for (int i = t; i < m; i += kPickThreads) out[i] = k64[i];
+  }
+  if (t == 0) fw.vinfo[r] = m;
+}
 
 // ---- k_fe_pick: grid (6, R), 6 wavefronts: sector j of ring r.  The block
 // loads the sector (curvature, columns, flags, reach) and sorts it once:
@@ -612,6 +761,10 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   static_assert(SORTN >= 64 && SORTN <= 2048 && (SORTN & (SORTN - 1)) == 0, "sort size");
   constexpr int kSortW = SORTN >= 256 ? 4 : SORTN / 64, kSortE = SORTN / (64 * kSortW);
+  if (blockIdx.x == 6) {  // the ring's VoxelGrid order (ring_vsort)
+    ring_vsort(ci, cfg, fw, smem);
+    return;
+  }
   const int j = blockIdx.x, r = blockIdx.y;
   const int t = threadIdx.x, lane = t & 63, v = t >> 6;
   const int n = *ci.n_ext;
@@ -621,7 +774,7 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   int sp, ep;
   sector_bounds(start, end, j, sp, ep);
   if (sp >= ep) {  // `if (sp >= ep) continue;`
-    if (lane == 0 && (j > 0 || v == 0)) {
+    if (lane == 0 && v < 6 && (j > 0 || v == 0)) {
       PickVar* pv = fw.var + (r * 6 + j) * 6 + v;
       pv->ncorner = 0;
       pv->nflat = 0;
@@ -683,7 +836,7 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     reach[q - pb] = (uint8_t)(rl | (rr << 4));
   }
   __syncthreads();
-  if (j == 0 && v > 0) return;  // nothing precedes the first sector
+  if (v >= 6 || (j == 0 && v > 0)) return;  // 6 variants; nothing precedes the first sector
   FSTAMP(2);
   const int slot = (r * 6 + j) * 6 + v;
   PickVar* pv = fw.var + slot;
@@ -806,6 +959,41 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   FSTAMP(5);
 }
 
+// The VoxelGrid's output from the surface list in voxel order: keys[q] =
+// voxel << 32 | ring position (m entries, in LDS), points from rp.  One
+// thread per voxel run start sums the run's points in list order
+// (CentroidPoint); voxels go out in ascending index (applyFilter).
+template <int NT>
+__device__ __forceinline__ void ring_voxels(const uint64_t* keys, float4* vp, const float4* rp, int start, int m,
+                                            float4* dst, int* scratch, int32_t* count) {
+  const int t = threadIdx.x;
+  for (int q = t; q < m; q += NT) vp[q] = rp[(int)(uint32_t)keys[q] - start];
+  __syncthreads();
+  const int per = (m + NT - 1) / NT;
+  const int q0 = t * per, q1 = min(q0 + per, m);
+  int starts = 0;
+  for (int q = q0; q < q1; ++q) starts += (q == 0) || ((keys[q] >> 32) != (keys[q - 1] >> 32));
+  int excl;
+  const int nvox = block_exclusive_scan<NT>(starts, scratch, excl);
+  int o = excl;
+  for (int q = q0; q < q1; ++q) {
+    if (!((q == 0) || ((keys[q] >> 32) != (keys[q - 1] >> 32)))) continue;
+    const uint32_t id = (uint32_t)(keys[q] >> 32);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int e = q;
+    for (; e < m && (uint32_t)(keys[e] >> 32) == id; ++e) {
+      const float4 p = vp[e];
+      s0 += p.x;
+      s1 += p.y;
+      s2 += p.z;
+      s3 += p.w;
+    }
+    const float cnt = (float)(e - q);
+    dst[o++] = make_float4(s0 / cnt, s1 / cnt, s2 / cnt, s3 / cnt);
+  }
+  if (t == 0) *count = nvox;
+}
+
 // ---- k_fe_ring: one workgroup per ring.  Variant selection (sector j gets
 // the prefix v_j the earlier sectors' marks reach), the ring's labels,
 // corners in pick order, surfaceCloudScan (:265-269: sector positions with
@@ -839,6 +1027,16 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int start = ci.start_ring[r], end = ci.end_ring[r];
   RGSTAMP(0);
+  // the ring's presorted VoxelGrid order (ring_vsort, beside the picks):
+  // this thread's share of the entries, loaded with the ring
+  const int vm = fw.vinfo ? fw.vinfo[r] : -1;
+  constexpr int kVPer = (kVsortN + kFeatThreads - 1) / kFeatThreads;
+  uint64_t vk[kVPer];
+#pragma unroll
+  for (int i = 0; i < kVPer; ++i) {
+    const int e = t * kVPer + i;
+    vk[i] = (vm > 0 && e < vm) ? fw.vkey[(int64_t)r * kVsortN + e] : 0ull;
+  }
   // the ring's points, loaded once (corners, surface list and voxel grid
   // read them from LDS)
   for (int q = start + t; q <= end; q += kFeatThreads) rp[q - start] = ci.xyzi[q];
@@ -911,6 +1109,31 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
   }
   __syncthreads();
   RGSTAMP(2);
+  float4* dst = out.surf_stage + (start - 4);  // ring's first extracted index
+  if (vm >= 0) {
+    // presorted: keep the entries whose label is <= 0 (the surface list, in
+    // VoxelGrid order), then the voxels' centroids below
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kVPer; ++i) {
+      const int e = t * kVPer + i;
+      cnt += e < vm && labr[(int)(uint32_t)vk[i] - start] <= 0;
+    }
+    int excl;
+    const int mk = block_exclusive_scan<kFeatThreads>(cnt, scratch, excl);
+#pragma unroll
+    for (int i = 0; i < kVPer; ++i) {
+      const int e = t * kVPer + i;
+      if (e < vm && labr[(int)(uint32_t)vk[i] - start] <= 0) keys[excl++] = vk[i];
+    }
+    __syncthreads();
+    if (mk == 0) {
+      if (t == 0) out.surf_count[r] = 0;
+      return;
+    }
+    ring_voxels<kFeatThreads>(keys, vp, rp, start, mk, dst, scratch, out.surf_count + r);
+    return;
+  }
   int m;
   {
     const int per = (end - start + 1 + kFeatThreads - 1) / kFeatThreads;
@@ -924,7 +1147,6 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
   }
   __syncthreads();
   RGSTAMP(3);
-  float4* dst = out.surf_stage + (start - 4);  // ring's first extracted index
   if (m == 0) {
     if (t == 0) out.surf_count[r] = 0;
     return;
@@ -1030,32 +1252,12 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
     RGSTAMP(5);
     sort_keys_lds<kSortW, kSortE>(keys);
   }
-  for (int q = t; q < m; q += kFeatThreads) vp[q] = rp[slist[(uint32_t)keys[q]] - start];
+  // (the keys' low words become ring positions: the list entries' own)
+  for (int q = t; q < m; q += kFeatThreads)
+    keys[q] = (keys[q] & 0xFFFFFFFF00000000ull) | (uint32_t)slist[(uint32_t)keys[q]];
   __syncthreads();
   RGSTAMP(6);
-  const int per = (m + kFeatThreads - 1) / kFeatThreads;
-  const int q0 = t * per, q1 = min(q0 + per, m);
-  int starts = 0;
-  for (int q = q0; q < q1; ++q) starts += (q == 0) || ((keys[q] >> 32) != (keys[q - 1] >> 32));
-  int excl;
-  const int nvox = block_exclusive_scan<kFeatThreads>(starts, scratch, excl);
-  int o = excl;
-  for (int q = q0; q < q1; ++q) {
-    if (!((q == 0) || ((keys[q] >> 32) != (keys[q - 1] >> 32)))) continue;
-    const uint32_t id = (uint32_t)(keys[q] >> 32);
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int e = q;
-    for (; e < m && (uint32_t)(keys[e] >> 32) == id; ++e) {
-      const float4 p = vp[e];
-      s0 += p.x;
-      s1 += p.y;
-      s2 += p.z;
-      s3 += p.w;
-    }
-    const float cnt = (float)(e - q);
-    dst[o++] = make_float4(s0 / cnt, s1 / cnt, s2 / cnt, s3 / cnt);
-  }
-  if (t == 0) out.surf_count[r] = nvox;
+  ring_voxels<kFeatThreads>(keys, vp, rp, start, m, dst, scratch, out.surf_count + r);
   RGSTAMP(7);
 }
 
@@ -1065,7 +1267,9 @@ struct FeatSmem {
 };
 inline FeatSmem feat_smem_sizes(const FeatCfg& fc) {
   const size_t pcap = (size_t)fc.sort_cap + 16;
-  return FeatSmem{12 * (size_t)fc.sort_cap + (4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
+  // (k_fe_pick's 7th workgroup per ring sorts kVsortN keys in the same LDS)
+  return FeatSmem{std::max(12 * (size_t)fc.sort_cap + (4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
+                           sizeof(uint64_t) * (size_t)kVsortN),
                   24 * (size_t)fc.vox_cap + 21 * (size_t)fc.ring_cap};
 }
 // the sorts' sizes (powers of two; 0: capacity not supported)
@@ -1084,11 +1288,13 @@ inline hipError_t feat_work_alloc(FeatWork& fw, int R, const FeatCfg& fc) {
   A(fw.spos, 4 * (size_t)6 * R * fc.sort_cap);
   A(fw.var, sizeof(PickVar) * 36 * (size_t)R);
   A(fw.lab, (size_t)36 * R * fc.sort_cap);
+  A(fw.vkey, sizeof(uint64_t) * kVsortN * (size_t)R);
+  A(fw.vinfo, sizeof(int32_t) * (size_t)R);
   return e;
 }
 
 inline void feat_work_free(FeatWork& fw) {
-  void* p[] = {fw.spos, fw.var, fw.lab};
+  void* p[] = {fw.spos, fw.var, fw.lab, fw.vkey, fw.vinfo};
   for (void* q : p)
     if (q) (void)hipFree(q);
   fw = FeatWork{};
@@ -1137,7 +1343,7 @@ inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, const flo
                             const uint8_t* picked0, const FeatCfg& fc, const FeatOut& fo,
                             const FeatWork& fw, std::pair<hipEvent_t, hipEvent_t> ev) {
   const FeatSmem sm = feat_smem_sizes(fc);
-  const dim3 gs(6, R);
+  const dim3 gs(7, R);  // 6 sectors + the ring's VoxelGrid order (ring_vsort)
   const uint32_t ps = (uint32_t)sm.pick;
   const uint8_t* gr = fo.ground;
 #define SLIO_PICK(N)                                                                                     \

@@ -86,7 +86,8 @@ def test_c3_ouster_bitexact(oracle_mod, c3, deskew):
 
 @pytest.mark.parametrize("seed,n_scan,horizon,ds,order", [
     (3, 8, 96, 1, "ring"), (4, 8, 96, 2, "shuffled"), (5, 6, 160, 1, "shuffled"),
-    (6, 16, 1800, 1, "ring"), (7, 3, 512, 1, "reversed")])
+    (6, 16, 1800, 1, "ring"), (7, 3, 512, 1, "reversed"),
+    (9, 2, 2048, 1, "ring")])   # rings of the largest horizon (ring_vsort's 2048 keys)
 def test_small_scans(oracle_mod, seed, n_scan, horizon, ds, order):
     from agi_lidar_slam_amd.frontend import imu_deskew_table
     sc = small_scan(seed, n_scan=n_scan, horizon=horizon)
@@ -112,6 +113,21 @@ def test_thresholds_and_leaf(oracle_mod):
     try:
         ci = check_projection(fe, ref, False)
         check_features(fe, ci, 8, oracle_mod, edge_threshold=0.5, surf_threshold=0.3, leaf=1.5)
+    finally:
+        fe.close()
+
+
+@pytest.mark.parametrize("leaf", [1e-3, 0.05])
+def test_voxel_grid_overflow_and_fine_leaf(oracle_mod, leaf):
+    """VoxelGrid with a leaf so fine that the ring's bounding box overflows
+    PCL's index check (1e-3 m: output = input, k_fe_ring's own path) or
+    nearly every point is its own voxel (0.05 m: the presorted path)."""
+    sc = small_scan(10, n_scan=8, horizon=256)
+    ref = oracle_mod.lio_project(sc, 8, 256, None)
+    fe = gpu_run(sc, 8, 256, None, odometrySurfLeafSize=leaf)
+    try:
+        ci = check_projection(fe, ref, False)
+        check_features(fe, ci, 8, oracle_mod, leaf=leaf)
     finally:
         fe.close()
 
