@@ -1,6 +1,6 @@
 // slio_lio.hip -- LIO-SAM front-end on gfx950.
 //
-// One scan = 7 launches on the handle's stream:
+// One scan = 6 launches on the handle's stream:
 //   (no reset of the cell owners: they carry the scan's generation)
 //   k_lio_claim   per point        projectPointCloud filters (:614-636); the
 //                                  cell goes to the smallest point index
@@ -10,18 +10,20 @@
 //                                  valid point; per-ring valid counts
 //   k_lio_extract block per ring   cloudExtraction (:656-678): ring offsets,
 //                                  start/endRingIndex, in-ring stream compaction
-//   k_lio_smooth  per point        calculateSmoothness (featureExtraction.cpp
-//                                  :108-131) + markOccludedPoints (:137-177) in
-//                                  pull form (each flag computed by its owner)
-//   k_fe_pick     block per (ring, sector)  extractFeatures (:183-296): the
-//                                  sector's std::sort (block radix sort), then
+//   k_fe_pick     block per (ring, sector)  calculateSmoothness
+//                                  (featureExtraction.cpp:108-131) +
+//                                  markOccludedPoints (:137-177) of the sector
+//                                  in pull form (each flag computed by its
+//                                  owner, from LDS), extractFeatures (:183-296):
+//                                  the sector's std::sort (bitonic), then
 //                                  one wavefront per variant: the greedy edge /
 //                                  flat picks (ballot over 64 candidates), once
 //                                  per possible prefix of marks from the
-//                                  previous sector (0..5 points)
+//                                  previous sector (0..5 points); a 7th block
+//                                  per ring sorts its VoxelGrid order (ring_vsort)
 //   k_fe_ring     block per ring   variant chain (exact sequential result),
 //                                  labels, corners, surfaceCloudScan, and
-//                                  pcl::VoxelGrid (radix sort, centroids)
+//                                  pcl::VoxelGrid (the presorted order, centroids)
 //   k_lio_concat  block per ring   ring-ordered cloud_corner / cloud_surface
 // Rings are independent in extractFeatures (suppression reaches 5 points, the
 // gap between rings' candidate ranges is 10); sectors within a ring interact
@@ -482,14 +484,13 @@ __device__ __forceinline__ bool occ_b(const float* r, const int32_t* col, int j)
   return cd < 10 && !((double)(r[j] - r[j + 1]) > 0.3) && (double)(r[j + 1] - r[j]) > 0.3;
 }
 
-__global__ __launch_bounds__(256) void k_lio_smooth(const float* __restrict__ r,
-                                                    const int32_t* __restrict__ col,
-                                                    const int32_t* n_ext, float* curvature,
-                                                    uint8_t* picked, int32_t* label) {
-  const int n = *n_ext;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float curv = 0.0f;
+// calculateSmoothness + markOccludedPoints of position i of the extracted
+// cloud (n points): r / col are range and column arrays indexed so that
+// r[q], col[q] hold position q's for q in [i - 6, i + 6] (k_fe_pick stages
+// them in LDS).
+__device__ __forceinline__ void smooth_at(const float* r, const int32_t* col, int n, int i, float& curv,
+                                          uint8_t& picked) {
+  curv = 0.0f;
   int pk = 1;  // entries the reference never initialises: never picked
   if (i >= 5 && i < n - 5) {
     const float diffRange = r[i - 5] + r[i - 4] + r[i - 3] + r[i - 2] + r[i - 1] - r[i] * 10 +
@@ -507,9 +508,7 @@ __global__ __launch_bounds__(256) void k_lio_smooth(const float* __restrict__ r,
       if ((double)diff1 > 0.02 * (double)r[i] && (double)diff2 > 0.02 * (double)r[i]) pk = 1;
     }
   }
-  curvature[i] = curv;
-  picked[i] = (uint8_t)pk;
-  label[i] = 0;  // k_lio_features writes the rings' [start, end]
+  picked = (uint8_t)pk;
 }
 
 struct FeatOut {
@@ -538,6 +537,10 @@ constexpr int kFeatThreads = 1024;
 // sector sort and reach phase only; all 8 sort the ring's VoxelGrid order in
 // the 7th workgroup of a ring, ring_vsort)
 constexpr int kPickThreads = 512;
+// k_fe_pick's per-position LDS arrays: sort_cap + kPickPad entries (a sector,
+// its 5-point margins, the last sector's extra point, and the 6-point halos
+// of the staged range / columns, kHalo on each side)
+constexpr int kPickPad = 32, kHalo = 6;
 
 // Scratch of the feature stage, per ring r, sector j, variant v.
 // Sectors of a ring interact only through the suppression marks a sector's
@@ -756,7 +759,7 @@ __device__ __forceinline__ void ring_vsort(const CloudInfo& ci, const FeatCfg& c
 // flats only on the ground, at most 4 per sector (the 4th does not suppress).
 template <int MODE, int SORTN>
 __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
-    const CloudInfo ci, const float* __restrict__ curvature, const uint8_t* __restrict__ picked0,
+    const CloudInfo ci, float* __restrict__ curvature, uint8_t* __restrict__ picked0, int32_t* __restrict__ label,
     const uint8_t* __restrict__ ground, FeatCfg cfg, FeatWork fw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   static_assert(SORTN >= 64 && SORTN <= 2048 && (SORTN & (SORTN - 1)) == 0, "sort size");
@@ -773,6 +776,51 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   const int span_end = min(end + 5, n - 1);
   int sp, ep;
   sector_bounds(start, end, j, sp, ep);
+  const int cap = cfg.sort_cap, pcap = cfg.sort_cap + kPickPad;
+  const int pb = max(sp - 5, base), pe = min(ep + 5, span_end);
+  // this block's share of the ring's points [start - 4, end + 5] for the
+  // smoothness outputs (sector j's positions; the first / last sector also
+  // the ring's 4 / 6 points outside every sector)
+  const int wlo = max(j == 0 ? start - 4 : sp, 0), whi = min(j == 5 ? end + 5 : ep, n - 1);
+  // LDS index base: pb (a live sector's share starts at or after pb; a ring
+  // with fewer than 11 points has no live sector, and its shares may reach
+  // back into the previous ring)
+  const int lb = min(pb, wlo), hi = max(pe, whi);
+  uint64_t* skey = reinterpret_cast<uint64_t*>(smem);  // SORTN (= cap) sort keys
+  int32_t* spos = reinterpret_cast<int32_t*>(skey + SORTN);  // the sector in sort order
+  float* curv = reinterpret_cast<float*>(spos + cap);
+  int32_t* col = reinterpret_cast<int32_t*>(curv + pcap) + kHalo;  // col[q - pb], q >= pb - kHalo
+  float* rng = reinterpret_cast<float*>(col - kHalo + pcap) + kHalo;  // range, as col
+  uint8_t* pk0 = reinterpret_cast<uint8_t*>(rng - kHalo + pcap);  // cloudNeighborPicked on entry
+  uint8_t* brk = pk0 + pcap;    // column step into position q exceeds 10
+  uint8_t* reach = brk + pcap;  // reachL | reachR << 4
+  uint8_t* gfl = reach + pcap;  // LeGO: segmentedCloudGroundFlag
+  // the wavefront's own flags and labels: written by one lane and read by
+  // the others of the wavefront: volatile LDS accesses, in program order
+  volatile uint8_t* flag = reinterpret_cast<volatile uint8_t*>(gfl + pcap) + v * 2 * pcap;
+  volatile int8_t* lab = reinterpret_cast<volatile int8_t*>(flag + pcap);
+  // calculateSmoothness + markOccludedPoints (featureExtraction.cpp:108-176)
+  // for [lb, hi] from range / column staged over [lb - 6, hi + 6]
+  for (int q = max(lb - kHalo, 0) + t; q <= min(hi + kHalo, n - 1); q += kPickThreads) {
+    rng[q - lb] = ci.prange[q];
+    col[q - lb] = ci.col_ind[q];
+  }
+  if (MODE == kModeLego)
+    for (int q = pb + t; q <= pe; q += kPickThreads) gfl[q - pb] = ground[q];
+  __syncthreads();
+  for (int q = lb + t; q <= hi; q += kPickThreads) {
+    float c;
+    uint8_t pk;
+    smooth_at(rng - lb, col - lb, n, q, c, pk);
+    curv[q - lb] = c;
+    pk0[q - lb] = pk;
+  }
+  __syncthreads();
+  for (int q = wlo + t; q <= whi; q += kPickThreads) {
+    curvature[q] = curv[q - lb];
+    picked0[q] = pk0[q - lb];
+    label[q] = 0;  // k_fe_ring writes the rings' [start, end]
+  }
   if (sp >= ep) {  // `if (sp >= ep) continue;`
     if (lane == 0 && v < 6 && (j > 0 || v == 0)) {
       PickVar* pv = fw.var + (r * 6 + j) * 6 + v;
@@ -783,32 +831,12 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     return;
   }
   FSTAMP(0);
-  const int cap = cfg.sort_cap, pcap = cfg.sort_cap + 16;
-  const int pb = max(sp - 5, base), pe = min(ep + 5, span_end);
-  uint64_t* skey = reinterpret_cast<uint64_t*>(smem);  // SORTN (= cap) sort keys
-  int32_t* spos = reinterpret_cast<int32_t*>(skey + SORTN);  // the sector in sort order
-  float* curv = reinterpret_cast<float*>(spos + cap);
-  int32_t* col = reinterpret_cast<int32_t*>(curv + pcap);
-  uint8_t* pk0 = reinterpret_cast<uint8_t*>(col + pcap);  // cloudNeighborPicked on entry
-  uint8_t* brk = pk0 + pcap;    // column step into position q exceeds 10
-  uint8_t* reach = brk + pcap;  // reachL | reachR << 4
-  uint8_t* gfl = reach + pcap;  // LeGO: segmentedCloudGroundFlag
-  // the wavefront's own flags and labels: written by one lane and read by
-  // the others of the wavefront: volatile LDS accesses, in program order
-  volatile uint8_t* flag = reinterpret_cast<volatile uint8_t*>(gfl + pcap) + v * 2 * pcap;
-  volatile int8_t* lab = reinterpret_cast<volatile int8_t*>(flag + pcap);
-  for (int q = pb + t; q <= pe; q += kPickThreads) {
-    curv[q - pb] = curvature[q];
-    col[q - pb] = ci.col_ind[q];
-    pk0[q - pb] = picked0[q];
-    if (MODE == kModeLego) gfl[q - pb] = ground[q];
-  }
   // the sector's sort: (value bits, position) keys, bitonic in registers and
   // LDS (sort_keys_lds) -- the stable sort by value
   const int len = ep - sp;
   for (int idx = t; idx < SORTN; idx += kPickThreads) {
     const int k = sp + idx;
-    skey[idx] = idx < len ? ((uint64_t)__float_as_uint((k >= 5 && k < n - 5) ? curvature[k] : 0.0f) << 32) |
+    skey[idx] = idx < len ? ((uint64_t)__float_as_uint((k >= 5 && k < n - 5) ? curv[k - pb] : 0.0f) << 32) |
                                 (uint32_t)k
                           : ~0ull;
   }
@@ -1127,11 +1155,13 @@ __global__ __launch_bounds__(kFeatThreads) void k_fe_ring(const CloudInfo ci, Fe
       if (e < vm && labr[(int)(uint32_t)vk[i] - start] <= 0) keys[excl++] = vk[i];
     }
     __syncthreads();
+    RGSTAMP(3);
     if (mk == 0) {
       if (t == 0) out.surf_count[r] = 0;
       return;
     }
     ring_voxels<kFeatThreads>(keys, vp, rp, start, mk, dst, scratch, out.surf_count + r);
+    RGSTAMP(7);
     return;
   }
   int m;
@@ -1266,9 +1296,9 @@ struct FeatSmem {
   size_t pick, ring;
 };
 inline FeatSmem feat_smem_sizes(const FeatCfg& fc) {
-  const size_t pcap = (size_t)fc.sort_cap + 16;
+  const size_t pcap = (size_t)fc.sort_cap + kPickPad;
   // (k_fe_pick's 7th workgroup per ring sorts kVsortN keys in the same LDS)
-  return FeatSmem{std::max(12 * (size_t)fc.sort_cap + (4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
+  return FeatSmem{std::max(12 * (size_t)fc.sort_cap + (4 + 4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
                            sizeof(uint64_t) * (size_t)kVsortN),
                   24 * (size_t)fc.vox_cap + 21 * (size_t)fc.ring_cap};
 }
@@ -1339,8 +1369,8 @@ inline void feat_set_smem(const FeatSmem& s, int sitems, int vitems) {
 // extractFeatures + per-ring VoxelGrid: 2 launches; ev brackets them (the
 // front-end bench's feature-stage timing)
 template <int MODE>
-inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, const float* curv,
-                            const uint8_t* picked0, const FeatCfg& fc, const FeatOut& fo,
+inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, float* curv,
+                            uint8_t* picked0, const FeatCfg& fc, const FeatOut& fo,
                             const FeatWork& fw, std::pair<hipEvent_t, hipEvent_t> ev) {
   const FeatSmem sm = feat_smem_sizes(fc);
   const dim3 gs(7, R);  // 6 sectors + the ring's VoxelGrid order (ring_vsort)
@@ -1349,7 +1379,7 @@ inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, const flo
 #define SLIO_PICK(N)                                                                                     \
   case N:                                                                                              \
     hipExtLaunchKernelGGL((k_fe_pick<MODE, N>), gs, dim3(kPickThreads), ps, s, ev.first, nullptr, 0, ci, \
-                          curv, picked0, gr, fc, fw);                                                  \
+                          curv, picked0, fo.label, gr, fc, fw);                                        \
     break
   switch (sort_items(fc.sort_cap)) {
     SLIO_PICK(64);
@@ -1703,8 +1733,6 @@ int slio_lio_run_async(slio_lio_handle h) {
       in, g, h->owner, hi, h->block_first, nclaim, d, h->range_mat, h->full, h->row_count);
   const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->prange, h->xyzi, h->n_ext};
   k_lio_extract<<<R, kRowThreads, 0, h->stream>>>(g, h->range_mat, h->full, h->row_count, ci);
-  k_lio_smooth<<<(unsigned)((g.cells + 255) / 256), 256, 0, h->stream>>>(
-      h->prange, h->col_ind, h->n_ext, h->curvature, h->picked0, h->label);
   const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
                    nullptr, nullptr, nullptr, nullptr, nullptr};
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
@@ -1856,8 +1884,9 @@ int slio_lio_get_clouds(slio_lio_handle h, float* corner_xyzi, float* surface_xy
 //   k_lego_label     per cell    labelMat (label, 999999 or -1)
 //   k_lego_half      per point   adjustDistortion's halfPassed switch point
 //   k_lego_deskew    per point   adjustDistortion (:617-805)
-//   k_lio_smooth     per point   calculateSmoothness + markOccludedPoints
-//   k_fe_features<kModeLego>     extractFeatures (:883-1007) + VoxelGrid 0.2
+//   k_fe_pick<kModeLego>  calculateSmoothness + markOccludedPoints +
+//                         extractFeatures (:883-1007); VoxelGrid order
+//   k_fe_ring<kModeLego>  variant chain, labels, VoxelGrid 0.2
 //   k_lego_concat    per ring    sharp / less sharp / flat / less flat clouds
 // ======================================================================
 namespace slio {
@@ -3500,8 +3529,6 @@ int slio_lego_run_async(slio_lego_handle h) {
   k_lego_deskew<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->slot, nslot, h->orient[0],
                                             h->orient[1], h->orient[2], h->prm.scan_period, h->imu,
                                             h->desk, h->io);
-  k_lio_smooth<<<cb, 256, 0, h->stream>>>(h->srange, h->col_ind, h->nseg, h->curvature, h->picked0,
-                                          h->flabel);
   const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->srange, h->desk, h->nseg};
   const FeatOut fo{h->flabel, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
                    h->corner_sharp, h->sharp_count, h->flat_stage, h->flat_count, h->gflag};

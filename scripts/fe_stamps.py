@@ -1,5 +1,5 @@
 """Phase stamps of k_fe_pick (diagnostic build -DSLIO_FE_STAMP,
-SLIO_LIB=agi_lidar_slam_amd/_abl/libslio_fe.so) on the C3 scan."""
+SLIO_LIB=_var/libslio_fe.so, OUT=_var bash scripts/build_variant.sh fe -DSLIO_FE_STAMP) on the C3 scan."""
 import ctypes as C
 import os
 import sys
@@ -38,8 +38,13 @@ lib.slio_dbg_ring_stamps.argtypes = [C.POINTER(C.c_ulonglong)]
 rb = (C.c_ulonglong * (256 * 8))()
 assert lib.slio_dbg_ring_stamps(rb) == 0
 rv = np.array(rb[:], dtype=np.int64).reshape(256, 8)[:64]
-rp = np.diff(rv, axis=1) / 100.0
-for k, nm in enumerate(["hdr+chain", "labels+corners", "surface scan", "bbox", "keys", "sort", "centroids"]):
+if (rv[:, 4] == 0).all():  # presorted VoxelGrid order (ring_vsort): stamps 0-3 and 7
+    rp = np.stack([rv[:, 1] - rv[:, 0], rv[:, 2] - rv[:, 1], rv[:, 3] - rv[:, 2], rv[:, 7] - rv[:, 3]], 1) / 100.0
+    phases = ["hdr+chain", "labels+corners", "keep label<=0", "centroids"]
+else:
+    rp = np.diff(rv, axis=1) / 100.0
+    phases = ["hdr+chain", "labels+corners", "surface scan", "bbox", "keys", "sort", "centroids"]
+for k, nm in enumerate(phases):
     print(f"ring {nm:15s} mean {rp[:, k].mean():6.2f} max {rp[:, k].max():6.2f} us")
 print(f"ring kernel: start spread {(rv[:, 0].max() - rv[:, 0].min()) / 100:.2f} us, "
       f"total mean {((rv[:, 7] - rv[:, 0]) / 100).mean():.2f} us")
