@@ -85,6 +85,7 @@ struct Deskew {
   int cur;  // imuPointerCur
   double t0;  // timeScanCur
   int on;
+  int sorted;  // imuTime non-decreasing: findRotation's scan is a binary search
 };
 
 // ---------------------------------------------------------------- math
@@ -156,10 +157,27 @@ __device__ Aff compose(const Aff& l, const Aff& r) {
 
 // findRotation (imageProjection.cpp:492-529)
 __device__ void find_rotation(const Deskew& d, double pointTime, float& ox, float& oy, float& oz) {
+  // the first f < cur with pointTime < imuTime[f], else cur: over a
+  // non-decreasing table that predicate is monotone in f, so a binary search
+  // finds the same f as the reference's linear scan (a NaN time: cur in both)
   int f = 0;
-  while (f < d.cur) {
-    if (pointTime < d.t[f]) break;
-    ++f;
+  if (d.sorted) {
+    int lo = 0, n = d.cur;
+    while (n > 0) {
+      const int h = n >> 1;
+      if (!(pointTime < d.t[lo + h])) {
+        lo += h + 1;
+        n -= h + 1;
+      } else {
+        n = h;
+      }
+    }
+    f = lo;
+  } else {
+    while (f < d.cur) {
+      if (pointTime < d.t[f]) break;
+      ++f;
+    }
   }
   if (pointTime > d.t[f] || f == 0) {
     ox = (float)d.rx[f];
@@ -368,6 +386,24 @@ __global__ __launch_bounds__(kFillThreads) void k_lio_fill(In in, Geo g, const u
   const int r = blockIdx.x, sp = blockIdx.y;
   const int t = threadIdx.x;
   const bool desk = d.on && d.cur > 0;
+  const int c0 = (int)((int64_t)g.horizon * sp / kFillSplit);
+  const int c1 = (int)((int64_t)g.horizon * (sp + 1) / kFillSplit);
+  // the thread's first cell: its owner and point loads go out before the
+  // scan-start rotation below (independent chains, overlapped)
+  const int colA = c0 + t;
+  uint32_t oA = kNone;
+  float pxA = 0.f, pyA = 0.f, pzA = 0.f, inA = 0.f, tmA = 0.f;
+  if (colA < c1) {
+    const unsigned long long ok = owner[colA + (int64_t)r * g.horizon];
+    oA = (uint32_t)(ok >> 32) == hi ? (uint32_t)ok : kNone;
+    if (oA != kNone) {
+      pxA = in.x[oA];
+      pyA = in.y[oA];
+      pzA = in.z[oA];
+      inA = in.in[oA];
+      if (desk) tmA = in.time[oA];
+    }
+  }
   if (desk) {
     if (d.cur < kImuLds) {
       for (int q = t; q <= d.cur; q += kFillThreads) {
@@ -398,29 +434,44 @@ __global__ __launch_bounds__(kFillThreads) void k_lio_fill(In in, Geo g, const u
     }
     __syncthreads();
   }
-  const int c0 = (int)((int64_t)g.horizon * sp / kFillSplit);
-  const int c1 = (int)((int64_t)g.horizon * (sp + 1) / kFillSplit);
   int cnt = 0;
-  for (int col = c0 + t; col < c1; col += kFillThreads) {
+  for (int col = colA; col < c1; col += kFillThreads) {
     const int64_t c = col + (int64_t)r * g.horizon;
-    const unsigned long long ok = owner[c];
-    const uint32_t o = (uint32_t)(ok >> 32) == hi ? (uint32_t)ok : kNone;
+    uint32_t o;
+    float px, py, pz, pin, ptm = 0.f;
+    if (col == colA) {
+      o = oA;
+      px = pxA;
+      py = pyA;
+      pz = pzA;
+      pin = inA;
+      ptm = tmA;
+    } else {
+      const unsigned long long ok = owner[c];
+      o = (uint32_t)(ok >> 32) == hi ? (uint32_t)ok : kNone;
+      if (o != kNone) {
+        px = in.x[o];
+        py = in.y[o];
+        pz = in.z[o];
+        pin = in.in[o];
+        if (desk) ptm = in.time[o];
+      }
+    }
     if (o == kNone) {
       range_mat[c] = FLT_MAX;
       continue;
     }
-    const float px = in.x[o], py = in.y[o], pz = in.z[o];
     float ox = px, oy = py, oz = pz;
     if (desk) {
       float rx, ry, rz;
-      find_rotation(d, d.t0 + (double)in.time[o], rx, ry, rz);
+      find_rotation(d, d.t0 + (double)ptm, rx, ry, rz);
       const Aff bt = compose(startInv, get_rot_sc(rx, ry, rz));
       ox = bt.m[0][0] * px + bt.m[0][1] * py + bt.m[0][2] * pz + bt.m[0][3];
       oy = bt.m[1][0] * px + bt.m[1][1] * py + bt.m[1][2] * pz + bt.m[1][3];
       oz = bt.m[2][0] * px + bt.m[2][1] * py + bt.m[2][2] * pz + bt.m[2][3];
     }
     range_mat[c] = point_range(px, py, pz);
-    full[c] = make_float4(ox, oy, oz, in.in[o]);
+    full[c] = make_float4(ox, oy, oz, pin);
     ++cnt;
   }
   int excl;
@@ -1454,6 +1505,7 @@ struct slio_lio {
   int n_imu = 0;
   double t0 = 0.0;
   int deskew = 0;
+  int imu_sorted = 0;  // the deskew table's times are non-decreasing
   // projection
   unsigned long long* owner = nullptr;  // cells + 1: (~generation << 32) | point index
   uint32_t gen = 0;                      // scans run (owner generation)
@@ -1680,6 +1732,9 @@ int slio_lio_set_deskew(slio_lio_handle h, const double* imu_time, const double*
   h->deskew = enabled ? 1 : 0;
   h->n_imu = enabled ? n_imu : 0;
   h->t0 = time_scan_cur;
+  h->imu_sorted = 1;
+  for (int k = 1; enabled && k < n_imu; ++k)
+    if (!(imu_time[k - 1] <= imu_time[k])) h->imu_sorted = 0;
   if (enabled) {
     LIO_HIP(hipMemcpyAsync(h->it, imu_time, 8 * n_imu, hipMemcpyHostToDevice, h->stream));
     LIO_HIP(hipMemcpyAsync(h->rx, rot_x, 8 * n_imu, hipMemcpyHostToDevice, h->stream));
@@ -1728,7 +1783,7 @@ int slio_lio_run_async(slio_lio_handle h) {
   const int nclaim = (int)((h->n + 255) / 256);
   if (h->n > 0)
     k_lio_claim<<<nclaim, 256, 0, h->stream>>>(in, g, h->owner, hi, h->block_first);
-  const Deskew d{h->it, h->rx, h->ry, h->rz, h->n_imu - 1, h->t0, h->deskew};
+  const Deskew d{h->it, h->rx, h->ry, h->rz, h->n_imu - 1, h->t0, h->deskew, h->imu_sorted};
   k_lio_fill<<<dim3(R, kFillSplit), kFillThreads, 0, h->stream>>>(
       in, g, h->owner, hi, h->block_first, nclaim, d, h->range_mat, h->full, h->row_count);
   const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->prange, h->xyzi, h->n_ext};
