@@ -2866,9 +2866,10 @@ __global__ __launch_bounds__(kLegoRowThreads) void k_lego_extract(
 
 __global__ __launch_bounds__(256) void k_lego_label(LGeo g, const int32_t* parent, const int32_t* csize,
                                                     const unsigned long long* rows,
-                                                    const int32_t* rootlab, int32_t* label) {
+                                                    const int32_t* rootlab, int32_t* label, int32_t* clear) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= g.cells) return;
+  clear[c] = -1;  // the other owner table, for the next sweep
   const int32_t p = parent[c];
   if (p < 0) {
     label[c] = -1;
@@ -2885,6 +2886,7 @@ struct LegoImuDev {
   double t0;
   float ang_last[3];
   int on;
+  int seg;  // entries on the ring from last_it to last; > 0: their times are non-decreasing
 };
 
 struct LegoImuOutDev {
@@ -2939,9 +2941,28 @@ __device__ ImuCur imu_at(const LegoImuDev& m, float pointTime) {
   ImuCur c;
   const double tq = m.t0 + pointTime;
   int f = m.last_it;
-  while (f != m.last) {
-    if (tq < m.time[f]) break;
-    f = f + 1 == m.Q ? 0 : f + 1;  // (f + 1) % Q without the division
+  if (m.seg > 0) {
+    // the first of the ring entries last_it, ... before last whose time
+    // exceeds tq, else last: over non-decreasing times the reference's walk
+    // ends where this binary search does (a NaN tq: at last in both)
+    int lo = 0, n = m.seg - 1;
+    while (n > 0) {
+      const int h = n >> 1;
+      const int q = m.last_it + lo + h;
+      if (!(tq < m.time[q >= m.Q ? q - m.Q : q])) {
+        lo += h + 1;
+        n -= h + 1;
+      } else {
+        n = h;
+      }
+    }
+    f = m.last_it + lo;
+    if (f >= m.Q) f -= m.Q;
+  } else {
+    while (f != m.last) {
+      if (tq < m.time[f]) break;
+      f = f + 1 == m.Q ? 0 : f + 1;  // (f + 1) % Q without the division
+    }
   }
   c.f = f;
   c.b = f == 0 ? m.Q - 1 : f - 1;
@@ -3197,7 +3218,10 @@ struct slio_lego {
   LegoSeamRec* seam = nullptr;  // k_lego_cc_band's seam records
   uint32_t* cc_arrive = nullptr;
   // image / segmentation
-  int32_t* owner = nullptr;
+  int32_t* owner = nullptr;      // this sweep's cell owners (0xFFFFFFFF: none)
+  int32_t* owner_alt = nullptr;  // the other table: the last sweep's, cleared by this sweep's
+                                 // k_lego_label for the next one (no memset per sweep)
+  bool swept = false;
   float* range_mat = nullptr;
   float4* full = nullptr;
   int8_t* ground = nullptr;
@@ -3255,7 +3279,7 @@ void lego_free(slio_lego* h) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
   }
-  void* dev[] = {h->x, h->y, h->z, h->itime, h->iarr, h->owner, h->range_mat, h->full, h->ground,
+  void* dev[] = {h->x, h->y, h->z, h->itime, h->iarr, h->owner, h->owner_alt, h->range_mat, h->full, h->ground,
                  h->parent, h->edges, h->csize, h->rows, h->cnt, h->rootlab, h->label, h->start_ring,
                  h->end_ring, h->col_ind, h->nseg, h->gflag, h->srange, h->sxyzi, h->outlier,
                  h->slot, h->desk, h->io, h->curvature, h->picked0, h->flabel, h->corner_stage,
@@ -3342,6 +3366,10 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   A(h->y, 4 * N);
   A(h->z, 4 * N);
   A(h->owner, 4 * C);
+  A(h->owner_alt, 4 * C);
+  if (!e) e = hipMemsetAsync(h->owner, 0xff, 4 * C, h->own);
+  if (!e) e = hipMemsetAsync(h->owner_alt, 0xff, 4 * C, h->own);
+  if (!e) e = hipStreamSynchronize(h->own);
   A(h->range_mat, 4 * C);
   A(h->full, 16 * C);
   A(h->ground, C);
@@ -3500,7 +3528,18 @@ int slio_lego_set_imu(slio_lego_handle h, const slio_lego_imu* m) {
   h->imu = LegoImuDev{h->itime, a, a + Q, a + 2 * Q, a + 3 * Q, a + 4 * Q, a + 5 * Q,
                       a + 9 * Q, a + 10 * Q, a + 11 * Q, m->pointer_last,
                       m->pointer_last_iteration, Q, m->time_scan_cur,
-                      {m->ang_last[0], m->ang_last[1], m->ang_last[2]}, 1};
+                      {m->ang_last[0], m->ang_last[1], m->ang_last[2]}, 1, 0};
+  {
+    // the entries imu_at walks (last_it .. last on the ring): a binary search
+    // when their times do not decrease
+    const int L = (m->pointer_last - m->pointer_last_iteration + Q) % Q + 1;
+    bool mono = true;
+    for (int k = 1; k < L && mono; ++k) {
+      const int a0 = (m->pointer_last_iteration + k - 1) % Q, a1 = (m->pointer_last_iteration + k) % Q;
+      mono = m->time[a0] <= m->time[a1];
+    }
+    h->imu.seg = mono ? L : 0;
+  }
   h->imu_last_host = m->pointer_last;
   return SLIO_OK;
 }
@@ -3549,7 +3588,9 @@ int slio_lego_run_async(slio_lego_handle h) {
   // atomics (SLIO_LEGO_CC_LDS1 / SLIO_LEGO_CC_GLOBAL; all give the same labels)
   const bool cc_band = h->seam && !h->cc_global && !h->cc_lds1;
   const bool cc_lds = !cc_band && g.cells <= kLegoCcCells && !h->cc_global;
-  LIO_HIP(hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream));
+  // this sweep's owner table: the one the last sweep cleared
+  if (h->swept) std::swap(h->owner, h->owner_alt);
+  h->swept = true;
   if (!cc_lds && !cc_band) {
     LIO_HIP(hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream));
     LIO_HIP(hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream));
@@ -3576,7 +3617,7 @@ int slio_lego_run_async(slio_lego_handle h) {
                    h->outlier, h->nseg};
   k_lego_extract<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
                                                        h->cnt, h->range_mat, h->full, h->rootlab, sg);
-  k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label);
+  k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label, h->owner_alt);
   // adjustDistortion
   const int nslot = (int)cb;
   k_lego_half<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->orient[0], h->slot, h->io,
