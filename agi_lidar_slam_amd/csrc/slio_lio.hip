@@ -1459,30 +1459,40 @@ inline void launch_features(hipStream_t s, int R, const CloudInfo& ci, float* cu
 #undef SLIO_RING
 }
 
-__global__ __launch_bounds__(256) void k_lio_concat(int n_scan, const int32_t* start_ring,
-                                                    FeatOut f, float4* corner, float4* surface,
-                                                    int64_t* counts /* n_corner, n_surface */) {
+// sum of cnt[0 .. r) by one wavefront (lanes take rings lane, lane + 64, ...),
+// every lane of the wavefront gets it
+__device__ __forceinline__ int wave_prefix_count(const int32_t* cnt, int r) {
+  const int lane = threadIdx.x & 63;
+  int v = 0;
+  for (int q = lane; q < r; q += 64) v += cnt[q];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+constexpr int kConcatThreads = 1024;
+__global__ __launch_bounds__(kConcatThreads) void k_lio_concat(int n_scan, const int32_t* start_ring,
+                                                               FeatOut f, float4* corner, float4* surface,
+                                                               int64_t* counts /* n_corner, n_surface */) {
   __shared__ int s_co, s_so;
-  const int r = blockIdx.x;
-  if (threadIdx.x == 0) {
-    int co = 0, so = 0;
-    for (int q = 0; q < r; ++q) {
-      co += f.corner_count[q];
-      so += f.surf_count[q];
-    }
-    s_co = co;
-    s_so = so;
-    if (r == n_scan - 1) {
-      counts[0] = co + f.corner_count[r];
-      counts[1] = so + f.surf_count[r];
+  const int r = blockIdx.x, w = threadIdx.x >> 6;
+  // ring offsets: wavefront 0 the corners', wavefront 1 the surfaces'
+  if (w < 2) {
+    const int o = wave_prefix_count(w == 0 ? f.corner_count : f.surf_count, r);
+    if ((threadIdx.x & 63) == 0) {
+      if (w == 0)
+        s_co = o;
+      else
+        s_so = o;
+      if (r == n_scan - 1) counts[w] = o + (w == 0 ? f.corner_count[r] : f.surf_count[r]);
     }
   }
   __syncthreads();
   const int nc = f.corner_count[r], ns = f.surf_count[r];
-  for (int q = threadIdx.x; q < nc; q += 256)
+  for (int q = threadIdx.x; q < nc; q += kConcatThreads)
     corner[s_co + q] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
   const float4* src = f.surf_stage + (start_ring[r] - 4);
-  for (int q = threadIdx.x; q < ns; q += 256) surface[s_so + q] = src[q];
+  for (int q = threadIdx.x; q < ns; q += kConcatThreads) surface[s_so + q] = src[q];
 }
 
 }  // namespace lio
@@ -1803,7 +1813,7 @@ int slio_lio_run_async(slio_lio_handle h) {
     h->pending.push_back(ev);
   }
   launch_features<kModeLio>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw, ev);
-  k_lio_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
+  k_lio_concat<<<R, kConcatThreads, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
   LIO_HIP(hipGetLastError());
   h->ran = true;
   return SLIO_OK;
@@ -3144,42 +3154,41 @@ __global__ __launch_bounds__(256) void k_lego_deskew(const float4* seg, const in
   out[i] = make_float4(px, py, pz, inten);
 }
 
-__global__ __launch_bounds__(256) void k_lego_concat(int n_scan, const int32_t* start_ring, FeatOut f,
-                                                     float4* sharp, float4* less_sharp, float4* flat,
-                                                     float4* less_flat, int64_t* counts) {
+__global__ __launch_bounds__(kConcatThreads) void k_lego_concat(int n_scan, const int32_t* start_ring,
+                                                                FeatOut f, float4* sharp, float4* less_sharp,
+                                                                float4* flat, float4* less_flat,
+                                                                int64_t* counts) {
   __shared__ int s_o[4];
-  const int r = blockIdx.x;
-  if (threadIdx.x == 0) {
-    int o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-    for (int q = 0; q < r; ++q) {
-      o0 += f.sharp_count[q];
-      o1 += f.corner_count[q];
-      o2 += f.flat_count[q];
-      o3 += f.surf_count[q];
+  const int r = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // ring offsets: wavefront k of the first four sums the earlier rings' counts
+  // of output k (sharp, less sharp, flat, less flat)
+  if (w < 4) {
+    const int32_t* cnt = w == 0 ? f.sharp_count : w == 1 ? f.corner_count : w == 2 ? f.flat_count : f.surf_count;
+    const int o = wave_prefix_count(cnt, r);
+    if (lane == 0) {
+      s_o[w] = o;
+      if (r == n_scan - 1) counts[w] = o + cnt[r];
     }
-    s_o[0] = o0;
-    s_o[1] = o1;
-    s_o[2] = o2;
-    s_o[3] = o3;
-    if (r == n_scan - 1) {
-      counts[0] = o0 + f.sharp_count[r];
-      counts[1] = o1 + f.corner_count[r];
-      counts[2] = o2 + f.flat_count[r];
-      counts[3] = o3 + f.surf_count[r];
-    }
-    // cornerPointsSharp: the label-2 picks in pick order (<= 12 per ring)
-    int k = 0;
-    for (int q = 0; q < f.corner_count[r]; ++q)
-      if (f.corner_sharp[(int64_t)r * kCornerPerRing + q])
-        sharp[o0 + k++] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < f.corner_count[r]; q += 256)
+  const int nc = f.corner_count[r];
+  if (w == 0) {
+    // cornerPointsSharp: the label-2 picks in pick order (ballot compaction)
+    int k = s_o[0];
+    for (int q0 = 0; q0 < nc; q0 += 64) {
+      const int q = q0 + lane;
+      const bool sh = q < nc && f.corner_sharp[(int64_t)r * kCornerPerRing + q];
+      const uint64_t b = __ballot(sh);
+      if (sh) sharp[k + __popcll(b & ((1ull << lane) - 1))] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
+      k += __popcll(b);
+    }
+  }
+  for (int q = threadIdx.x; q < nc; q += kConcatThreads)
     less_sharp[s_o[1] + q] = f.corner_stage[(int64_t)r * kCornerPerRing + q];
-  for (int q = threadIdx.x; q < f.flat_count[r]; q += 256)
+  for (int q = threadIdx.x; q < f.flat_count[r]; q += kConcatThreads)
     flat[s_o[2] + q] = f.flat_stage[(int64_t)r * kFlatPerRing + q];
   const float4* src = f.surf_stage + (start_ring[r] - 4);
-  for (int q = threadIdx.x; q < f.surf_count[r]; q += 256) less_flat[s_o[3] + q] = src[q];
+  for (int q = threadIdx.x; q < f.surf_count[r]; q += kConcatThreads) less_flat[s_o[3] + q] = src[q];
 }
 
 }  // namespace lego
@@ -3641,7 +3650,7 @@ int slio_lego_run_async(slio_lego_handle h) {
     h->pending.push_back(ev);
   }
   launch_features<kModeLego>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw, ev);
-  k_lego_concat<<<R, 256, 0, h->stream>>>(R, h->start_ring, fo, h->c_sharp, h->c_less_sharp,
+  k_lego_concat<<<R, kConcatThreads, 0, h->stream>>>(R, h->start_ring, fo, h->c_sharp, h->c_less_sharp,
                                           h->c_flat, h->c_less_flat, h->counts);
   LIO_HIP(hipGetLastError());
   h->ran = true;
