@@ -291,6 +291,98 @@ __device__ __forceinline__ void sort_keys_lds(K* key) {
   __syncthreads();
 }
 
+// Stable LSD radix sort (8-bit digits) of n <= NT * E (key, value) pairs in
+// LDS by the low `bits` bits of the key, ascending; pairs with equal keys
+// keep their input order.  Wavefront w ranks the contiguous segment
+// [w * seg, (w + 1) * seg) of the input in rounds of 64 (a lane's peers with
+// the same digit from 8 ballots, their running count per (wave, digit) in
+// LDS), one block scan over the (digit, wave) counts gives every bucket's
+// start, and each pair is scattered to its rank.  k0 / v0 hold the input and,
+// on return, the sorted pairs (k1 / v1: the other buffer of each pass);
+// cnt: 256 * NT / 64 ints; scratch: NT / 64 + 1 ints.  Every thread of the
+// block calls it (block barriers inside).
+template <int NT, int E>
+__device__ __forceinline__ void radix_sort_pairs_lds(uint32_t* k0, int32_t* v0, uint32_t* k1, int32_t* v1,
+                                                     int n, int bits, int* cnt, int* scratch) {
+  constexpr int W = NT / 64;
+  static_assert(256 * W % NT == 0, "radix counters");
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int seg = (n + W - 1) / W;
+  const int s0 = min(w * seg, n), s1 = min(s0 + seg, n);
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t* ks = k0;
+  int32_t* vs = v0;
+  uint32_t* kd = k1;
+  int32_t* vd = v1;
+  for (int sh = 0; sh < bits; sh += 8) {
+    for (int q = t; q < 256 * W; q += NT) cnt[q] = 0;
+    __syncthreads();
+    uint32_t key[E];
+    int32_t val[E], rank[E], dig[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const int i = s0 + 64 * k + lane;
+      const bool ok = i < s1;
+      key[k] = ok ? ks[i] : 0u;
+      val[k] = ok ? vs[i] : 0;
+      const int d = (int)((key[k] >> sh) & 255u);
+      dig[k] = d;
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t m = __ballot(ok && ((d >> b) & 1));
+        peers &= ((d >> b) & 1) ? m : ~m;
+      }
+      // (a lane's own digit: cnt[d * W + w] before this round's peers)
+      const int before = ok ? cnt[d * W + w] : 0;
+      rank[k] = before + __popcll(peers & lt);
+      __builtin_amdgcn_wave_barrier();
+      if (ok && (peers & lt) == 0) cnt[d * W + w] = before + __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // bucket starts: exclusive scan over (digit, wave) in digit-major order
+    constexpr int P = 256 * W / NT;
+    int loc[P], sum = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      loc[j] = cnt[t * P + j];
+      sum += loc[j];
+    }
+    int excl;
+    block_exclusive_scan<NT>(sum, scratch, excl);
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      cnt[t * P + j] = excl;
+      excl += loc[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const int i = s0 + 64 * k + lane;
+      if (i < s1) {
+        const int dst = cnt[dig[k] * W + w] + rank[k];
+        kd[dst] = key[k];
+        vd[dst] = val[k];
+      }
+    }
+    __syncthreads();
+    uint32_t* tk = ks;
+    ks = kd;
+    kd = tk;
+    int32_t* tv = vs;
+    vs = vd;
+    vd = tv;
+  }
+  if (ks != k0) {  // an odd number of passes: the result back into k0 / v0
+    for (int i = t; i < n; i += NT) {
+      k0[i] = ks[i];
+      v0[i] = vs[i];
+    }
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ int pow2ceil(int v) {
   int p = 1;
   while (p < v) p <<= 1;
@@ -639,6 +731,12 @@ __device__ unsigned long long g_fstamp[256 * 36][6];
           __builtin_amdgcn_s_memrealtime();                                        \
   } while (0)
 __device__ unsigned long long g_rstamp[256][8];
+__device__ unsigned long long g_vstamp[256][4];  // ring_vsort: start, keys built, sorted, end
+#define VSTAMP(k)                                                                  \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.y < 256)                                      \
+      g_vstamp[blockIdx.y][k] = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
 #define RGSTAMP(k)                                                                 \
   do {                                                                             \
     if (threadIdx.x == 0 && blockIdx.x < 256)                                      \
@@ -650,6 +748,9 @@ __device__ unsigned long long g_rstamp[256][8];
   } while (0)
 #define RGSTAMP(k) \
   do {             \
+  } while (0)
+#define VSTAMP(k) \
+  do {            \
   } while (0)
 #endif
 
@@ -669,14 +770,16 @@ __device__ unsigned long long g_rstamp[256][8];
 // -1 and k_fe_ring sorts the surface list itself.
 __device__ __forceinline__ void ring_vsort(const CloudInfo& ci, const FeatCfg& cfg, const FeatWork& fw,
                                            unsigned char* smem) {
-  constexpr int kW = kPickThreads / 64, kE = kVsortN / (64 * kW), kQBits = __builtin_ctz(kVsortN);
+  constexpr int kW = kPickThreads / 64;
   constexpr int kHeld = kVsortN / kPickThreads;  // points per thread, kept in registers
-  static_assert(kVsortN % kPickThreads == 0 && (kW & (kW - 1)) == 0, "ring_vsort layout");
+  static_assert(kVsortN % kPickThreads == 0, "ring_vsort layout");
   const int r = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  VSTAMP(0);
   const int start = ci.start_ring[r], end = ci.end_ring[r];
   __shared__ int s_lo[6], s_cnt[7];
   __shared__ float wmn[kPickThreads / 64][3], wmx[kPickThreads / 64][3];
-  __shared__ int s_ok, s_minb[3], s_mul[3], s_narrow;
+  __shared__ int s_ok, s_minb[3], s_mul[3], s_bits;
+  __shared__ int rscratch[kW + 1];
   if (t == 0) {
     int c = 0;
     for (int j = 0; j < 6; ++j) {
@@ -760,7 +863,7 @@ __device__ __forceinline__ void ring_vsort(const CloudInfo& ci, const FeatCfg& c
     s_mul[1] = (int)divb[0];
     s_mul[2] = (int)(divb[0] * divb[1]);
     const uint32_t top = s_ok ? (uint32_t)(cells - 1) : 0u;
-    s_narrow = (top ? 32 - __clz((int)top) : 1) + kQBits <= 32;
+    s_bits = top ? 32 - __clz((int)top) : 1;
   }
   __syncthreads();
   if (!s_ok) {
@@ -774,23 +877,25 @@ __device__ __forceinline__ void ring_vsort(const CloudInfo& ci, const FeatCfg& c
     return (uint32_t)(i0 * s_mul[0] + i1 * s_mul[1] + i2 * s_mul[2]);
   };
   uint64_t* out = fw.vkey + (int64_t)r * kVsortN;
-  if (s_narrow) {
-    uint32_t* k32 = reinterpret_cast<uint32_t*>(smem);
+  // (voxel, position) pairs in list order, then the stable sort by voxel
+  uint32_t* vk0 = reinterpret_cast<uint32_t*>(smem);
+  int32_t* vv0 = reinterpret_cast<int32_t*>(vk0 + kVsortN);
+  uint32_t* vk1 = reinterpret_cast<uint32_t*>(vv0 + kVsortN);
+  int32_t* vv1 = reinterpret_cast<int32_t*>(vk1 + kVsortN);
+  int* vcnt = reinterpret_cast<int*>(vv1 + kVsortN);
 #pragma unroll
-    for (int k = 0; k < kHeld; ++k)
-      k32[t + k * kPickThreads] = hq[k] >= 0 ? (voxel_of(held[k]) << kQBits) | (uint32_t)(hq[k] - start) : ~0u;
-    sort_keys_lds<kW, kE, uint32_t>(k32);
-    for (int i = t; i < m; i += kPickThreads)
-      out[i] = ((uint64_t)(k32[i] >> kQBits) << 32) | (uint32_t)(start + (int)(k32[i] & (kVsortN - 1)));
-  } else {
-    uint64_t* k64 = reinterpret_cast<uint64_t*>(smem);
-#pragma unroll
-    for (int k = 0; k < kHeld; ++k)
-      k64[t + k * kPickThreads] = hq[k] >= 0 ? ((uint64_t)voxel_of(held[k]) << 32) | (uint32_t)hq[k] : ~0ull;
-    sort_keys_lds<kW, kE>(k64);
-    for (int i = t; i < m; i += kPickThreads) out[i] = k64[i];
-  }
+  for (int k = 0; k < kHeld; ++k)
+    if (hq[k] >= 0) {
+      vk0[t + k * kPickThreads] = voxel_of(held[k]);
+      vv0[t + k * kPickThreads] = hq[k];
+    }
+  __syncthreads();
+  VSTAMP(1);
+  radix_sort_pairs_lds<kPickThreads, kHeld>(vk0, vv0, vk1, vv1, m, s_bits, vcnt, rscratch);
+  VSTAMP(2);
+  for (int i = t; i < m; i += kPickThreads) out[i] = ((uint64_t)vk0[i] << 32) | (uint32_t)vv0[i];
   if (t == 0) fw.vinfo[r] = m;
+  VSTAMP(3);
 }
 
 // ---- k_fe_pick: grid (6, R), 6 wavefronts: sector j of ring r.  The block
@@ -814,7 +919,8 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     const uint8_t* __restrict__ ground, FeatCfg cfg, FeatWork fw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   static_assert(SORTN >= 64 && SORTN <= 2048 && (SORTN & (SORTN - 1)) == 0, "sort size");
-  constexpr int kSortW = SORTN >= 256 ? 4 : SORTN / 64, kSortE = SORTN / (64 * kSortW);
+  constexpr int kRadixE = SORTN >= kPickThreads ? SORTN / kPickThreads : 1;
+  __shared__ int rscratch[kPickThreads / 64 + 1];
   if (blockIdx.x == 6) {  // the ring's VoxelGrid order (ring_vsort)
     ring_vsort(ci, cfg, fw, smem);
     return;
@@ -837,9 +943,14 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   // with fewer than 11 points has no live sector, and its shares may reach
   // back into the previous ring)
   const int lb = min(pb, wlo), hi = max(pe, whi);
-  uint64_t* skey = reinterpret_cast<uint64_t*>(smem);  // SORTN (= cap) sort keys
-  int32_t* spos = reinterpret_cast<int32_t*>(skey + SORTN);  // the sector in sort order
-  float* curv = reinterpret_cast<float*>(spos + cap);
+  // the sector's sort (SORTN = cap): keys / positions and the radix sort's
+  // second buffers and counters; spos: the sector in sort order after it
+  uint32_t* rk0 = reinterpret_cast<uint32_t*>(smem);
+  int32_t* spos = reinterpret_cast<int32_t*>(rk0 + SORTN);
+  uint32_t* rk1 = reinterpret_cast<uint32_t*>(spos + SORTN);
+  int32_t* rv1 = reinterpret_cast<int32_t*>(rk1 + SORTN);
+  int* rcnt = reinterpret_cast<int*>(rv1 + SORTN);  // 256 x waves
+  float* curv = reinterpret_cast<float*>(rcnt + 256 * (kPickThreads / 64));
   int32_t* col = reinterpret_cast<int32_t*>(curv + pcap) + kHalo;  // col[q - pb], q >= pb - kHalo
   float* rng = reinterpret_cast<float*>(col - kHalo + pcap) + kHalo;  // range, as col
   uint8_t* pk0 = reinterpret_cast<uint8_t*>(rng - kHalo + pcap);  // cloudNeighborPicked on entry
@@ -882,19 +993,16 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     return;
   }
   FSTAMP(0);
-  // the sector's sort: (value bits, position) keys, bitonic in registers and
-  // LDS (sort_keys_lds) -- the stable sort by value
+  // the sector's sort: the stable sort of (value bits, position) by value
+  // (values >= +0 order as their bits; equal values keep position order)
   const int len = ep - sp;
-  for (int idx = t; idx < SORTN; idx += kPickThreads) {
+  for (int idx = t; idx < len; idx += kPickThreads) {
     const int k = sp + idx;
-    skey[idx] = idx < len ? ((uint64_t)__float_as_uint((k >= 5 && k < n - 5) ? curv[k - pb] : 0.0f) << 32) |
-                                (uint32_t)k
-                          : ~0ull;
+    rk0[idx] = __float_as_uint((k >= 5 && k < n - 5) ? curv[k - pb] : 0.0f);
+    spos[idx] = k;
   }
   __syncthreads();
-  sort_keys_lds<kSortW, kSortE>(skey);
-  for (int idx = t; idx < len; idx += kPickThreads) spos[idx] = (int32_t)(uint32_t)skey[idx];
-  __syncthreads();
+  radix_sort_pairs_lds<kPickThreads, kRadixE>(rk0, spos, rk1, rv1, len, 32, rcnt, rscratch);
   FSTAMP(1);
   // suppression reach (:220-237, 247-262): points ind + l, l = 1..5 (and
   // -1..-5), are flagged while consecutive columns differ by <= 10, so a
@@ -1348,9 +1456,11 @@ struct FeatSmem {
 };
 inline FeatSmem feat_smem_sizes(const FeatCfg& fc) {
   const size_t pcap = (size_t)fc.sort_cap + kPickPad;
-  // (k_fe_pick's 7th workgroup per ring sorts kVsortN keys in the same LDS)
-  return FeatSmem{std::max(12 * (size_t)fc.sort_cap + (4 + 4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
-                           sizeof(uint64_t) * (size_t)kVsortN),
+  // (k_fe_pick's 7th workgroup per ring sorts kVsortN pairs in the same LDS;
+  // both sorts: two key / value buffers and 256 counters per wavefront)
+  const size_t rcnt = sizeof(int) * 256 * (kPickThreads / 64);
+  return FeatSmem{std::max(16 * (size_t)fc.sort_cap + rcnt + (4 + 4 + 4 + 1 + 1 + 1 + 1 + 6 * 2) * pcap,
+                           16 * (size_t)kVsortN + rcnt),
                   24 * (size_t)fc.vox_cap + 21 * (size_t)fc.ring_cap};
 }
 // the sorts' sizes (powers of two; 0: capacity not supported)
@@ -3197,6 +3307,9 @@ __global__ __launch_bounds__(kConcatThreads) void k_lego_concat(int n_scan, cons
 using namespace slio::lego;
 
 #ifdef SLIO_FE_STAMP
+extern "C" int slio_dbg_vsort_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(slio::lio::g_vstamp), sizeof(slio::lio::g_vstamp)) == hipSuccess ? 0 : -1;
+}
 extern "C" int slio_dbg_band_stamps(unsigned long long* band, unsigned long long* merge) {
   return hipMemcpyFromSymbol(band, HIP_SYMBOL(g_bstamp), sizeof(g_bstamp)) == hipSuccess &&
                  hipMemcpyFromSymbol(merge, HIP_SYMBOL(g_mstamp), sizeof(g_mstamp)) == hipSuccess

@@ -48,4 +48,14 @@ for k, nm in enumerate(phases):
     print(f"ring {nm:15s} mean {rp[:, k].mean():6.2f} max {rp[:, k].max():6.2f} us")
 print(f"ring kernel: start spread {(rv[:, 0].max() - rv[:, 0].min()) / 100:.2f} us, "
       f"total mean {((rv[:, 7] - rv[:, 0]) / 100).mean():.2f} us")
+lib.slio_dbg_vsort_stamps.argtypes = [C.POINTER(C.c_ulonglong)]
+vb = (C.c_ulonglong * (256 * 4))()
+assert lib.slio_dbg_vsort_stamps(vb) == 0
+vv = np.array(vb[:], dtype=np.int64).reshape(256, 4)[:64]
+ok = vv[:, 3] > 0
+vp = np.diff(vv[ok], axis=1) / 100.0
+narrow = "?"
+print(f"vsort: keys {vp[:, 0].mean():.2f} sort {vp[:, 1].mean():.2f} out {vp[:, 2].mean():.2f} us; "
+      f"total mean {((vv[ok, 3] - vv[ok, 0]) / 100).mean():.2f} max {((vv[ok, 3] - vv[ok, 0]) / 100).max():.2f}; "
+      f"end (vs the sector blocks' first start) max {((vv[ok, 3] - t0) / 100).max():.2f} us")
 fe.close()
