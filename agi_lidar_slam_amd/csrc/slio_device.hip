@@ -2668,6 +2668,8 @@ struct SearchLds {
   alignas(16) int32_t nb_idx[SLIO_CHUNK][5];  // Nearest_Points ids, for one coalesced store
   float nb_d5[SLIO_CHUNK];
   float4 qw[SLIO_CHUNK];            // the query; .w: its certificate bound G (KC, -2: none written)
+  float4 qb[SLIO_CHUNK];            // the body point (the fit phase's copy, loaded by the kNN lanes)
+  float4 qpl[SLIO_CHUNK];           // KC: the last pass's plane of the point (loaded with its certificate)
   uint32_t kc_n[2];                 // KC: certified queries, searched queries
   uint32_t kx6[SLIO_CHUNK];         // KC: the 6th of the point's certified set
   uint8_t ksame[SLIO_CHUNK];        // KC: certified in the last pass's order (plane reusable)
@@ -2779,15 +2781,20 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
     // (the last pass's 5 in order, then the 6th), loaded with the scan point:
     // no dependent round trip
     float4 ka = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+    float4 kpl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     uint32_t kp[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
     if (KC && cache_ok && live) {
       ka = out.kq[i];
 #pragma unroll
       for (int j = 0; j < 5; ++j) kp[j] = out.nbr_pos[5 * i + j];
       kp[5] = out.k6[i];
+      kpl = out.plane[i];  // (the fit reuses it when the certified 5 keep their order)
     }
+    float bx = 0.0f, by = 0.0f, bz = 0.0f;
     if (live) {
-      const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
+      bx = scan.bx[i];
+      by = scan.by[i];
+      bz = scan.bz[i];
       body_to_world(pose, bx, by, bz, qx, qy, qz);
     }
     Top5 t;
@@ -3016,6 +3023,8 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
       nb_d5[slot] = (t.k[4] != kInfKey) ? d5 : __int_as_float(0x7f800000);
       // (KC: a certified query keeps the certificate it was certified by)
       qw[slot] = make_float4(qx, qy, qz, KC ? (reused ? -2.0f : kG) : 0.0f);
+      lds.s.qb[slot] = make_float4(bx, by, bz, 0.0f);
+      if (KC) lds.s.qpl[slot] = kpl;
       if (KC) {
         lds.s.kx6[slot] = kx6;
         lds.s.ksame[slot] = same5 ? 1 : 0;
@@ -3168,14 +3177,15 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
       float pd2 = __int_as_float(0x7fc00000);
       const float4 q = qw[slot];
       FSTAMP(0, false);
-      const float bx = scan.bx[i], by = scan.by[i], bz = scan.bz[i];
+      const float4 qb = lds.s.qb[slot];
+      const float bx = qb.x, by = qb.y, bz = qb.z;
       // KC: certified with the last pass's 5 in the same order -- the same
       // esti_plane input, so its plane (when it had one) is reused
       bool rp = false;
       float4 cpl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       if constexpr (KC) {
         if (lds.s.ksame[slot]) {
-          cpl = out.plane[i];
+          cpl = lds.s.qpl[slot];
           rp = isfinite(cpl.x) && isfinite(cpl.y) && isfinite(cpl.z) && isfinite(cpl.w);
         }
       }

@@ -753,12 +753,17 @@ def main():
     P_ptr, xs_ref, st_ref = L.dptr(P), C.byref(xs), C.byref(stats)
     fn = lib.slio_ikf_update if args.host_loop else lib.slio_ikf_update_device
     mode = L.SLIO_MODE_REFERENCE if args.mode == "reference" else L.SLIO_MODE_FIXED
+    P0c = np.ascontiguousarray(P0)
+    xs_a, xs0_a, xs_n = C.addressof(xs), C.addressof(xs0), C.sizeof(xs)
+    P_a, P0_a, P_n = P.ctypes.data, P0c.ctypes.data, P.nbytes
+    R_c, it_c, ext_c, mode_c = C.c_double(0.001), C.c_int(args.iters), C.c_int(0), C.c_int(mode)
 
     def step():
-        # every step restarts from the same prior (same work per step)
-        C.memmove(C.addressof(xs), C.addressof(xs0), C.sizeof(xs))
-        P[...] = P0
-        rc = fn(h, xs_ref, P_ptr, 0.001, args.iters, 0, mode, reduce_cb, None, st_ref)
+        # every step restarts from the same prior (same work per step): x and
+        # P copied back by memmove, the call's scalars prebuilt
+        C.memmove(xs_a, xs0_a, xs_n)
+        C.memmove(P_a, P0_a, P_n)
+        rc = fn(h, xs_ref, P_ptr, R_c, it_c, ext_c, mode_c, reduce_cb, None, st_ref)
         if rc:
             L.check(rc, "ikf")
         return xs
