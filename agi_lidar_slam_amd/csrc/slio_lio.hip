@@ -383,6 +383,45 @@ __device__ __forceinline__ void radix_sort_pairs_lds(uint32_t* k0, int32_t* v0, 
   }
 }
 
+// The same stable order by counting: element i of key[0, n) goes to place
+// #{j : key[j] < key[i]} + #{j < i : key[j] == key[i]}, and pos[place] =
+// first + i.  Every lane walks the whole list as broadcast 16-byte LDS reads
+// (j below its wavefront's elements counts with <=, above with <), so the
+// cost is n compares per element and no barrier between them: for a few
+// hundred keys it beats the radix passes' scans.  key[n, round_up(n, 4)) must
+// hold 0xffffffff; pos may alias nothing read here.
+template <int NT, int E>
+__device__ __forceinline__ void rank_sort_lds(const uint32_t* key, int n, int32_t* pos, int first) {
+  const int t = threadIdx.x;
+  const int n4 = (n + 3) & ~3;
+  const uint4* k4 = reinterpret_cast<const uint4*>(key);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = t + e * NT, wb = (i & ~63);
+    if (wb >= n) break;  // wavefront-uniform
+    const uint32_t ki = i < n ? key[i] : 0xffffffffu;
+    int c = 0;
+    const int a = min(wb, n4), b = min(wb + 64, n4);
+#pragma unroll 8
+    for (int j = 0; j < a; j += 4) {  // 8 reads in flight: the loop is LDS-latency bound
+      const uint4 q = k4[j >> 2];
+      c += (q.x <= ki) + (q.y <= ki) + (q.z <= ki) + (q.w <= ki);
+    }
+    for (int j = a; j < b; j += 4) {
+      const uint4 q = k4[j >> 2];
+      c += (q.x < ki || (q.x == ki && j < i)) + (q.y < ki || (q.y == ki && j + 1 < i)) +
+           (q.z < ki || (q.z == ki && j + 2 < i)) + (q.w < ki || (q.w == ki && j + 3 < i));
+    }
+#pragma unroll 8
+    for (int j = b; j < n4; j += 4) {
+      const uint4 q = k4[j >> 2];
+      c += (q.x < ki) + (q.y < ki) + (q.z < ki) + (q.w < ki);
+    }
+    if (i < n) pos[c] = first + i;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ int pow2ceil(int v) {
   int p = 1;
   while (p < v) p <<= 1;
@@ -680,6 +719,7 @@ constexpr int kFeatThreads = 1024;
 // sector sort and reach phase only; all 8 sort the ring's VoxelGrid order in
 // the 7th workgroup of a ring, ring_vsort)
 constexpr int kPickThreads = 512;
+static_assert(kPickThreads > 6 * 64, "waves past the 6 variants store the smoothness outputs");
 // k_fe_pick's per-position LDS arrays: sort_cap + kPickPad entries (a sector,
 // its 5-point margins, the last sector's extra point, and the 6-point halos
 // of the staged range / columns, kHalo on each side)
@@ -978,12 +1018,18 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     pk0[q - lb] = pk;
   }
   __syncthreads();
-  for (int q = wlo + t; q <= whi; q += kPickThreads) {
-    curvature[q] = curv[q - lb];
-    picked0[q] = pk0[q - lb];
-    label[q] = 0;  // k_fe_ring writes the rings' [start, end]
-  }
+  // the block's smoothness outputs: stored here by a dead sector, else by
+  // waves 6-7 once they are done with the sort and the reach (a barrier
+  // waits for every store issued before it)
+  auto store_outputs = [&](int t0, int nt) {
+    for (int q = wlo + t0; q <= whi; q += nt) {
+      curvature[q] = curv[q - lb];
+      picked0[q] = pk0[q - lb];
+      label[q] = 0;  // k_fe_ring writes the rings' [start, end]
+    }
+  };
   if (sp >= ep) {  // `if (sp >= ep) continue;`
+    store_outputs(t, kPickThreads);
     if (lane == 0 && v < 6 && (j > 0 || v == 0)) {
       PickVar* pv = fw.var + (r * 6 + j) * 6 + v;
       pv->ncorner = 0;
@@ -996,13 +1042,22 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
   // the sector's sort: the stable sort of (value bits, position) by value
   // (values >= +0 order as their bits; equal values keep position order)
   const int len = ep - sp;
-  for (int idx = t; idx < len; idx += kPickThreads) {
-    const int k = sp + idx;
-    rk0[idx] = __float_as_uint((k >= 5 && k < n - 5) ? curv[k - pb] : 0.0f);
-    spos[idx] = k;
+  if constexpr (SORTN <= 2 * kPickThreads) {  // counting ranks (rank_sort_lds)
+    for (int idx = t; idx < ((len + 3) & ~3); idx += kPickThreads) {
+      const int k = sp + idx;
+      rk0[idx] = idx < len ? __float_as_uint((k >= 5 && k < n - 5) ? curv[k - pb] : 0.0f) : 0xffffffffu;
+    }
+    __syncthreads();
+    rank_sort_lds<kPickThreads, (SORTN + kPickThreads - 1) / kPickThreads>(rk0, len, spos, sp);
+  } else {
+    for (int idx = t; idx < len; idx += kPickThreads) {
+      const int k = sp + idx;
+      rk0[idx] = __float_as_uint((k >= 5 && k < n - 5) ? curv[k - pb] : 0.0f);
+      spos[idx] = k;
+    }
+    __syncthreads();
+    radix_sort_pairs_lds<kPickThreads, kRadixE>(rk0, spos, rk1, rv1, len, 32, rcnt, rscratch);
   }
-  __syncthreads();
-  radix_sort_pairs_lds<kPickThreads, kRadixE>(rk0, spos, rk1, rv1, len, 32, rcnt, rscratch);
   FSTAMP(1);
   // suppression reach (:220-237, 247-262): points ind + l, l = 1..5 (and
   // -1..-5), are flagged while consecutive columns differ by <= 10, so a
@@ -1023,7 +1078,11 @@ __global__ __launch_bounds__(kPickThreads) void k_fe_pick(
     reach[q - pb] = (uint8_t)(rl | (rr << 4));
   }
   __syncthreads();
-  if (v >= 6 || (j == 0 && v > 0)) return;  // 6 variants; nothing precedes the first sector
+  if (v >= 6) {
+    store_outputs(t - 6 * 64, kPickThreads - 6 * 64);
+    return;
+  }
+  if (j == 0 && v > 0) return;  // 6 variants; nothing precedes the first sector
   FSTAMP(2);
   const int slot = (r * 6 + j) * 6 + v;
   PickVar* pv = fw.var + slot;
