@@ -26,7 +26,8 @@ SLIO_KERNEL_SUPER = 2
 SLIO_PROFILE_KEEP = 16
 SLIO_LIO_PROFILE_KEEP = 16
 
-ERRORS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ECAPACITY", -5: "ESTATE"}
+ERRORS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ECAPACITY", -5: "ESTATE", -6: "ETIMEOUT"}
+SLIO_ETIMEOUT = -6
 
 
 class SlioParams(C.Structure):
@@ -230,6 +231,7 @@ SIGNATURES = {
     "slio_debug_update_path": (C.c_int, [_P]),
     "slio_debug_host_stamps": (C.c_int, [_P, C.c_int, _I64P]),
     "slio_debug_knn_cert": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    "slio_debug_wait_limit": (C.c_int, [_P, C.c_int64]),
     # include/slio_frontend.h (LIO-SAM front-end)
     "slio_lio_params_default": (C.c_int, [C.POINTER(SlioLioParams)]),
     "slio_lio_create": (C.c_int, [C.POINTER(_P), C.POINTER(SlioLioParams)]),

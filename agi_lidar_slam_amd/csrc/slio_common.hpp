@@ -74,7 +74,7 @@ struct IkfCtl {
   int32_t singular;
   int32_t published;  // mapped host block: set (release, system scope) after x, P and the flags
   int32_t seq;        // the update's sequence number (a fused group's passes and gates check it)
-  int32_t pad_;
+  int32_t timeout;    // mapped host block: set (system scope) by a device-side wait that gave up
   // PoseDev of x (rotation matrices formed) for the pass that follows, in slot
   // (passes completed) % kPoseSlots (device only): a slot is first read by a
   // pass after its writer's step, so a persistent update's scalar-cache loads
@@ -88,5 +88,11 @@ struct IkfCtl {
 // P_DD^-1 (D x D) and G = P[:, :D] P_DD^-1 (24 x D) of an update's prior P,
 // D = 6 or 12 (slio_ikf.cpp)
 bool info_constants(const double* P, int D, double P11i[144], double G[288]);
+
+// Live handles per HIP device (IKF, LIO-SAM and LeGO-LOAM handles; delta +1
+// at create, -1 at destroy; returns the count after the change).  The
+// persistent update assumes every workgroup of its launch is resident at
+// once, which only holds when no other handle's kernels share the device.
+int dev_users(int device, int delta);
 
 }  // namespace slio

@@ -2480,6 +2480,9 @@ struct FuseArgs {
   // apart) of the flag (gseq << 32) | done << 31 | passes its filter step
   // publishes after each pass; null otherwise
   uint64_t* goflag;
+  // device-side waits (k_update_persist): give up after this many 100 MHz
+  // ticks (0: 1 s), raising the mapped host block's timeout word
+  uint64_t wait_ticks;
 };
 constexpr int kGoFlagStride = 16;  // uint64 words between the replicas
 constexpr int kSegCnt = 16;
@@ -3387,10 +3390,15 @@ wait:
   if (threadIdx.x == 0) {
     int go = 0;
     const unsigned long long t0 = wall_clock64();
+    const unsigned long long lim = fa.wait_ticks ? fa.wait_ticks : 100000000ull;
 #ifdef SLIO_SOLVE_STAMP
     if (blockIdx.x == 0) g_sstamp[40 + ((fa.iter + p + 1) & 3)] = t0;  // per pass: block 0 waits
 #endif
     while (true) {
+      if (lim == 1) {  // give up at once (the test hook of slio_debug_wait_limit)
+        __hip_atomic_store(&fa.hblk->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
       const uint64_t fl = __hip_atomic_load((const guint64*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((int32_t)(fl >> 32) == fa.gseq) {
         if (fl & 0x80000000ull) break;  // the update ended
@@ -3399,7 +3407,10 @@ wait:
           break;
         }
       }
-      if (wall_clock64() - t0 > 100000000ull) break;  // 100 MHz: 1 s
+      if (wall_clock64() - t0 > lim) {  // 100 MHz: 1 s
+        __hip_atomic_store(&fa.hblk->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
       __builtin_amdgcn_s_sleep(4);  // (1 / 16 / 64: the same pass times, profiles/r05_persist_stamps.log)
     }
     s_go = go;
@@ -3719,11 +3730,20 @@ struct Ctx {
   int ncu = 0;
   int64_t persist_cap = -1;
   int last_path = 0;  // the last device-resident update: 1 persistent launch, 0 a launch per pass
+  bool dev_counted = false;  // counted in dev_users (slio_create succeeded)
+  uint64_t wait_ticks = 0;  // device-side waits give up after this many 100 MHz ticks (0: 1 s;
+                            // slio_debug_wait_limit)
   // host clock stamps (CLOCK_MONOTONIC ns) of the last device-resident update
   // (slio_debug_host_stamps)
   bool hstamp = false;
   int64_t hst[8] = {};
 };
+
+int dev_users(int device, int delta) {
+  static std::atomic<int> users[256];
+  if (device < 0 || device >= 256) return 0;
+  return users[device].fetch_add(delta) + delta;
+}
 
 static bool env_on(const char* name) {
   const char* e = std::getenv(name);
@@ -3948,6 +3968,20 @@ static hipError_t wait_published(Ctx& c) {
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   return hipSuccess;
+}
+
+// After an update that did not complete (a device-side wait gave up, or a
+// launch failed): wait for the handle's stream to drain, then zero the
+// arrival counters (segment rows, passes, far queue), the persistent update's
+// flag replicas and, on a group's rank 0, the ranks' arrival word and gate
+// flag, so that the next update's last arriver is the right one.
+static void reset_update_counters(Ctx& c) {
+  (void)hipStreamSynchronize(c.stream);
+  if (c.count) (void)hipMemsetAsync(c.count, 0, sizeof(uint32_t) * kCountWords, c.stream);
+  if (c.goflag) (void)hipMemsetAsync(c.goflag, 0, sizeof(uint64_t) * 8 * kGoFlagStride, c.stream);
+  if (c.garrive) (void)hipMemsetAsync(c.garrive, 0, 4 * sizeof(uint32_t), c.stream);
+  (void)hipStreamSynchronize(c.stream);
+  (void)hipGetLastError();
 }
 
 // Fused filter step of a single-rank device-resident update.
@@ -4330,6 +4364,8 @@ int slio_create(slio_handle* out, const slio_params* p) {
     return SLIO_ENOMEM;
   }
   h->c.d_super = h->c.d_super_own;
+  h->c.dev_counted = true;
+  dev_users(p->device, +1);
   *out = h;
   return SLIO_OK;
 }
@@ -4363,6 +4399,7 @@ int slio_destroy(slio_handle h) {
   map_attach(h->c, nullptr);
   if (h->c.map_ev) (void)hipEventDestroy(h->c.map_ev);
   if (h->c.own_stream) (void)hipStreamDestroy(h->c.own_stream);
+  if (h->c.dev_counted) dev_users(h->c.prm.device, -1);
   delete h;
   return SLIO_OK;
 }
@@ -4392,6 +4429,16 @@ int slio_debug_host_stamps(slio_handle h, int enable, int64_t out[8]) {
   if (!h) return SLIO_EINVAL;
   if (out) std::memcpy(out, h->c.hst, sizeof(h->c.hst));
   if (enable >= 0) h->c.hstamp = enable != 0;
+  return SLIO_OK;
+}
+
+int slio_debug_wait_limit(slio_handle h, int64_t ticks) {
+  SLIO_CHECK_H(h);
+  if (ticks < 0) {
+    set_error("slio_debug_wait_limit: ticks < 0");
+    return SLIO_EINVAL;
+  }
+  h->c.wait_ticks = (uint64_t)ticks;
   return SLIO_OK;
 }
 
@@ -6853,7 +6900,11 @@ __global__ void k_s2m_coeff(const float* __restrict__ wx, const float* __restric
 
 // LMOptimization rows (:1583-1626, lidar <-> camera axis swap included) of the
 // selected points and their A^T A (21) / A^T B (6) / count, summed in double:
-// each workgroup its 256 points in a fixed tree, one partial per workgroup
+// each workgroup its 256 points in a fixed tree (a butterfly over each
+// wavefront's lanes, then the four wavefronts in order), one partial per
+// workgroup.  (The 28 sequential block-wide LDS trees this replaces -- 252
+// barriers -- took 27.8 us per launch for 20k points,
+// profiles/r05_final_s2m_kernel_stats.csv.)
 struct S2mTrig {
   float srx, crx, sry, cry, srz, crz;
 };
@@ -6862,7 +6913,7 @@ __global__ __launch_bounds__(256) void k_s2m_rows(const float* __restrict__ bx, 
                                                   const float* __restrict__ bz, const float4* __restrict__ coeff,
                                                   const uint8_t* __restrict__ sel, int64_t n, S2mTrig T,
                                                   double* __restrict__ partial) {
-  __shared__ double red[256];
+  __shared__ double red[4 * kS2mSums];
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   double v[kS2mSums];
 #pragma unroll
@@ -6891,15 +6942,20 @@ __global__ __launch_bounds__(256) void k_s2m_rows(const float* __restrict__ bx, 
     for (int r = 0; r < 6; ++r) v[21 + r] = (double)a[r] * (double)b;
     v[27] = 1.0;
   }
-  for (int k = 0; k < kS2mSums; ++k) {
-    red[threadIdx.x] = v[k];
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-      if (threadIdx.x < st) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + st];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) partial[(int64_t)blockIdx.x * kS2mSums + k] = red[0];
-    __syncthreads();
+  // (a + b == b + a: both lanes of a butterfly pair hold the same sum)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < kS2mSums; ++k) v[k] = v[k] + __shfl_xor(v[k], off);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < kS2mSums; ++k) red[w * kS2mSums + k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < kS2mSums) {
+    const int k = threadIdx.x;
+    partial[(int64_t)blockIdx.x * kS2mSums + k] =
+        ((red[k] + red[kS2mSums + k]) + red[2 * kS2mSums + k]) + red[3 * kS2mSums + k];
   }
 }
 
@@ -7394,6 +7450,7 @@ struct UpdateRun {
     hc.last_m = 0;
     hc.singular = 0;
     hc.published = 0;
+    hc.timeout = 0;
     for (int k = 0; k < 24; ++k) hc.dxn[k] = 0.0;  // x == x_propagated on pass 0
   }
 
@@ -7482,9 +7539,15 @@ struct UpdateRun {
 
   // The whole update as one persistent launch (k_update_persist): the fused
   // configuration, and every chunk's workgroup resident at once (the
-  // occupancy the device reports for the kernel, times its CUs).
+  // occupancy the device reports for the kernel, times its CUs).  That
+  // count assumes the launch has the device to itself: with another live
+  // handle on the device (its kernels, or another persistent launch, may
+  // hold CUs while this launch's spinning workgroups wait for chunks that
+  // cannot start) or a map shared with other handles, it takes a launch
+  // per pass instead.
   bool persist_ok() {
     if (!c.sw.persist || c.sw.no_fuse0 || !fusable() || !c.goflag || c.ncu <= 0) return false;
+    if (dev_users(c.prm.device, 0) > 1 || (c.map && c.map->users.size() > 1)) return false;
     if (c.persist_cap < 0) {
       int b6 = 0, b12 = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b6, k_update_persist<SLIO_SEARCH_U, 6>,
@@ -7518,6 +7581,7 @@ struct UpdateRun {
                 nullptr, nullptr,
                 c.upd_seq};
     fa.goflag = c.goflag;
+    fa.wait_ticks = c.wait_ticks;
     if (int rc = enqueue_pass(c, &pose0, c.ctl, 1, ext, &sa, true, false, nullptr, &fa, maxit - first)) return rc;
     SLIO_HSTAMP(c, 3);
     SLIO_HIP(hipGetLastError());
@@ -7540,10 +7604,22 @@ struct UpdateRun {
     SLIO_HIP(wait_published(c));
     SLIO_HSTAMP(c, 5);
     const IkfCtl& hc = *c.h_ctl;
-    if (!hc.done) {
-      set_error("slio_ikf_update_device: the update did not complete (passes " + std::to_string(hc.passes) +
-                ", searches " + std::to_string(hc.searches) + ", converge " + std::to_string(hc.converge) +
-                ", published " + std::to_string(hc.published) + ")");
+    // a wait that gave up let a pass run before its predecessor's filter step
+    // (or skipped passes): the result is void even if the update ended
+    if (!hc.done || hc.timeout) {
+      const bool to = hc.timeout != 0;
+      const std::string st = "(passes " + std::to_string(hc.passes) + ", searches " + std::to_string(hc.searches) +
+                             ", converge " + std::to_string(hc.converge) + ", published " +
+                             std::to_string(hc.published) + ")";
+      // some workgroups (or ranks) may have arrived on the handle's counters
+      // and others never will: back to zero before the next update
+      reset_update_counters(c);
+      if (to) {
+        set_error("slio_ikf_update_device: a device-side wait gave up (persistent pass flag or group gate, "
+                  "> 1 s) " + st + "; the handle's arrival counters were reset");
+        return SLIO_ETIMEOUT;
+      }
+      set_error("slio_ikf_update_device: the update did not complete " + st);
       return SLIO_EDEVICE;
     }
     if (hc.singular) {
@@ -7591,9 +7667,15 @@ __global__ __launch_bounds__(256) void k_group_reduce(GroupSupers g) {
 // pass workgroups (<= the scan's chunks) always fit beside the N gates.  A
 // wait past ~1 s gives up (the next pass then exits and the update reports
 // that it did not complete) instead of hanging.
-__global__ __launch_bounds__(64) void k_group_gate(const uint32_t* __restrict__ garrive, int pass_idx, int32_t seq) {
+__global__ __launch_bounds__(64) void k_group_gate(const uint32_t* __restrict__ garrive, int pass_idx, int32_t seq,
+                                                   IkfCtl* __restrict__ hblk, uint64_t wait_ticks) {
   if (threadIdx.x != 0) return;
   const unsigned long long t0 = wall_clock64();
+  const unsigned long long lim = wait_ticks ? wait_ticks : 100000000ull;
+  if (lim == 1) {  // give up at once (the test hook of slio_debug_wait_limit)
+    __hip_atomic_store(&hblk->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   while (true) {
     const uint64_t fl = __hip_atomic_load((const guint64*)(const uint64_t*)(garrive + 2), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
@@ -7603,7 +7685,11 @@ __global__ __launch_bounds__(64) void k_group_gate(const uint32_t* __restrict__ 
     // this update's step has counted the pass or ended the update, or a newer
     // update owns the group (a stale gate)
     if ((fseq == seq && (done || passes >= pass_idx)) || (int32_t)(fseq - seq) > 0) return;
-    if (wall_clock64() - t0 > 100000000ull) return;  // 100 MHz: 1 s
+    if (wall_clock64() - t0 > lim) {  // 100 MHz: 1 s
+      // the group's mapped host block reports the timeout (SLIO_ETIMEOUT)
+      __hip_atomic_store(&hblk->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     __builtin_amdgcn_s_sleep(2);
   }
 }
@@ -7855,7 +7941,7 @@ static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], do
       const int which = p0 ? 1 : (mode == SLIO_MODE_FIXED ? 1 : 2);
       for (int r = 0; r < n && !rc; ++r) {
         Ctx& cr = hs[r]->c;
-        if (!p0) k_group_gate<<<1, 64, 0, cr.stream>>>(c0.garrive, i - runs[0].first, seq);
+        if (!p0) k_group_gate<<<1, 64, 0, cr.stream>>>(c0.garrive, i - runs[0].first, seq, c0.d_hctl, c0.wait_ticks);
         const SolveArgs sa = runs[r].args(i);
         const FuseArgs fa{c0.ctl,  (p0 && r == 0) ? (const IkfCtl*)c0.d_hctl : nullptr,
                           cr.d_seg, c0.gsup,
@@ -7865,7 +7951,8 @@ static int group_update(slio_handle* hs, int n, slio_state* x, double P[576], do
                           C,       kNSeg / n,
                           r * (SLIO_NSUPER / n), n,
                           c0.gsup, c0.garrive,
-                          seq};
+                          seq,     nullptr,
+                          c0.wait_ticks};
         rc = enqueue_pass(cr, p0 ? &runs[r].pose0 : nullptr, c0.ctl, which, extrinsic_est, &sa, true, false,
                           nullptr, &fa);
         if (!rc && hipGetLastError() != hipSuccess) {
@@ -8020,6 +8107,10 @@ int slio_group_ikf_update(slio_handle* hs, int n, slio_state* x, double P[576], 
     for (int r = 0; r < n; ++r) {
       (void)hipSetDevice(hs[r]->c.prm.device);
       (void)hipStreamSynchronize(hs[r]->c.stream);
+    }
+    for (int r = 0; r < n; ++r) {
+      (void)hipSetDevice(hs[r]->c.prm.device);
+      reset_update_counters(hs[r]->c);
     }
   }
   (void)hipSetDevice(caller_dev);

@@ -1671,6 +1671,7 @@ using namespace slio;
 using namespace slio::lio;
 
 struct slio_lio {
+  bool dev_counted = false;  // counted in slio::dev_users
   slio_lio_params prm{};
   Geo g{};
   hipStream_t own = nullptr, stream = nullptr;
@@ -1881,6 +1882,8 @@ int slio_lio_create(slio_lio_handle* out, const slio_lio_params* p) {
     return SLIO_ENOMEM;
   }
   feat_set_smem<kModeLio>(fsm, sort_items(h->fc.sort_cap), vox_items(h->fc.vox_cap));
+  h->dev_counted = true;
+  slio::dev_users(h->prm.device, +1);
   *out = h;
   return SLIO_OK;
 }
@@ -1890,6 +1893,7 @@ int slio_lio_destroy(slio_lio_handle h) {
   (void)hipSetDevice(h->prm.device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   lio_free(h);
+  if (h->dev_counted) slio::dev_users(h->prm.device, -1);
   delete h;
   return SLIO_OK;
 }
@@ -2754,8 +2758,14 @@ __global__ __launch_bounds__(kLegoBandThreads) void k_lego_cc_band(
     }
   }
   BSTAMP(5);
-  // 5. arrival (after every wave's stores have completed); the last band merges
+  // 5. arrival (after every wave's stores have completed); the last band merges.
+  // The band's parent / csize / rows lines are written back from this XCD's L2
+  // (agent-scope release: buffer_wbl2) before the arrival: the merging band,
+  // possibly on another XCD, overwrites some of the same words with plain
+  // stores, and two L2s holding the same dirty words write them back at the
+  // kernel's end in any order -- the band's stale copy could win.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (t == 0)
     s_last = __hip_atomic_fetch_add(arrive_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1;
@@ -3381,6 +3391,7 @@ extern "C" int slio_dbg_cc_stamps(unsigned long long* out) {
 #endif
 
 struct slio_lego {
+  bool dev_counted = false;  // counted in slio::dev_users
   slio_lego_params prm{};
   LGeo g{};
   hipStream_t own = nullptr, stream = nullptr;
@@ -3651,6 +3662,8 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
       return SLIO_EDEVICE;
     }
   }
+  h->dev_counted = true;
+  slio::dev_users(h->prm.device, +1);
   *out = h;
   return SLIO_OK;
 }
@@ -3660,6 +3673,7 @@ int slio_lego_destroy(slio_lego_handle h) {
   (void)hipSetDevice(h->prm.device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   lego_free(h);
+  if (h->dev_counted) slio::dev_users(h->prm.device, -1);
   delete h;
   return SLIO_OK;
 }
@@ -3769,24 +3783,35 @@ int slio_lego_run_async(slio_lego_handle h) {
   // atomics (SLIO_LEGO_CC_LDS1 / SLIO_LEGO_CC_GLOBAL; all give the same labels)
   const bool cc_band = h->seam && !h->cc_global && !h->cc_lds1;
   const bool cc_lds = !cc_band && g.cells <= kLegoCcCells && !h->cc_global;
-  // this sweep's owner table: the one the last sweep cleared
-  if (h->swept) std::swap(h->owner, h->owner_alt);
-  h->swept = true;
+  // this sweep's owner table: the one the last sweep cleared; the swap is
+  // committed only once k_lego_label (which clears the other table for the
+  // next sweep) is enqueued, and a failed enqueue re-clears both tables
+  int32_t* own = h->swept ? h->owner_alt : h->owner;
+  int32_t* idle = h->swept ? h->owner : h->owner_alt;
+  auto fail = [&](hipError_t e) {
+    (void)hipGetLastError();
+    (void)hipMemsetAsync(h->owner, 0xff, 4 * g.cells, h->stream);
+    (void)hipMemsetAsync(h->owner_alt, 0xff, 4 * g.cells, h->stream);
+    (void)hipStreamSynchronize(h->stream);
+    h->swept = false;
+    set_error(std::string("slio_lego_run_async: ") + hipGetErrorString(e));
+    return SLIO_EDEVICE;
+  };
   if (!cc_lds && !cc_band) {
-    LIO_HIP(hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream));
-    LIO_HIP(hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream));
+    hipError_t e = hipMemsetAsync(h->csize, 0, 4 * g.cells, h->stream);
+    if (!e) e = hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream);
+    if (e) return fail(e);
   }
   if (h->n > 0)
-    k_lego_claim<<<(unsigned)((h->n + 255) / 256), 256, 0, h->stream>>>(h->x, h->y, h->z, h->n, g,
-                                                                          h->owner);
-  k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, h->owner, h->range_mat, h->full, h->ground);
-  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, h->owner, h->full, h->ground, h->parent,
+    k_lego_claim<<<(unsigned)((h->n + 255) / 256), 256, 0, h->stream>>>(h->x, h->y, h->z, h->n, g, own);
+  k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, own, h->range_mat, h->full, h->ground);
+  k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, own, h->full, h->ground, h->parent,
                                                            !cc_lds && !cc_band);
   if (cc_band) {
     k_lego_cc_band<<<(g.H + kLegoBandW - 1) / kLegoBandW, kLegoBandThreads, 0, h->stream>>>(
-        g, h->owner, h->ground, h->range_mat, h->parent, h->csize, h->rows, h->seam, h->cc_arrive);
+        g, own, h->ground, h->range_mat, h->parent, h->csize, h->rows, h->seam, h->cc_arrive);
   } else if (cc_lds) {
-    k_lego_edges<<<cb, 256, 0, h->stream>>>(g, h->owner, h->ground, h->range_mat, h->edges, h->csize, h->rows);
+    k_lego_edges<<<cb, 256, 0, h->stream>>>(g, own, h->ground, h->range_mat, h->edges, h->csize, h->rows);
     k_lego_cc<<<1, kLegoCcThreads, 5 * g.cells, h->stream>>>(g, h->edges, h->parent, h->csize, h->rows);
   } else {
     k_lego_union<<<cb, 256, 0, h->stream>>>(g, h->range_mat, h->parent);
@@ -3798,7 +3823,11 @@ int slio_lego_run_async(slio_lego_handle h) {
                    h->outlier, h->nseg};
   k_lego_extract<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
                                                        h->cnt, h->range_mat, h->full, h->rootlab, sg);
-  k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label, h->owner_alt);
+  k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label, idle);
+  if (const hipError_t e = hipGetLastError()) return fail(e);
+  h->owner = own;
+  h->owner_alt = idle;
+  h->swept = true;
   // adjustDistortion
   const int nslot = (int)cb;
   k_lego_half<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->orient[0], h->slot, h->io,

@@ -73,14 +73,20 @@ class ScanToMap:
         self.n_corner = _upload(self.lib, self.lib.slio_scan_upload, self.hc, corner_last_ds)
         self.n_surf = _upload(self.lib, self.lib.slio_scan_upload, self.hs, surf_last_ds)
 
-    def corner_optimization(self, transform: np.ndarray) -> int:
+    def corner_optimization(self, transform: np.ndarray, count: bool = True) -> int:
+        """:1303-1432; count: return the selected points (a device -> host
+        copy and a wait; the LM loop takes the count from the normal
+        equations instead)."""
         k = C.c_int64()
-        L.check(self.lib.slio_s2m_coeffs(self.hc, 0, L.fptr(transform), C.byref(k)), "cornerOptimization")
+        L.check(self.lib.slio_s2m_coeffs(self.hc, 0, L.fptr(transform), C.byref(k) if count else None),
+                "cornerOptimization")
         return k.value
 
-    def surf_optimization(self, transform: np.ndarray) -> int:
+    def surf_optimization(self, transform: np.ndarray, count: bool = True) -> int:
+        """:1438-1515 (see corner_optimization)."""
         k = C.c_int64()
-        L.check(self.lib.slio_s2m_coeffs(self.hs, 1, L.fptr(transform), C.byref(k)), "surfOptimization")
+        L.check(self.lib.slio_s2m_coeffs(self.hs, 1, L.fptr(transform), C.byref(k) if count else None),
+                "surfOptimization")
         return k.value
 
     def normal_equations(self, transform: np.ndarray):
@@ -108,8 +114,8 @@ class ScanToMap:
         if not (self.n_corner > EDGE_FEATURE_MIN_VALID_NUM and self.n_surf > SURF_FEATURE_MIN_VALID_NUM):
             return tf
         for it in range(30):
-            self.corner_optimization(tf)
-            self.surf_optimization(tf)
+            self.corner_optimization(tf, count=False)
+            self.surf_optimization(tf, count=False)
             self.iterations = it + 1
             if self.LMOptimization(tf, it):
                 break

@@ -408,3 +408,38 @@ def make_vlp16_sweep(seed: int = 20261015, horizon: int = 1800, yaw_rate: float 
                gyro=np.tile([0.0, 0.0, yaw_rate], (stamps.size, 1)))
     return dict(x=np.ascontiguousarray(pts[:, 0]), y=np.ascontiguousarray(pts[:, 1]),
                 z=np.ascontiguousarray(pts[:, 2]), time_scan_cur=time_scan_cur, imu=imu)
+
+
+def s2m_lidar_pose(fr):
+    """LIO-SAM's transformTobeMapped (roll, pitch, yaw, x, y, z) of a frame's
+    ground-truth LiDAR pose, with its rotation matrix and translation."""
+    R = quat_matrix(fr.gt_rot)
+    t = fr.gt_pos + R @ AVIA_T_LI
+    yaw = np.arctan2(R[1, 0], R[0, 0])
+    pitch = np.arcsin(-R[2, 0])
+    roll = np.arctan2(R[2, 1], R[2, 2])
+    return np.array([roll, pitch, yaw, *t], np.float32), R, t
+
+
+def make_s2m_problem(seed: int = 20261015, n_map: int = 200000, n_surf: int = 20000) -> dict:
+    """A LIO-SAM scan-to-map problem (mapOptmization.cpp:1706-1740): the
+    surf map sampled from the urban scene, a corner map along the buildings'
+    vertical edges (0.1 m apart), the surf scan (an Avia-like frame) and the
+    corner scan (edge points within 40 m of the sensor, in the LiDAR frame),
+    and the ground-truth transformTobeMapped."""
+    scene = make_scene(seed, n_map)
+    surf_map = sample_map(scene, seed, n_map)
+    rng = np.random.default_rng(4)
+    lines = []
+    for b in scene.boxes:
+        for (cx, cy) in ((b[0], b[1]), (b[2], b[1]), (b[0], b[3]), (b[2], b[3])):
+            z = np.arange(0.0, b[5], 0.1)
+            lines.append(np.stack([cx + rng.normal(0, 0.005, z.size), cy + rng.normal(0, 0.005, z.size), z], 1))
+    corner_map = np.concatenate(lines).astype(np.float32)
+    fr = make_frame(scene, seed, n_surf, "avia")
+    tf, R, t = s2m_lidar_pose(fr)
+    near = np.linalg.norm(corner_map[:, :2] - t[:2], axis=1) < 40
+    cw = corner_map[near][::3]
+    cw = cw + rng.normal(0, 0.01, cw.shape)
+    corner_scan = ((cw - t) @ R).astype(np.float32)
+    return dict(surf_map=surf_map, corner_map=corner_map, surf_scan=fr.body, corner_scan=corner_scan, tf=tf)

@@ -583,9 +583,185 @@ def bench_c5(args, rank, world, dev, dist):
         raise SystemExit("C5: a concurrent replica's result differs from its solo run")
 
 
-def synth_t_li():
+def bench_s2m(args, rank, world, dev, dist):
+    """LIO-SAM mapOptimization::scan2MapOptimization (mapOptmization.cpp:
+    1706-1740) on the device: per LM iteration
+    cornerOptimization + surfOptimization (pointAssociateToMap, exact 5-NN in
+    the corner / surf local maps, line / plane fits, :1303-1515), the
+    LMOptimization normal equations on the device (:1552-1626) and the 6 x 6
+    step on the host (slio_s2m_lm_step).  One step = one scan2MapOptimization
+    call from the same perturbed prior to convergence (<= 30 iterations, the
+    reference's loop); value = LM iterations/s (and scans/s).  N > 1:
+    replicas (no collective)."""
+    from agi_lidar_slam_amd import _lib as L, build, synth
+    from agi_lidar_slam_amd.lio_sam import ScanToMap
+
+    if rank == 0:
+        build.build()
+    if world > 1:
+        dist.barrier()
+    L.load()
+    pr = synth.make_s2m_problem()
+    s = ScanToMap(max_points=max(pr["surf_scan"].shape[0], pr["corner_scan"].shape[0]), device=dev)
+    s.set_maps(pr["corner_map"], pr["surf_map"])
+    s.set_scan(pr["corner_scan"], pr["surf_scan"])
+    tf0 = pr["tf"] + np.array([0.005, -0.004, 0.01, 0.15, -0.1, 0.05], np.float32)
+    lib = s.lib
+    for _ in range(args.warmup):
+        s.scan2MapOptimization(tf0)
+    iters = s.iterations
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tf = s.scan2MapOptimization(tf0)
+    el = time.perf_counter() - t0
+    assert s.iterations == iters
+    # the dominant kernel's time (HIP events on the kNN passes, SLIO_KERNEL_SEARCH) and
+    # the whole iteration's device time, over further steps after the timed region
+    ms, nl = C.c_double(), C.c_int64()
+    search_bit = 1 << (L.SLIO_KERNEL_SEARCH + 1)
+    per_kernel = {}
+    if not args.no_kernel_timing:
+        for h in (s.hc, s.hs):
+            lib.slio_profile(h, search_bit)
+        for _ in range(max(1, args.timing_steps // 4)):
+            s.scan2MapOptimization(tf0)
+        for name, h in (("corner", s.hc), ("surf", s.hs)):
+            lib.slio_profile(h, search_bit | L.SLIO_PROFILE_KEEP)
+            lib.slio_profile_read(h, L.SLIO_KERNEL_SEARCH, C.byref(ms), C.byref(nl))
+            per_kernel[name] = (ms.value, nl.value)
+            lib.slio_profile(h, 0)
+    if world > 1:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    nc, ns = pr["corner_scan"].shape[0], pr["surf_scan"].shape[0]
+    value = args.steps * iters * world / el
+    # kNN pass (slio_s2m_coeffs' search launch, kNN-only): per query point the
+    # point (12 B), its 5 neighbours (80 B with the map index), the neighbour
+    # positions, ids and distances written (60 B)
+    alg = {"corner": 152 * nc, "surf": 152 * ns}
+    roof = None
+    if per_kernel and per_kernel["surf"][1] > 0:
+        avg_s = per_kernel["surf"][0] / per_kernel["surf"][1] * 1e-3
+        achieved = alg["surf"] / avg_s / 1e9
+        roof = {"bound": "hbm", "kernel": "k_search_pass (kNN-only: the surf cloud's 5-NN per LM iteration)",
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None, "alg_bytes_per_launch": alg["surf"], "avg_launch_us": avg_s * 1e6,
+                "launches": int(per_kernel["surf"][1]),
+                "corner_launch_us": (per_kernel["corner"][0] / max(per_kernel["corner"][1], 1)) * 1e3,
+                "timing": "HIP events in the dispatch packet of the kNN launches of further calls"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        Tc, Ts = O.Tree(pr["corner_map"]), O.Tree(pr["surf_map"])
+        n = max(1, args.cpu_s2m_iters)
+        tfc = tf0.copy()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            clouds = []
+            for kind, T, body, mp in ((0, Tc, pr["corner_scan"], pr["corner_map"]),
+                                      (1, Ts, pr["surf_scan"], pr["surf_map"])):
+                wpt = O.s2m_transform(tfc, body)
+                idx, sqd = T.knn(wpt, 5, threads=1)
+                cf, sl = O.s2m_coeffs(kind, wpt, mp, idx, sqd)
+                clouds.append((body, cf, sl))
+            O.s2m_normal_equations(tfc, clouds)
+        cel = time.perf_counter() - t0
+        cpu = {"value": n / cel, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+               "sample": (f"{n} LM iterations (pointAssociateToMap + kd-tree 5-NN + corner / surf "
+                          f"coefficients + normal equations, {nc} corner + {ns} surf points) of the "
+                          f"single-threaded C++ restatement; host {cpu_model()}")}
+    out = {
+        "metric": "LIO-SAM scan2MapOptimization LM iterations/sec",
+        "value": value,
+        "unit": "LM iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "scans_per_s": args.steps * world / el,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (kNN, fits, coefficients) + f64 (normal-equation sums)",
+        "data": "synthetic (seeded urban scene: surf map sampled from its surfaces, corner map along its "
+                "vertical edges; Avia-like surf scan)",
+        "config": {
+            "workload": (f"LIO-SAM scan2MapOptimization: {nc} corner + {ns} surf points vs a "
+                         f"{pr['corner_map'].shape[0]}-pt corner map and a {pr['surf_map'].shape[0]}-pt "
+                         f"surf map, {iters} LM iterations to convergence"),
+            "lm_iterations_per_step": iters,
+            "degenerate": int(s.isDegenerate.value),
+            "final_error_m": float(np.abs(tf[3:] - pr["tf"][3:]).max()),
+            "parallelism": (f"replicas x{world}, no collective" if world > 1 else "single GPU"),
+        },
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    s.close()
+
+
+def synth_t_li():def synth_t_li():
     from agi_lidar_slam_amd import synth
     return synth.AVIA_T_LI
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def resolve_gpus(args, argv=None):
+    """--gpus N against the launch (before anything touches a GPU):
+
+    * under torch.distributed.run (WORLD_SIZE set): N must equal WORLD_SIZE;
+      with the nccl backend every local rank needs a device of its own;
+    * a plain `bench.py --gpus N`, N > 1: the N ranks are started here, one
+      process per GPU, by torch.distributed.run in a child process (the
+      driver's own launch; this process never initialises a GPU, then exits
+      with the child's status);
+    * N must not exceed the visible devices (torch.cuda.device_count() does
+      not initialise the GPU on this image): a run that cannot place its ranks
+      exits non-zero instead of printing a line measured on fewer GPUs.
+
+    Returns None to go on in this process, else the exit status."""
+    import subprocess
+    if args.gpus < 1:
+        log(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        world = int(env_world)
+        if world != args.gpus:
+            log(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world} (one rank per GPU)")
+            return 2
+        if world > 1 and args.dist_backend == "nccl":
+            import torch
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            ndev = torch.cuda.device_count()
+            if ndev < local_world:
+                log(f"bench.py: {local_world} ranks on this node need {local_world} GPUs, {ndev} visible")
+                return 2
+        return None
+    if args.gpus == 1:
+        return None
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus and args.dist_backend == "nccl":
+        log(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {ndev} visible")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    log(f"bench.py: --gpus {args.gpus}: one rank per GPU via {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
 
 
 def main():
@@ -622,14 +798,14 @@ def main():
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
     ap.add_argument("--group-ranks", type=int, default=8,
                     help="group: ranks of the one-GPU C4 rehearsal (must divide 8)")
-    ap.add_argument("--workload", choices=["c2", "c3", "c5", "lego", "group"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c5", "lego", "group", "s2m"], default="c2",
                     help="c2: IKF iterations/s, 100k Avia scan vs 10M map (BASELINE.json metric); "
                          "c3: LIO-SAM front-end scans/s on a 64 x 2048 Ouster scan; "
                          "c5: batched replay, --replicas concurrent distinct 100k scans per GPU vs a "
                          "shared 50M map (BASELINE config 5: 32 scans on 8 GPUs = 4 per GPU); "
                          "lego: LeGO-LOAM front-end scans/s on a VLP-16 16 x 1800 sweep, IMU on; "
                          "group: the C4 group path (slio_group_ikf_update) rehearsed with --group-ranks "
-                         "ranks on one GPU")
+                         "ranks on one GPU; s2m: LIO-SAM scan2MapOptimization LM iterations/s")
     ap.add_argument("--replicas", type=int, default=4, help="c5: concurrent scans per GPU")
     ap.add_argument("--cpu-scans-c5", type=int, default=4)
     ap.add_argument("--reduce-hook", action="store_true",
@@ -637,6 +813,7 @@ def main():
                          "instead of the library's own RCCL communicator (slio_comm_init); implied by "
                          "--dist-backend gloo (RCCL refuses two ranks on one device)")
     ap.add_argument("--cpu-scans-c3", type=int, default=300)
+    ap.add_argument("--cpu-s2m-iters", type=int, default=40)
     ap.add_argument("--cpu-scans-lego", type=int, default=300)
     ap.add_argument("--c3-streams", type=int, default=1,
                     help="c3: independent scans in flight per GPU, each on its own handle and stream "
@@ -647,6 +824,9 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "search_traffic.json"))
     args = ap.parse_args()
 
+    rc = resolve_gpus(args)
+    if rc is not None:
+        raise SystemExit(rc)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -662,8 +842,8 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev)
         dist.init_process_group(args.dist_backend if args.workload == "c2" else "gloo")
-    if args.workload in ("c3", "c5", "lego", "group"):
-        {"c3": bench_c3, "c5": bench_c5, "lego": bench_lego, "group": bench_group}[args.workload](
+    if args.workload in ("c3", "c5", "lego", "group", "s2m"):
+        {"c3": bench_c3, "c5": bench_c5, "lego": bench_lego, "group": bench_group, "s2m": bench_s2m}[args.workload](
             args, rank, world, dev, dist)
         if world > 1:
             dist.destroy_process_group()

@@ -49,7 +49,11 @@ enum {
   SLIO_ENOMEM = -2,    /* device or host allocation failed */
   SLIO_EDEVICE = -3,   /* HIP runtime error */
   SLIO_ECAPACITY = -4, /* scan larger than params.max_points */
-  SLIO_ESTATE = -5     /* call out of order (e.g. iterate before map upload) */
+  SLIO_ESTATE = -5,    /* call out of order (e.g. iterate before map upload) */
+  SLIO_ETIMEOUT = -6   /* a device-side wait of the update gave up (the persistent
+                          update's pass flag or a fused group's gate, > 1 s): the
+                          result is not written; the handle's arrival counters
+                          are reset, so the next update runs normally */
 };
 
 typedef struct slio_ctx* slio_handle;
@@ -477,6 +481,12 @@ int slio_debug_host_stamps(slio_handle h, int enable, int64_t out[8]);
  * search's 5 nearest and bound, out[1] queries searched in full in passes that write
  * certificates (device-resident passes after the first). */
 int slio_debug_knn_cert(slio_handle h, uint32_t out[2]);
+/* The device-side waits of the next updates on this handle (a persistent
+ * update's workgroups waiting for the pass flag; on a group's rank 0, every
+ * rank's gate between fused group passes) give up after `ticks` 100 MHz
+ * clock ticks instead of 1 s (0 restores 1 s).  A test hook: 1 forces the
+ * give-up path (SLIO_ETIMEOUT, counters reset). */
+int slio_debug_wait_limit(slio_handle h, int64_t ticks);
 
 #ifdef __cplusplus
 }

@@ -177,11 +177,9 @@ def preproc(n_raw):
 
 
 def s2m():
-    import test_gpu_lio_s2m as T
+    from agi_lidar_slam_amd import synth
     from agi_lidar_slam_amd.lio_sam import ScanToMap
-    pr = T.problem.__wrapped__() if hasattr(T.problem, "__wrapped__") else None
-    if pr is None:
-        return
+    pr = synth.make_s2m_problem()
     s = ScanToMap(max_points=60000)
     s.set_maps(pr["corner_map"], pr["surf_map"])
     s.set_scan(pr["corner_scan"], pr["surf_scan"])

@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-tag=${1:-r05b}
+tag=${1:-r06b}
 part=${2:-1}
 if [ $part = 1 ]; then
 bash scripts/pmc_search.sh $tag || exit 2

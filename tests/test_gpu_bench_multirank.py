@@ -37,6 +37,16 @@ def test_bench_two_ranks_gloo_matches_single():
     assert two["result_digest"] == one["result_digest"]
 
 
+def test_bench_gpus_spawns_its_ranks():
+    """A plain `bench.py --gpus 2` (no torch.distributed.run around it) starts
+    its two ranks itself, one process each, before touching a GPU: the same
+    line as the driver's torchrun launch (gloo here: the box has one GPU)."""
+    one = _run([sys.executable, "bench.py", *SMALL])
+    two = _run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", *SMALL])
+    assert two["n_gpus"] == 2 and two["value"] > 0
+    assert two["result_digest"] == one["result_digest"]
+
+
 def test_bench_reference_flow_line():
     """--mode reference --iters 3 (the drop-in's control flow, mapping_avia.launch:11):
     a bench line whose passes include reuse passes, with a roofline."""

@@ -168,3 +168,54 @@ def test_comm_init_one_rank_bitwise(L, c2):
         assert (stt.passes, stt.searches, stt.valid_passes, stt.last_m) == s1
     finally:
         lib.slio_destroy(h)
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_group_gate_timeout_reported_and_recovers(L, c2, n):
+    """A gate between fused group passes that gives up (forced here through
+    slio_debug_wait_limit(rank 0, 1): every gate gives up at once, so the
+    ranks' passes run without waiting for the group's filter step and their
+    arrivals on the group counter mix passes) is reported as its own error,
+    SLIO_ETIMEOUT, never as a result; the group's and every rank's arrival
+    counters are reset, so the next update (normal wait) is bitwise equal to
+    one rank alone."""
+    mp, fr, _ = c2
+    st = state_of(fr)
+    x1, P1, s1 = single_update(L, mp, fr, st)
+    lib = L.load()
+    p = L.SlioParams()
+    lib.slio_params_default(C.byref(p))
+    p.max_points, p.grid_cell = fr.body.shape[0], C2_CELL
+    hs = (C.c_void_p * n)()
+    dv = (C.c_int32 * n)(*([0] * n))
+    L.check(lib.slio_create_group(hs, n, dv, C.byref(p)), "group")
+    try:
+        upload_map(L, hs[0], mp)
+        for r in range(1, n):
+            L.check(lib.slio_map_share(hs[r], hs[0]), "share")
+        for r in range(n):
+            assert upload_scan(L, hs[r], fr.body) == 0
+
+        def update():
+            xs = slio_state(st)
+            P = np.eye(24) * 1e-2
+            stt = L.SlioIkfStats()
+            rc = lib.slio_group_ikf_update(hs, n, C.byref(xs), L.dptr(P), 0.001, 4, 0, L.SLIO_MODE_FIXED,
+                                           C.byref(stt))
+            return rc, state_array(xs), P, (stt.passes, stt.searches, stt.valid_passes, stt.last_m)
+
+        L.check(lib.slio_debug_wait_limit(hs[0], 1), "wait limit")
+        for _ in range(2):
+            rc, *_ = update()
+            assert rc == L.SLIO_ETIMEOUT, (rc, lib.slio_last_error().decode())
+            assert "gave up" in lib.slio_last_error().decode()
+        L.check(lib.slio_debug_wait_limit(hs[0], 0), "wait limit")
+        for _ in range(2):
+            rc, xg, Pg, sg = update()
+            assert rc == 0, lib.slio_last_error().decode()
+            np.testing.assert_array_equal(xg, x1)
+            np.testing.assert_array_equal(Pg, P1)
+            assert sg == s1
+    finally:
+        for r in range(n):
+            lib.slio_destroy(hs[r])

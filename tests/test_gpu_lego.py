@@ -193,3 +193,45 @@ def test_sector_variants_stress(oracle_mod):
             check_features(oracle_mod, fe, si, P)
         finally:
             fe.close()
+
+
+def seam_sweep(horizon=1800, n_scan=16, res_y=2.0):
+    """Walls all around the sensor: rings above the horizon hit a cylinder of
+    20 m (rings 12-15: one component across every 64-column band seam and
+    the column wrap) or of 8 m (rings 8-11, with no return every 97th column:
+    ~19 components of 96 columns, most across a seam), rings below it the
+    ground -- the seam merge of k_lego_cc_band decides every label."""
+    cols = np.repeat(np.arange(horizon), n_scan)
+    rings = np.tile(np.arange(n_scan), horizon)
+    az = -(cols + 0.25) * (2 * np.pi / horizon) + np.pi
+    el = np.deg2rad(-15.0 + res_y * rings)
+    d = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], 1)
+    rad = np.where(rings >= 12, 20.0, 8.0)
+    with np.errstate(divide="ignore"):
+        t = np.where(d[:, 2] < 0, -1.7 / d[:, 2], rad / np.hypot(d[:, 0], d[:, 1]))
+    keep = ~((rings >= 8) & (rings < 12) & (cols % 97 == 0))
+    p = (d * t[:, None]).astype(np.float32)[keep]
+    return dict(x=p[:, 0].copy(), y=p[:, 1].copy(), z=p[:, 2].copy())
+
+
+def test_components_span_every_seam(oracle_mod):
+    """Components that span every band seam and the column wrap, the same
+    handle run 12 times: labels, sizes and the segmented cloud bit-exact
+    against the oracle every time (the bands' parent / csize / rows stores
+    and the last band's merge stores to the same words must not race through
+    two XCDs' L2 write-backs)."""
+    from agi_lidar_slam_amd.lego import LegoFrontEnd, LegoParams
+    P = LegoParams()
+    sc = seam_sweep()
+    ref = oracle_mod.lego_project(sc["x"], sc["y"], sc["z"], P)
+    fe = LegoFrontEnd(P, max_points=sc["x"].size)
+    try:
+        for _ in range(12):
+            fe.set_imu(None)
+            fe.upload(sc["x"], sc["y"], sc["z"])
+            fe.run()
+            si = check_image(fe, ref)
+        lab = fe.image()["label"]
+        assert len(np.unique(lab[(lab > 0) & (lab < 999999)])) >= 15  # the 20 m wall, the 8 m pieces
+    finally:
+        fe.close()

@@ -19,36 +19,13 @@ pytestmark = pytest.mark.gpu
 
 def lidar_pose(fr):
     from agi_lidar_slam_amd import synth
-    R = synth.quat_matrix(fr.gt_rot)
-    t = fr.gt_pos + R @ synth.AVIA_T_LI
-    yaw = np.arctan2(R[1, 0], R[0, 0])
-    pitch = np.arcsin(-R[2, 0])
-    roll = np.arctan2(R[2, 1], R[2, 2])
-    return np.array([roll, pitch, yaw, *t], np.float32), R, t
+    return synth.s2m_lidar_pose(fr)
 
 
 @pytest.fixture(scope="module")
 def problem():
     from agi_lidar_slam_amd import synth
-    seed = 20261015
-    scene = synth.make_scene(seed, 200000)
-    surf_map = synth.sample_map(scene, seed, 200000)
-    rng = np.random.default_rng(4)
-    # corner map: the vertical edges of the buildings, 0.1 m apart
-    lines = []
-    for b in scene.boxes:
-        for (cx, cy) in ((b[0], b[1]), (b[2], b[1]), (b[0], b[3]), (b[2], b[3])):
-            z = np.arange(0.0, b[5], 0.1)
-            lines.append(np.stack([cx + rng.normal(0, 0.005, z.size), cy + rng.normal(0, 0.005, z.size), z], 1))
-    corner_map = np.concatenate(lines).astype(np.float32)
-    fr = synth.make_frame(scene, seed, 20000, "avia")
-    tf, R, t = lidar_pose(fr)
-    # corner scan: edge points within 40 m of the sensor, seen in the LiDAR frame
-    near = np.linalg.norm(corner_map[:, :2] - t[:2], axis=1) < 40
-    cw = corner_map[near][::3]
-    cw = cw + rng.normal(0, 0.01, cw.shape)
-    corner_scan = ((cw - t) @ R).astype(np.float32)
-    return dict(surf_map=surf_map, corner_map=corner_map, surf_scan=fr.body, corner_scan=corner_scan, tf=tf)
+    return synth.make_s2m_problem()
 
 
 @pytest.mark.parametrize("kind", [0, 1])

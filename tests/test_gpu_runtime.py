@@ -322,6 +322,8 @@ def test_persistent_update_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
     runs reuse passes), D = 6 / 12, one pass and more passes than before.  The
     two paths alternate on one handle (pose slots, flags and certificates
     carry over between updates of either kind)."""
+    import gc
+    gc.collect()  # (a handle left to the collector would keep the device shared)
     mp, fr, _ = c2
     st = state_of(fr)
     body = np.ascontiguousarray(fr.body[:npts])
@@ -347,6 +349,62 @@ def test_persistent_update_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
             assert lib.slio_debug_update_path(h) == (0 if rep == 2 else 1)
             for a, b in zip(got, per):
                 np.testing.assert_array_equal(a, b)
+    finally:
+        persist(False)
+        lib.slio_destroy(h)
+
+
+def test_persistent_timeout_reported_and_recovers(L, c2, monkeypatch):
+    """The persistent update's workgroups wait between passes for the flag
+    the filter step publishes; a wait that gives up (forced through
+    slio_debug_wait_limit(h, 1): every workgroup gives up at its first wait)
+    ends the update with SLIO_ETIMEOUT -- not "did not complete", and never a
+    result -- and resets the handle's arrival counters and flag replicas, so
+    the next persistent update is bitwise equal to a launch per pass.  The
+    persistent path is refused while another handle lives on the device
+    (co-residency of its workgroups is then not guaranteed)."""
+    import gc
+    gc.collect()
+    mp, fr, _ = c2
+    st = state_of(fr)
+    lib = L.load()
+    h = mk(L, cell=C2_CELL)
+
+    def persist(on):
+        if on:
+            monkeypatch.setenv("SLIO_PERSIST", "1")
+        else:
+            monkeypatch.delenv("SLIO_PERSIST", raising=False)
+        lib.slio_debug_reload_switches(h)
+
+    try:
+        upload_map(L, h, mp)
+        assert upload_scan(L, h, fr.body) == 0
+        per = _update_once(L, h, st)
+        persist(True)
+        L.check(lib.slio_debug_wait_limit(h, 1), "wait limit")
+        xs = slio_state(st)
+        P = np.eye(24) * 1e-2
+        stt = L.SlioIkfStats()
+        rc = lib.slio_ikf_update_device(h, C.byref(xs), L.dptr(P), 0.001, 4, 0, 1, L.ALLREDUCE_FN(), None,
+                                        C.byref(stt))
+        assert lib.slio_debug_update_path(h) == 1, "another handle is alive on the device"
+        assert rc == L.SLIO_ETIMEOUT, (rc, lib.slio_last_error().decode())
+        L.check(lib.slio_debug_wait_limit(h, 0), "wait limit")
+        for _ in range(2):
+            got = _update_once(L, h, st)
+            assert lib.slio_debug_update_path(h) == 1
+            for a, b in zip(got, per):
+                np.testing.assert_array_equal(a, b)
+        # a second live handle on the device: a launch per pass
+        h2 = mk(L, cell=C2_CELL)
+        try:
+            got = _update_once(L, h, st)
+            assert lib.slio_debug_update_path(h) == 0
+            for a, b in zip(got, per):
+                np.testing.assert_array_equal(a, b)
+        finally:
+            lib.slio_destroy(h2)
     finally:
         persist(False)
         lib.slio_destroy(h)
