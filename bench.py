@@ -706,7 +706,7 @@ def bench_s2m(args, rank, world, dev, dist):
     s.close()
 
 
-def synth_t_li():def synth_t_li():
+def synth_t_li():
     from agi_lidar_slam_amd import synth
     return synth.AVIA_T_LI
 
