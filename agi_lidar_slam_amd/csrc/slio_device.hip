@@ -3949,6 +3949,11 @@ struct Ctx {
     bool no_kc = false;       // SLIO_NO_KNN_CERT: every pass searches in full
     bool persist = false;     // SLIO_PERSIST: one persistent launch per update (k_update_persist)
     bool no_steal = false;    // SLIO_NO_STEAL: the first pass refines every query in its own workgroup
+    // SLIO_LDS_PAD=<bytes>, SLIO_LDS_PAD_PASSES=<mask>: extra (unused) LDS per
+    // workgroup of the fused passes whose iteration bit is set -- an occupancy
+    // experiment (3 instead of 4 workgroups per CU)
+    int lds_pad = 0;
+    int lds_pad_mask = 0;
   } sw;
   // refinement work sharing of the fused first pass (RqItem): items, results,
   // per-chunk done counts, the last launch tag handed out
@@ -3989,6 +3994,12 @@ static void load_switches(Ctx& c) {
   c.sw.no_kc = env_on("SLIO_NO_KNN_CERT");
   c.sw.persist = env_on("SLIO_PERSIST");
   c.sw.no_steal = env_on("SLIO_NO_STEAL");
+  {
+    const char* e = std::getenv("SLIO_LDS_PAD");
+    c.sw.lds_pad = e ? std::max(0, std::min(65536, std::atoi(e))) : 0;
+    const char* m = std::getenv("SLIO_LDS_PAD_PASSES");
+    c.sw.lds_pad_mask = m ? std::atoi(m) : 0xff;
+  }
 }
 static inline int64_t mono_ns() {
   timespec ts;
@@ -4354,8 +4365,10 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
       // (D = 6, or 12 with extrinsic estimation) runs in this launch, no
       // k_super_sums; a later pass is a search or a reuse pass as the update
       // decides on the device
-#define SLIO_LAUNCH_FUSED(DEV, D)                                                                           \
-  hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, DEV, true, D>, nb, dim3(kSolveThreads), 0, \
+      const unsigned pad =
+          (c.sw.lds_pad > 0 && ((c.sw.lds_pad_mask >> (fuse->iter & 7)) & 1)) ? (unsigned)c.sw.lds_pad : 0u;
+#define SLIO_LAUNCH_FUSED(DEV, D)                                                                             \
+  hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, DEV, true, D>, nb, dim3(kSolveThreads), pad, \
                         c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse)
 #define SLIO_LAUNCH_PERSIST(D)                                                                    \
   hipExtLaunchKernelGGL(k_update_persist<SLIO_SEARCH_U, D>, nb, dim3(kSolveThreads), 0, c.stream, ev.first, \

@@ -41,6 +41,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def native_loop():
+    """scripts/bench_loop.c -- the C2 step loop as a compiled caller (what
+    laserMapping is) -- built next to its source if missing or older than it;
+    None when it cannot be built (bench.py then times the Python loop)."""
+    import subprocess
+    src = os.path.join(ROOT, "scripts", "bench_loop.c")
+    so = os.path.join(ROOT, "scripts", "libbench_loop.so")
+    try:
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"), src, "-o",
+                            so + ".tmp"], check=True, capture_output=True)
+            os.replace(so + ".tmp", so)
+        lib = C.CDLL(so)
+    except (OSError, subprocess.CalledProcessError) as e:
+        log(f"bench.py: no native caller loop ({e}); timing the Python loop")
+        return None
+    return lib.bench_c2_loop
+
+
 def l2_demand_bytes(mp: np.ndarray, body: np.ndarray, st0: np.ndarray, cell: float) -> float:
     """Estimated bytes one search launch asks of the L1/L2 (not HBM): per
     query the 2 block-row bounds (8 B), every candidate of its 3x3x3 block
@@ -793,6 +812,11 @@ def main():
     ap.add_argument("--timing-steps", type=int, default=40,
                     help="c2: steps after the timed region whose search launches carry HIP events "
                          "(roofline.avg_launch_us)")
+    ap.add_argument("--caller", choices=["native", "python"], default="native",
+                    help="c2: the timed step loop in C (scripts/bench_loop.c, the laserMapping-style "
+                         "caller) or in Python (ctypes per step)")
+    ap.add_argument("--no-python-reference", action="store_true",
+                    help="c2: skip timing the Python loop beside the native one")
     ap.add_argument("--host-loop", action="store_true",
                     help="run the 24x24 step on the host after every pass (slio_ikf_update)")
     ap.add_argument("--cache-dir", default=os.environ.get("SLIO_CACHE", "/tmp/slio_cache"))
@@ -948,20 +972,49 @@ def main():
             L.check(rc, "ikf")
         return xs
 
-    for _ in range(args.warmup):
-        step()
+    # the timed loop: the compiled caller (scripts/bench_loop.c) unless
+    # --caller python; each step copies the prior in and runs one update
+    loop = native_loop() if args.caller == "native" else None
+    if loop is not None:
+        loop.restype = C.c_int
+        loop.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(L.SlioState), C.POINTER(C.c_double), C.c_double,
+                         C.c_int, C.c_int, C.c_int, L.ALLREDUCE_FN, C.c_void_p, C.c_int64,
+                         C.POINTER(L.SlioState), C.POINTER(C.c_double), C.POINTER(L.SlioIkfStats)]
+        fn_addr = C.cast(fn, C.c_void_p)
+        P0_ptr = L.dptr(P0c)
+
+    def run(k):
+        if loop is None:
+            for _ in range(k):
+                step()
+            return
+        rc = loop(fn_addr, h, C.byref(xs0), P0_ptr, R_c, it_c, ext_c, mode_c, reduce_cb, None, k, xs_ref, P_ptr,
+                  st_ref)
+        if rc:
+            L.check(rc, "ikf")
+
+    run(args.warmup)
     lib.slio_profile(h, 0)  # reset totals
     search_bit = 1 << (L.SLIO_KERNEL_SEARCH + 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        xs = step()
+    run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # the same steps from the Python loop, for reference (not `value`)
+    py_el = None
+    if loop is not None and not args.no_python_reference:
+        npy = min(args.steps, 100)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(npy):
+            step()
+        torch.cuda.synchronize()
+        py_el = (time.perf_counter() - t1) / npy
     # the roofline's per-launch kernel time: HIP events in the dispatch
     # packets of every search launch of further steps of the same work, after
     # the timed region (events cost ~5 us of idle per launch, so they stay
@@ -1089,6 +1142,9 @@ def main():
             "parallelism": (f"scan points sharded x{world}, map replicated, one all-reduce of 8x91 fp64 "
                             f"per iteration: {comm}" if world > 1 else "single GPU"),
             "effective_points": int(stats.last_m),
+            "caller": ("native: scripts/bench_loop.c calls slio_ikf_update_device once per step, as "
+                       "laserMapping's C++ loop does" if loop is not None else "Python ctypes loop"),
+            "python_loop_value": (passes / py_el) if py_el else None,
         },
         "roofline": {
             "bound": "hbm",
