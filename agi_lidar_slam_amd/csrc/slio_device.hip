@@ -1264,24 +1264,6 @@ struct ScanDev {
   int64_t n;
 };
 
-// Refinement work sharing (the fused first pass, see search_pass_body): a
-// workgroup with more than kRqKeep refining queries hands the rest, four
-// queries to an item, to whichever wavefront of the launch takes them
-// (one wavefront, 16 lanes a query); the results go back to the owner.
-constexpr int kRqKeep = 16;
-struct alignas(16) RqItem {
-  float4 q[4];          // queries; .w: the refinement bound (lim)
-  uint64_t top[4][5];   // the owner's block lists
-  uint32_t owner;       // the owner's chunk
-  uint32_t n;           // queries in the item (1..4)
-  uint32_t tag;         // the launch's tag, stored after the rest (write-through, drained)
-  uint32_t pad;
-};
-struct alignas(16) RqRes {
-  uint64_t top[4][5];
-  uint32_t fin[4];      // 1: exact within the 5x5x5 cube, 0: to the owner's far queue
-};
-
 struct PassOut {
   int32_t* nbr_idx;  // n * 5  (map point ids)
   uint32_t* nbr_pos; // n * 5  (positions in the cell-sorted pts, for map_incremental)
@@ -1301,11 +1283,6 @@ struct PassOut {
   uint32_t* k6;         // the 6th of the certified set (nbr_pos holds the other 5)
   uint32_t* kepoch;     // per chunk (global index)
   uint32_t* kc_count;   // [0] certified queries, [1] queries searched with a certificate written
-  // refinement work sharing: items, results, per-chunk done counts (the queue's
-  // tail / head are far_ctr[6] / far_ctr[7], reset by the pass's final workgroup)
-  RqItem* rq_items;
-  RqRes* rq_res;
-  uint32_t* rq_done;
 };
 
 // far_query_margin: squared distance from the query to the grid's bounding box
@@ -1333,7 +1310,6 @@ struct PassCfg {
   const uint32_t* perm;    // block -> chunk order within each XCD's range (chunk_order), or null
   uint32_t kc_epoch;       // kNN certificates of this update (0: off); see k_search_pass
   int32_t seq;             // fused group pass: run only if ctl->seq == seq (0: no check)
-  uint32_t rq_tag;         // refinement work sharing in this launch (0: off), see RqItem
 };
 
 // ---------------------------------------------------------------- far queries
@@ -1600,12 +1576,6 @@ __device__ __forceinline__ double ld_sys(const double* p) {
 }
 __device__ __forceinline__ uint32_t ld_sys_u32(const uint32_t* p) {
   return __hip_atomic_load((const guint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sc1_u64(uint64_t* p, uint64_t v) {
-  __hip_atomic_store((guint64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
-  return __hip_atomic_load((const guint64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t arrive(uint32_t* p) {
   return __hip_atomic_fetch_add((guint*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2614,10 +2584,6 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     st_sc1_u32(fa.cnt + 6, ld_sc1_u32(fa.cnt + 5));
     st_sc1_u32(fa.cnt + 4, 0u);
     st_sc1_u32(fa.cnt + 5, 0u);
-    // the refinement work-sharing queue's tail and head (every workgroup of
-    // the pass has arrived: none takes or hands out items any more)
-    st_sc1_u32(fa.cnt + 10, 0u);
-    st_sc1_u32(fa.cnt + 11, 0u);
   }
   if (!fa.gsup) {
     final_step<NT, D, true, false, WT>(L, fa.seg_out, fa.super_out, ctl, fa.src, fa.hblk, fa.R, iter, fa.maxit);
@@ -2712,8 +2678,6 @@ struct SearchLds {
   uint8_t ksame[SLIO_CHUNK];        // KC: certified in the last pass's order (plane reusable)
   // deferred (far) queries of this chunk and the far workers' scratch
   int far_cnt, ref_cnt;
-  uint32_t rq_base;  // refinement work sharing: this chunk's first item
-  int rq_fail;       // a work-sharing wait gave up
   uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
   uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
   int32_t tab_dl[NT / 16][kTab];
@@ -3088,54 +3052,7 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
     // refinements used to run on that wavefront alone, 8 per round with a
     // per-lane share of the runs, ~10 us a round, so one wave with 30
     // refining queries set the kernel's end.
-    // Work sharing (the fused first pass): the chunk keeps its first kRqKeep
-    // refining queries and hands the rest, four to an item, to the launch's
-    // queue; every wavefront, once its own workgroup's refinements are done,
-    // takes items while any is unclaimed (16 lanes a query); the owner then
-    // waits for its items' results.  The few workgroups whose chunk lies where
-    // the prior pose puts many queries off the map (pass 0: up to 62 refining
-    // queries in one chunk, 20 us of refinement, the launch's end) no longer
-    // refine alone.  Exact either way: a refinement's result does not depend
-    // on who computes it.
-    constexpr bool STEAL = FUSE && !DEVPOSE && !PERS && LPQ == 2 && !SPHERE;
-    const bool steal = STEAL && cfg.rq_tag != 0;
-    const int nref_all = ref_cnt;
-    int nitems = 0;
-    if constexpr (STEAL) {
-      if (steal && nref_all > kRqKeep) {
-        nitems = (nref_all - kRqKeep + 3) / 4;
-        if (tid == 0) {
-          lds.s.rq_base = __hip_atomic_fetch_add((guint*)(out.far_ctr + 6), (uint32_t)nitems, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-          lds.s.rq_fail = 0;
-        }
-        __syncthreads();
-        const uint32_t base = lds.s.rq_base;
-        for (int e = tid; e < nitems * 4; e += NT) {
-          const int it = e >> 2, j = e & 3, k = kRqKeep + e;
-          RqItem* I = out.rq_items + base + it;
-          if (k < nref_all) {
-            const float4 q = ref.q[k];
-            uint32_t* qd = reinterpret_cast<uint32_t*>(&I->q[j]);
-            st_sc1_u32(qd + 0, __float_as_uint(q.x));
-            st_sc1_u32(qd + 1, __float_as_uint(q.y));
-            st_sc1_u32(qd + 2, __float_as_uint(q.z));
-            st_sc1_u32(qd + 3, __float_as_uint(q.w));
-#pragma unroll
-            for (int m = 0; m < 5; ++m) st_sc1_u64(&I->top[j][m], ref.top[k][m]);
-          }
-          if (j == 0) {
-            st_sc1_u32(&I->owner, (uint32_t)chunk);
-            st_sc1_u32(&I->n, (uint32_t)min(4, nref_all - (kRqKeep + 4 * it)));
-          }
-        }
-        // every item's contents stored (write-through) before any tag
-        drain_stores();
-        __syncthreads();
-        for (int it = tid; it < nitems; it += NT) st_sc1_u32(&out.rq_items[base + it].tag, cfg.rq_tag);
-      }
-    }
-    const int nref = nitems > 0 ? kRqKeep : nref_all;  // refined in this workgroup
+    const int nref = ref_cnt;
     WSTAMP(0, __builtin_amdgcn_s_memrealtime());
     auto refine_all = [&](auto rl) {
       constexpr int RL = decltype(rl)::value;
@@ -3213,148 +3130,6 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
       else
         refine_all(std::integral_constant<int, 2>{});
       __syncthreads();
-    }
-    if constexpr (STEAL) {
-      if (steal) {
-        const int lane = tid & 63, w = tid >> 6;
-        uint32_t* const rq_tail = out.far_ctr + 6;
-        uint32_t* const rq_head = out.far_ctr + 7;
-        const unsigned long long lim = fa.wait_ticks > 1 ? fa.wait_ticks : 100000000ull;  // 100 MHz: 1 s
-        auto give_up = [&]() {
-          if (fa.hblk) __hip_atomic_store(&fa.hblk->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          lds.s.rq_fail = 1;
-        };
-        // one unclaimed item for this wavefront (lane 0 claims; ~0u: none)
-        auto claim = [&]() -> uint32_t {
-          uint32_t h = ~0u;
-          if (lane == 0) {
-            for (;;) {
-              uint32_t hd = ld_sc1_u32(rq_head);
-              const uint32_t tl = ld_sc1_u32(rq_tail);
-              if (hd >= tl) break;
-              if (__hip_atomic_compare_exchange_strong((guint*)rq_head, &hd, hd + 1, __ATOMIC_RELAXED,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                h = hd;
-                break;
-              }
-            }
-          }
-          return __builtin_amdgcn_readfirstlane(h);
-        };
-        // one item's refinements on this wavefront, 16 lanes a query (the
-        // RL = 16 refinement of refine_all); results to the item's slot, then
-        // the owner's done count
-        auto process = [&](uint32_t h) {
-          const RqItem* I = out.rq_items + h;
-          uint32_t ok = 1;
-          if (lane == 0) {
-            // the owner stores the tag after the contents
-            const unsigned long long t0 = wall_clock64();
-            while (ld_sc1_u32(&I->tag) != cfg.rq_tag) {
-              if (wall_clock64() - t0 > lim) {
-                give_up();
-                ok = 0;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-            }
-          }
-          if (!__builtin_amdgcn_readfirstlane(ok)) return;
-          const uint32_t n = ld_sc1_u32(&I->n), owner = ld_sc1_u32(&I->owner);
-          const int j = lane >> 4, rsub = lane & 15;
-          const bool has = (uint32_t)j < n;
-          float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          if (has) {
-            const uint32_t* qd = reinterpret_cast<const uint32_t*>(&I->q[j]);
-            q = make_float4(__uint_as_float(ld_sc1_u32(qd)), __uint_as_float(ld_sc1_u32(qd + 1)),
-                            __uint_as_float(ld_sc1_u32(qd + 2)), __uint_as_float(ld_sc1_u32(qd + 3)));
-          }
-          int rx = 0, ry = 0, rz = 0;
-          uint64_t runs = 0;
-          if (has) {
-            rx = cell_coord(q.x, g.ox, g.inv_h);
-            ry = cell_coord(q.y, g.oy, g.inv_h);
-            rz = cell_coord(q.z, g.oz, g.inv_h);
-          }
-          const RunCtx rq{rx, ry, rz, q.x, q.y, q.z, 2, 0.0f, q.w};
-          if (has) {
-            const uint64_t rows = sphere_rows(g, rq, rq.lim);
-            runs = rows | ((rows & 0x739c0ull) << 32);
-          }
-          Top5 tr;
-          top5_clear(tr);
-          scan_runs_wide<16, U>(pts, start, g, rq, runs, rsub, tab_pre[w * 4 + j], tab_dl[w * 4 + j], tr);
-          group_merge_rolled(tr, 16);
-          if (has && rsub == 0) {
-#pragma unroll
-            for (int m = 0; m < 5; ++m) top5_insert(tr, ld_sc1_u64(&I->top[j][m]));
-            bool cov2;
-            const float b2 = outside_bound(g, rx, ry, rz, 2, q.x, q.y, q.z, cov2);
-            const float d5n = __uint_as_float((uint32_t)(tr.k[4] >> 32));
-            const bool fin = cov2 || (tr.k[4] != kInfKey && b2 > 0.0f && d5n < (b2 * b2) * 0.99999f);
-            RqRes* R = out.rq_res + h;
-#pragma unroll
-            for (int m = 0; m < 5; ++m) st_sc1_u64(&R->top[j][m], tr.k[m]);
-            st_sc1_u32(&R->fin[j], fin ? 1u : 0u);
-          }
-          drain_stores();  // (the wavefront's stores: s_waitcnt is per wavefront)
-          if (lane == 0)
-            __hip_atomic_fetch_add((guint*)(out.rq_done + owner), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        for (uint32_t h = claim(); h != ~0u; h = claim()) process(h);
-        if (nitems > 0) {
-          // the owner: wait for its items' results, taking any item still unclaimed
-          const unsigned long long t0 = wall_clock64();
-          for (;;) {
-            uint32_t d = 0;
-            if (lane == 0) d = ld_sc1_u32(out.rq_done + chunk);
-            if (__builtin_amdgcn_readfirstlane(d) >= (uint32_t)nitems) break;
-            const uint32_t h = claim();
-            if (h != ~0u) {
-              process(h);
-              continue;
-            }
-            uint32_t late = 0;
-            if (lane == 0 && wall_clock64() - t0 > lim) {
-              give_up();
-              late = 1;
-            }
-            if (__builtin_amdgcn_readfirstlane(late)) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-        __syncthreads();
-        if (nitems > 0) {
-          // the results into the chunk's neighbour lists (or its far queue)
-          const uint32_t base = lds.s.rq_base;
-          for (int e = tid; e < nref_all - kRqKeep; e += NT) {
-            const int it = e >> 2, j = e & 3, k = kRqKeep + e;
-            const RqRes* R = out.rq_res + base + it;
-            uint64_t tk[5];
-#pragma unroll
-            for (int m = 0; m < 5; ++m) tk[m] = ld_sc1_u64(&R->top[j][m]);
-            const bool fin = ld_sc1_u32(&R->fin[j]) != 0;
-            const int slot = ref.slot[k];
-            const float4 q = ref.q[k];
-            const float d5n = __uint_as_float((uint32_t)(tk[4] >> 32));
-            if (fin) {
-#pragma unroll
-              for (int m = 0; m < 5; ++m) {
-                const uint64_t mk = tk[m];
-                nb_sqd[slot][m] = (mk == kInfKey) ? __int_as_float(0x7f800000) : __uint_as_float((uint32_t)(mk >> 32));
-                nb_pos[slot][m] = (mk == kInfKey) ? 0xFFFFFFFFu : (uint32_t)mk;
-              }
-              nb_d5[slot] = (tk[4] != kInfKey) ? d5n : __int_as_float(0x7f800000);
-            } else {
-              const int f = atomicAdd(&far_cnt, 1);
-              far_slot[f] = (uint8_t)slot;
-              far_q[f] = make_float4(q.x, q.y, q.z, tk[4] != kInfKey ? d5n : __int_as_float(0x7f800000));
-            }
-          }
-          if (tid == 0 && !lds.s.rq_fail) st_sc1_u32(out.rq_done + chunk, 0u);
-          __syncthreads();
-        }
-      }
     }
     WSTAMP(1, __builtin_amdgcn_s_memrealtime());
   }
@@ -3948,19 +3723,12 @@ struct Ctx {
     bool event_wait = false;  // SLIO_EVENT_WAIT: wait on a completion event
     bool no_kc = false;       // SLIO_NO_KNN_CERT: every pass searches in full
     bool persist = false;     // SLIO_PERSIST: one persistent launch per update (k_update_persist)
-    bool no_steal = false;    // SLIO_NO_STEAL: the first pass refines every query in its own workgroup
     // SLIO_LDS_PAD=<bytes>, SLIO_LDS_PAD_PASSES=<mask>: extra (unused) LDS per
     // workgroup of the fused passes whose iteration bit is set -- an occupancy
     // experiment (3 instead of 4 workgroups per CU)
     int lds_pad = 0;
     int lds_pad_mask = 0;
   } sw;
-  // refinement work sharing of the fused first pass (RqItem): items, results,
-  // per-chunk done counts, the last launch tag handed out
-  RqItem* rq_items = nullptr;
-  RqRes* rq_res = nullptr;
-  uint32_t* rq_done = nullptr;
-  uint32_t rq_next = 0;
   // persistent update (k_update_persist): the flag replicas, the CU count and
   // the workgroups the device holds at once (-1: not yet queried)
   uint64_t* goflag = nullptr;
@@ -3993,7 +3761,6 @@ static void load_switches(Ctx& c) {
   c.sw.event_wait = env_on("SLIO_EVENT_WAIT");
   c.sw.no_kc = env_on("SLIO_NO_KNN_CERT");
   c.sw.persist = env_on("SLIO_PERSIST");
-  c.sw.no_steal = env_on("SLIO_NO_STEAL");
   {
     const char* e = std::getenv("SLIO_LDS_PAD");
     c.sw.lds_pad = e ? std::max(0, std::min(65536, std::atoi(e))) : 0;
@@ -4154,12 +3921,6 @@ static void free_scan(Ctx* c) {
   (void)hipFree(c->kq);
   (void)hipFree(c->k6);
   (void)hipFree(c->kepoch);
-  (void)hipFree(c->rq_items);
-  (void)hipFree(c->rq_res);
-  (void)hipFree(c->rq_done);
-  c->rq_items = nullptr;
-  c->rq_res = nullptr;
-  c->rq_done = nullptr;
   c->kq = nullptr;
   c->k6 = nullptr;
   c->kepoch = nullptr;
@@ -4230,7 +3991,6 @@ static void reset_update_counters(Ctx& c) {
   if (c.count) (void)hipMemsetAsync(c.count, 0, sizeof(uint32_t) * kCountWords, c.stream);
   if (c.goflag) (void)hipMemsetAsync(c.goflag, 0, sizeof(uint64_t) * 8 * kGoFlagStride, c.stream);
   if (c.garrive) (void)hipMemsetAsync(c.garrive, 0, 4 * sizeof(uint32_t), c.stream);
-  if (c.rq_done) (void)hipMemsetAsync(c.rq_done, 0, 4 * (num_chunks(c.prm.max_points) + 1), c.stream);
   (void)hipStreamSynchronize(c.stream);
   (void)hipGetLastError();
 }
@@ -4314,17 +4074,9 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
   if (!devpose) c.kc_version = c.map->version;
   cfg.kc_epoch = ((devpose || persist) && c.kq && c.map->version == c.kc_version) ? c.kc_epoch : 0;
   cfg.seq = fuse ? c.group_seq : 0;
-  // refinement work sharing: the fused first pass (its final workgroup resets
-  // the queue); a fresh tag per launch, so no item of an earlier launch is taken
-  cfg.rq_tag = 0;
-  if (fuse && !devpose && persist == 0 && !knn_only && c.rq_items && !c.sw.no_steal) {
-    if (++c.rq_next == 0) c.rq_next = 1;
-    cfg.rq_tag = c.rq_next;
-  }
   PassOut o{c.nbr_idx,    c.nbr_pos,    c.nbr_sqd,   c.plane,  c.sel,    c.resid,
             c.chunk_part, c.count + 4, c.nbr_pose, c.chunk_cost, c.kq, c.k6,
-            c.kepoch,     c.kc_stats ? c.count + kKcCount : nullptr,
-            c.rq_items,   c.rq_res,    c.rq_done};
+            c.kepoch,     c.kc_stats ? c.count + kKcCount : nullptr};
   ScanDev s = sd ? *sd : ScanDev{c.bx, c.by, c.bz, c.n};
   const PoseDev P = Parg ? *Parg : PoseDev{};
   const int64_t nblk = c1 - c0;
@@ -5092,13 +4844,7 @@ static int ensure_scan_buffers(Ctx& c) {
         (e = hipMalloc(&c.chunk_part, 8 * SLIO_NPROD * capc)) ||
         (e = hipMalloc(&c.chunk_cost, 4 * capc)) || (e = hipMalloc(&c.chunk_perm, 4 * capc)) ||
         (e = hipMalloc(&c.kq, 16 * cap)) || (e = hipMalloc(&c.k6, 4 * cap)) ||
-        (e = hipMalloc(&c.kepoch, 4 * capc)) || (e = hipMemset(c.kepoch, 0, 4 * capc)) ||
-        // (a chunk's items: its refining queries past kRqKeep, four to an item,
-        // at most one part-filled: cap / 4 + capc items for any pass)
-        (e = hipMalloc(&c.rq_items, sizeof(RqItem) * (cap / 4 + capc))) ||
-        (e = hipMemset(c.rq_items, 0, sizeof(RqItem) * (cap / 4 + capc))) ||
-        (e = hipMalloc(&c.rq_res, sizeof(RqRes) * (cap / 4 + capc))) ||
-        (e = hipMalloc(&c.rq_done, 4 * capc)) || (e = hipMemset(c.rq_done, 0, 4 * capc))) {
+        (e = hipMalloc(&c.kepoch, 4 * capc)) || (e = hipMemset(c.kepoch, 0, 4 * capc))) {
       free_scan(&c);
       set_error(std::string("slio scan buffers: hipMalloc: ") + hipGetErrorString(e));
       return SLIO_ENOMEM;
