@@ -13,6 +13,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "libslio_oracle.so")
+# scripts/sanitize.sh: the same sources built with ASan + UBSan
+SAN_LIB = os.environ.get("SLIO_ORACLE_LIB")
 
 _FP = C.POINTER(C.c_float)
 _DP = C.POINTER(C.c_double)
@@ -33,8 +35,11 @@ def build() -> str:
 def load() -> C.CDLL:
     global _lib
     if _lib is None:
-        build()
-        lib = C.CDLL(LIB)
+        if SAN_LIB:
+            lib = C.CDLL(SAN_LIB)
+        else:
+            build()
+            lib = C.CDLL(LIB)
         lib.orc_tree_build.restype = C.c_void_p
         lib.orc_tree_build.argtypes = [_FP, _FP, _FP, C.c_int64]
         lib.orc_tree_free.argtypes = [C.c_void_p]

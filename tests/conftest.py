@@ -10,6 +10,13 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    # scripts/sanitize.sh: the product's host C++ built with ASan + UBSan (the
+    # same sources and build id; bound before any test loads the library)
+    san = os.environ.get("SLIO_SANITIZE_LIB")
+    if san:
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        from variant import use
+        use(san)
 
 
 @pytest.fixture(scope="session")
