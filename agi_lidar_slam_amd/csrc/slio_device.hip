@@ -1312,6 +1312,11 @@ struct PassCfg {
   int32_t seq;             // fused group pass: run only if ctl->seq == seq (0: no check)
 };
 
+// The plane output's .x bits when esti_plane rejected the point's 5 neighbours
+// (a quiet NaN: the output reads as NaN, as the oracle's, and a certified pass
+// whose 5 keep their order reuses the rejection without the QR)
+constexpr uint32_t kPlaneRejected = 0x7fc00e57u;
+
 // ---------------------------------------------------------------- far queries
 // A query the fine grid cannot finish (its 5th neighbour lies beyond the
 // 5x5x5 fine cube, or its cell lies outside the grid) is DEFERRED to the end
@@ -3183,20 +3188,24 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
       const float4 qb = lds.s.qb[slot];
       const float bx = qb.x, by = qb.y, bz = qb.z;
       // KC: certified with the last pass's 5 in the same order -- the same
-      // esti_plane input, so its plane (when it had one) is reused
-      bool rp = false;
+      // esti_plane input, so its result is reused: the plane when it had one,
+      // and its rejection (the kPlaneRejected NaN the fit stores when
+      // esti_plane returns false: 9 % of C2's points, in 82 % of the fit's
+      // wavefronts, which all used to rerun the QR in every certified pass)
+      bool rp = false, rf = false;
       float4 cpl = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       if constexpr (KC) {
         if (lds.s.ksame[slot]) {
           cpl = lds.s.qpl[slot];
           rp = isfinite(cpl.x) && isfinite(cpl.y) && isfinite(cpl.z) && isfinite(cpl.w);
+          rf = __float_as_uint(cpl.x) == kPlaneRejected;
         }
       }
       // the 5 neighbours: coordinates for the fit, map index for
       // Nearest_Points (-1 when the map has fewer than 5 points)
       float nb[5][3];
 #pragma unroll
-      for (int j = 0; j < 5 && !rp; ++j) {
+      for (int j = 0; j < 5 && !rp && !rf; ++j) {
         const uint32_t ps = nb_pos[slot][j];
         float4 c = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
 #ifdef SLIO_BOUNDS_CHECK
@@ -3220,6 +3229,9 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
         abcd[2] = cpl.z;
         abcd[3] = cpl.w;
         sel = residual_gate(abcd, q.x, q.y, q.z, bx, by, bz, pd2);
+      } else if (sel && rf) {
+        sel = false;
+        abcd[0] = __uint_as_float(kPlaneRejected);
       } else if (sel) {
         float pl[4];
         sel = esti_plane_dev(nb, cfg.plane_thr, pl);
@@ -3227,6 +3239,8 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
 #pragma unroll
           for (int j = 0; j < 4; ++j) abcd[j] = pl[j];
           sel = residual_gate(abcd, q.x, q.y, q.z, bx, by, bz, pd2);
+        } else {
+          abcd[0] = __uint_as_float(kPlaneRejected);  // (a NaN: the plane output stays NaN)
         }
       }
       FSTAMP(2, false);
@@ -3723,11 +3737,6 @@ struct Ctx {
     bool event_wait = false;  // SLIO_EVENT_WAIT: wait on a completion event
     bool no_kc = false;       // SLIO_NO_KNN_CERT: every pass searches in full
     bool persist = false;     // SLIO_PERSIST: one persistent launch per update (k_update_persist)
-    // SLIO_LDS_PAD=<bytes>, SLIO_LDS_PAD_PASSES=<mask>: extra (unused) LDS per
-    // workgroup of the fused passes whose iteration bit is set -- an occupancy
-    // experiment (3 instead of 4 workgroups per CU)
-    int lds_pad = 0;
-    int lds_pad_mask = 0;
   } sw;
   // persistent update (k_update_persist): the flag replicas, the CU count and
   // the workgroups the device holds at once (-1: not yet queried)
@@ -3761,12 +3770,6 @@ static void load_switches(Ctx& c) {
   c.sw.event_wait = env_on("SLIO_EVENT_WAIT");
   c.sw.no_kc = env_on("SLIO_NO_KNN_CERT");
   c.sw.persist = env_on("SLIO_PERSIST");
-  {
-    const char* e = std::getenv("SLIO_LDS_PAD");
-    c.sw.lds_pad = e ? std::max(0, std::min(65536, std::atoi(e))) : 0;
-    const char* m = std::getenv("SLIO_LDS_PAD_PASSES");
-    c.sw.lds_pad_mask = m ? std::atoi(m) : 0xff;
-  }
 }
 static inline int64_t mono_ns() {
   timespec ts;
@@ -4117,10 +4120,8 @@ static int enqueue_pass(Ctx& c, const PoseDev* Parg, IkfCtl* ctl, int which,
       // (D = 6, or 12 with extrinsic estimation) runs in this launch, no
       // k_super_sums; a later pass is a search or a reuse pass as the update
       // decides on the device
-      const unsigned pad =
-          (c.sw.lds_pad > 0 && ((c.sw.lds_pad_mask >> (fuse->iter & 7)) & 1)) ? (unsigned)c.sw.lds_pad : 0u;
-#define SLIO_LAUNCH_FUSED(DEV, D)                                                                             \
-  hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, DEV, true, D>, nb, dim3(kSolveThreads), pad, \
+#define SLIO_LAUNCH_FUSED(DEV, D)                                                                           \
+  hipExtLaunchKernelGGL(k_search_pass<2, SLIO_SEARCH_U, false, DEV, true, D>, nb, dim3(kSolveThreads), 0, \
                         c.stream, ev.first, ev.second, 0, mv, s, P, cfg, o, *fuse)
 #define SLIO_LAUNCH_PERSIST(D)                                                                    \
   hipExtLaunchKernelGGL(k_update_persist<SLIO_SEARCH_U, D>, nb, dim3(kSolveThreads), 0, c.stream, ev.first, \
