@@ -993,9 +993,28 @@ def main():
         if rc:
             L.check(rc, "ikf")
 
-    run(args.warmup)
-    lib.slio_profile(h, 0)  # reset totals
+    # the roofline's per-launch kernel time first: HIP events in the dispatch
+    # packets of every search launch of --timing-steps steps of the same work
+    # (events cost ~5 us of idle per launch, so they stay out of the steps
+    # `value` is measured on).  Run BEFORE the warmup, they also bring the GPU
+    # out of idle: the driver's short setting (--steps 20 --warmup 5) read
+    # ~3 % low from clock ramp-up alone when they ran after the timed region.
     search_bit = 1 << (L.SLIO_KERNEL_SEARCH + 1)
+    ms = C.c_double()
+    nl = C.c_int64()
+    lib.slio_profile(h, 0)  # reset totals
+    if not args.no_kernel_timing:
+        # (a fresh map index gets its block rows after 8 unchanged search
+        # passes, kBlkAfterPasses: those updates stay out of the timing)
+        for _ in range(3):
+            step()
+        lib.slio_profile(h, search_bit)
+        for k in range(max(1, args.timing_steps)):
+            step()
+        lib.slio_profile(h, search_bit | L.SLIO_PROFILE_KEEP)
+        lib.slio_profile_read(h, L.SLIO_KERNEL_SEARCH, C.byref(ms), C.byref(nl))
+    lib.slio_profile(h, 0)
+    run(args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1015,19 +1034,6 @@ def main():
             step()
         torch.cuda.synchronize()
         py_el = (time.perf_counter() - t1) / npy
-    # the roofline's per-launch kernel time: HIP events in the dispatch
-    # packets of every search launch of further steps of the same work, after
-    # the timed region (events cost ~5 us of idle per launch, so they stay
-    # out of the steps `value` is measured on)
-    ms = C.c_double()
-    nl = C.c_int64()
-    if not args.no_kernel_timing:
-        lib.slio_profile(h, search_bit)
-        for k in range(max(1, args.timing_steps)):
-            step()
-        lib.slio_profile(h, search_bit | L.SLIO_PROFILE_KEEP)
-    lib.slio_profile_read(h, L.SLIO_KERNEL_SEARCH, C.byref(ms), C.byref(nl))
-    lib.slio_profile(h, 0)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1164,7 +1170,7 @@ def main():
             "avg_launch_us": avg_kernel_s * 1e6,
             "launches": int(nl.value),
             "timing": (f"HIP events in the dispatch packet of every search launch of {args.timing_steps} "
-                       "further steps after the timed region"),
+                       "steps of the same work before the warmup and the timed region"),
         },
         "roofline_l2": l2,
         "cpu_baseline": cpu,
