@@ -2611,7 +2611,12 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
     // the group's buffer, write-through and drained, then one arrival on the
     // group's counter; the rank that arrives last runs the filter step on
     // the 8 super rows (the same sums, the same bits as one rank) for the
-    // whole group: the ranks' next passes read the group's control block
+    // whole group: the ranks' next passes read the group's control block.
+    // No arrival word (garrive null): a rank of an all-reduce group
+    // (slio_comm_init, a reduce hook, RCCL or the in-device reduce of
+    // slio_create_group) -- its super rows and zeros in the other ranks'
+    // rows, as k_super_sums leaves them, for the all-reduce and k_ikf_solve
+    // that follow the launch.
     const int nsup = SLIO_NSUPER / fa.granks;
     if (t < SLIO_NPROD) {
       for (int k = 0; k < nsup; ++k) {
@@ -2621,7 +2626,11 @@ __device__ __forceinline__ void fused_tail(StepLds& L, int& bcast, const FuseArg
         for (int q = 1; q < kSuperSeg; ++q) a = a + ld_sc1(fa.seg_out + (ss * kSuperSeg + q) * SLIO_NPROD + t);
         st_sc1(fa.gsup + ss * SLIO_NPROD + t, a);
       }
+      if (!fa.garrive)
+        for (int ss = 0; ss < SLIO_NSUPER; ++ss)
+          if (ss < fa.s0 || ss >= fa.s0 + nsup) st_sc1(fa.gsup + ss * SLIO_NPROD + t, 0.0);
     }
+    if (!fa.garrive) return;
     drain_stores();
     __syncthreads();
     if (t == 0) bcast = (int)arrive(fa.garrive);
@@ -7512,6 +7521,27 @@ struct UpdateRun {
       SLIO_HIP(hipGetLastError());
       return SLIO_OK;
     }
+    if (fused_rows() && !(p0 && c.sw.no_fuse0)) {
+      const int nr = c.prm.nranks;
+      const FuseArgs fa{c.ctl,   nullptr,
+                        c.d_seg, c.d_super,
+                        c.ctl,   c.d_hctl,
+                        c.count, R,
+                        i,       maxit,
+                        num_chunks(c.n), kNSeg / nr,
+                        c.prm.rank * (SLIO_NSUPER / nr), nr,
+                        c.d_super, nullptr,
+                        0};
+      if (p0) fill_block();
+      if (p0 && !info_constants(P, dim, c.h_ctl->P11i, c.h_ctl->G)) {
+        set_error("slio_ikf_update_device: singular covariance block P[:D, :D]");
+        return SLIO_EINVAL;
+      }
+      int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, true, false, nullptr, &fa);
+      if (rc) return rc;
+      SLIO_HIP(hipGetLastError());
+      return SLIO_OK;
+    }
     int rc = enqueue_pass(c, p0 ? &pose0 : nullptr, c.ctl, which, ext, &sa, !p0 || multi);
     if (rc) return rc;
     if (p0) {
@@ -7550,6 +7580,10 @@ struct UpdateRun {
            (lpq != 1 && lpq != 4 && lpq != 8) && !(c.prm.search_radius > 0.0f) &&
            num_chunks(c.n) >= (int64_t)kNSeg;
   }
+  // a rank of an all-reduce group: its pass, segment rows and super rows in
+  // one launch (the rows-only fused tail), then the all-reduce and
+  // k_ikf_solve -- no k_super_sums launch between the pass and the collective
+  bool fused_rows() const { return multi && fused_ok() && (SLIO_NSUPER % c.prm.nranks) == 0; }
 
   // The whole update as one persistent launch (k_update_persist): the fused
   // configuration, and every chunk's workgroup resident at once (the
