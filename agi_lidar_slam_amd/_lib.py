@@ -25,6 +25,7 @@ SLIO_KERNEL_REUSE = 1
 SLIO_KERNEL_SUPER = 2
 SLIO_PROFILE_KEEP = 16
 SLIO_LIO_PROFILE_KEEP = 16
+SLIO_LIO_PROFILE_SCAN = 32
 
 ERRORS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ECAPACITY", -5: "ESTATE", -6: "ETIMEOUT"}
 SLIO_ETIMEOUT = -6

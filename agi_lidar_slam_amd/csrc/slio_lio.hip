@@ -1714,6 +1714,7 @@ struct slio_lio {
   bool ran = false;
   // feature-stage timing
   bool prof = false;
+  bool prof_scan = false;  // SLIO_LIO_PROFILE_SCAN: the events span the whole scan
   double prof_ms = 0.0;
   int64_t prof_n = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
@@ -1964,15 +1965,6 @@ int slio_lio_run_async(slio_lio_handle h) {
   const uint32_t hi = ~(++h->gen);
   const In in{h->x, h->y, h->z, h->in, h->ring, h->time, h->n};
   const int nclaim = (int)((h->n + 255) / 256);
-  if (h->n > 0)
-    k_lio_claim<<<nclaim, 256, 0, h->stream>>>(in, g, h->owner, hi, h->block_first);
-  const Deskew d{h->it, h->rx, h->ry, h->rz, h->n_imu - 1, h->t0, h->deskew, h->imu_sorted};
-  k_lio_fill<<<dim3(R, kFillSplit), kFillThreads, 0, h->stream>>>(
-      in, g, h->owner, hi, h->block_first, nclaim, d, h->range_mat, h->full, h->row_count);
-  const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->prange, h->xyzi, h->n_ext};
-  k_lio_extract<<<R, kRowThreads, 0, h->stream>>>(g, h->range_mat, h->full, h->row_count, ci);
-  const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
-                   nullptr, nullptr, nullptr, nullptr, nullptr};
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (h->prof) {
     if (h->pending.size() > 256) lio_prof_drain(h);
@@ -1985,8 +1977,24 @@ int slio_lio_run_async(slio_lio_handle h) {
     }
     h->pending.push_back(ev);
   }
-  launch_features<kModeLio>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw, ev);
-  k_lio_concat<<<R, kConcatThreads, 0, h->stream>>>(R, h->start_ring, fo, h->corner, h->surface, h->counts);
+  // the events: in the first and last launches' dispatch packets (the whole
+  // scan), or around the feature stage
+  const hipEvent_t e0 = h->prof_scan ? ev.first : nullptr, e1 = h->prof_scan ? ev.second : nullptr;
+  if (h->n > 0)
+    hipExtLaunchKernelGGL(k_lio_claim, dim3(nclaim), dim3(256), 0, h->stream, e0, nullptr, 0, in, g, h->owner, hi,
+                          h->block_first);
+  const Deskew d{h->it, h->rx, h->ry, h->rz, h->n_imu - 1, h->t0, h->deskew, h->imu_sorted};
+  hipExtLaunchKernelGGL(k_lio_fill, dim3(R, kFillSplit), dim3(kFillThreads), 0, h->stream,
+                        h->n > 0 ? nullptr : e0, nullptr, 0, in, g, h->owner, hi, h->block_first, nclaim, d,
+                        h->range_mat, h->full, h->row_count);
+  const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->prange, h->xyzi, h->n_ext};
+  k_lio_extract<<<R, kRowThreads, 0, h->stream>>>(g, h->range_mat, h->full, h->row_count, ci);
+  const FeatOut fo{h->label, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
+                   nullptr, nullptr, nullptr, nullptr, nullptr};
+  launch_features<kModeLio>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw,
+                            h->prof_scan ? std::pair<hipEvent_t, hipEvent_t>{nullptr, nullptr} : ev);
+  hipExtLaunchKernelGGL(k_lio_concat, dim3(R), dim3(kConcatThreads), 0, h->stream, nullptr, e1, 0, R,
+                        h->start_ring, fo, h->corner, h->surface, h->counts);
   LIO_HIP(hipGetLastError());
   h->ran = true;
   return SLIO_OK;
@@ -1996,6 +2004,7 @@ int slio_lio_profile(slio_lio_handle h, int enable) {
   LIO_CHECK_H(h);
   const bool keep = (enable & SLIO_LIO_PROFILE_KEEP) != 0;
   h->prof = (enable & ~SLIO_LIO_PROFILE_KEEP) != 0;
+  h->prof_scan = (enable & SLIO_LIO_PROFILE_SCAN) != 0;
   if (!keep) {  // pausing / resuming never waits; a reset drains first
     lio_prof_drain(h);
     h->prof_ms = 0.0;
@@ -3445,6 +3454,7 @@ struct slio_lego {
   FeatWork fw{};
   bool ran = false;
   bool prof = false;
+  bool prof_scan = false;  // SLIO_LIO_PROFILE_SCAN: the events span the whole scan
   double prof_ms = 0.0;
   int64_t prof_n = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
@@ -3802,9 +3812,26 @@ int slio_lego_run_async(slio_lego_handle h) {
     if (!e) e = hipMemsetAsync(h->rows, 0, 16 * g.cells, h->stream);
     if (e) return fail(e);
   }
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (h->prof) {
+    if (h->pending.size() > 256) lego_prof_drain(h);
+    if (!h->pool.empty()) {
+      ev = h->pool.back();
+      h->pool.pop_back();
+    } else {
+      LIO_HIP(hipEventCreate(&ev.first));
+      LIO_HIP(hipEventCreate(&ev.second));
+    }
+    h->pending.push_back(ev);
+  }
+  // the events: in the first and last launches' dispatch packets (the whole
+  // sweep), or around the feature stage
+  const hipEvent_t e0 = h->prof_scan ? ev.first : nullptr, e1 = h->prof_scan ? ev.second : nullptr;
   if (h->n > 0)
-    k_lego_claim<<<(unsigned)((h->n + 255) / 256), 256, 0, h->stream>>>(h->x, h->y, h->z, h->n, g, own);
-  k_lego_fill<<<cb, 256, 0, h->stream>>>(h->x, h->y, h->z, g, own, h->range_mat, h->full, h->ground);
+    hipExtLaunchKernelGGL(k_lego_claim, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, h->stream, e0, nullptr,
+                          0, h->x, h->y, h->z, h->n, g, own);
+  hipExtLaunchKernelGGL(k_lego_fill, dim3(cb), dim3(256), 0, h->stream, h->n > 0 ? nullptr : e0, nullptr, 0, h->x,
+                        h->y, h->z, g, own, h->range_mat, h->full, h->ground);
   k_lego_ground<<<(g.H + 255) / 256, 256, 0, h->stream>>>(g, own, h->full, h->ground, h->parent,
                                                            !cc_lds && !cc_band);
   if (cc_band) {
@@ -3838,21 +3865,10 @@ int slio_lego_run_async(slio_lego_handle h) {
   const CloudInfo ci{h->start_ring, h->end_ring, h->col_ind, h->srange, h->desk, h->nseg};
   const FeatOut fo{h->flabel, h->corner_stage, h->corner_count, h->surf_stage, h->surf_count,
                    h->corner_sharp, h->sharp_count, h->flat_stage, h->flat_count, h->gflag};
-  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  if (h->prof) {
-    if (h->pending.size() > 256) lego_prof_drain(h);
-    if (!h->pool.empty()) {
-      ev = h->pool.back();
-      h->pool.pop_back();
-    } else {
-      LIO_HIP(hipEventCreate(&ev.first));
-      LIO_HIP(hipEventCreate(&ev.second));
-    }
-    h->pending.push_back(ev);
-  }
-  launch_features<kModeLego>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw, ev);
-  k_lego_concat<<<R, kConcatThreads, 0, h->stream>>>(R, h->start_ring, fo, h->c_sharp, h->c_less_sharp,
-                                          h->c_flat, h->c_less_flat, h->counts);
+  launch_features<kModeLego>(h->stream, R, ci, h->curvature, h->picked0, h->fc, fo, h->fw,
+                             h->prof_scan ? std::pair<hipEvent_t, hipEvent_t>{nullptr, nullptr} : ev);
+  hipExtLaunchKernelGGL(k_lego_concat, dim3(R), dim3(kConcatThreads), 0, h->stream, nullptr, e1, 0, R,
+                        h->start_ring, fo, h->c_sharp, h->c_less_sharp, h->c_flat, h->c_less_flat, h->counts);
   LIO_HIP(hipGetLastError());
   h->ran = true;
   return SLIO_OK;
@@ -3969,6 +3985,7 @@ int slio_lego_profile(slio_lego_handle h, int enable) {
   LEGO_CHECK_H(h);
   const bool keep = (enable & SLIO_LIO_PROFILE_KEEP) != 0;
   h->prof = (enable & ~SLIO_LIO_PROFILE_KEEP) != 0;
+  h->prof_scan = (enable & SLIO_LIO_PROFILE_SCAN) != 0;
   if (!keep) {
     lego_prof_drain(h);
     h->prof_ms = 0.0;

@@ -122,20 +122,75 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def frontend_traffic(workload):
-    """HBM bytes of one feature-stage pass (k_fe_pick + k_fe_ring) from the
-    committed PMC summary (scripts/pmc_frontend.sh: rocprofv3 --pmc cannot run
-    inside this process), only when the library was built from the same
-    sources."""
+def frontend_traffic(workload, kernels=None):
+    """HBM bytes of one scan through the front-end (every kernel's per-launch
+    mean summed; `kernels`: only those) from the committed PMC summary
+    (scripts/pmc_frontend.sh: rocprofv3 --pmc cannot run inside this
+    process), only when the library was built from the same sources."""
     path = os.path.join(ROOT, "profiles", f"{workload}_traffic.json")
     try:
         tj = json.load(open(path))
         from agi_lidar_slam_amd import build
         if tj.get("workload") == workload and tj.get("source_hash") == build.source_hash():
-            return tj.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+            if kernels is None:
+                return tj.get("hbm_bytes_per_launch")
+            pk = tj.get("counters_per_kernel", {})
+            if all(k in pk for k in kernels):
+                return sum(2 * pk[k]["FETCH_SIZE"] + pk[k]["WRITE_SIZE"] for k in kernels) * 1024
+    except (OSError, ValueError, KeyError):
         pass
     return None
+
+
+# SURVEY.md §8d's compulsory model of a LiDAR front-end scan: per input point
+# 22 B in (xyz, intensity, ring, time), 8 B range-image cell, 24 B compacted
+# out, ~16 B curvature / flags / labels -> 70 B
+FRONTEND_BYTES_PER_PT = 70
+
+
+def frontend_rooflines(lib, h, args, prefix, points_in, n_ext, nfeat, run_async, workload, feat_kernels):
+    """(scan roofline, feature-stage roofline): HIP events in the first and
+    last launches of --timing-steps further scans (the whole scan: every
+    kernel), then in the feature stage's (k_fe_pick .. k_fe_ring)."""
+    from agi_lidar_slam_amd import _lib as L
+    prof = getattr(lib, f"{prefix}_profile")
+    read = getattr(lib, f"{prefix}_profile_read")
+    out = []
+    for mode in (L.SLIO_LIO_PROFILE_SCAN, 1):
+        prof(h, mode)
+        for k in range(max(1, args.timing_steps)):
+            L.check(run_async(h), "run_async")
+        prof(h, mode | L.SLIO_LIO_PROFILE_KEEP)
+        ms, nl = C.c_double(), C.c_int64()
+        read(h, C.byref(ms), C.byref(nl))
+        prof(h, 0)
+        out.append(((ms.value / max(nl.value, 1)) * 1e-3, int(nl.value)))
+    (scan_s, scan_n), (feat_s, feat_n) = out
+    alg = FRONTEND_BYTES_PER_PT * points_in
+    achieved = alg / scan_s / 1e9 if scan_s > 0 else None
+    # feature stage (k_fe_pick + k_fe_ring): per extracted point curvature 4 + column 4 +
+    # flag 1 + label 4 + the point 16 (surface / corner gathers), and the outputs 16 B each
+    falg = 29 * n_ext + 16 * nfeat
+    fach = falg / feat_s / 1e9 if feat_s > 0 else None
+    scan = {
+        "bound": "hbm",
+        "kernel": f"the whole scan: every front-end launch ({workload}), first start to last end",
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+        "traffic": frontend_traffic(workload),
+        "alg_bytes_per_launch": alg,
+        "alg_model": f"{FRONTEND_BYTES_PER_PT} B per input point (SURVEY.md 8d)",
+        "avg_launch_us": scan_s * 1e6, "launches": scan_n,
+        "timing": (f"HIP events in the dispatch packets of the first and last launches of each of "
+                   f"{args.timing_steps} further scans"),
+    }
+    feat = {
+        "kernel": "feature stage: k_fe_pick + k_fe_ring (one timed span)",
+        "achieved": fach, "frac": (fach / HBM_PEAK_GBS) if fach else None,
+        "traffic": frontend_traffic(workload, feat_kernels), "alg_bytes_per_launch": falg,
+        "avg_launch_us": feat_s * 1e6, "launches": feat_n,
+    }
+    return scan, feat
 
 
 def bench_c3(args, rank, world, dev, dist):
@@ -188,29 +243,22 @@ def bench_c3(args, rank, world, dev, dist):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # the feature stage's kernel time: HIP events on further scans of stream
-    # 0 alone, after the timed region (events cost idle time per launch)
-    if not args.no_kernel_timing:
-        lib.slio_lio_profile(h, 1)
-        for k in range(max(1, args.timing_steps)):
-            L.check(lib.slio_lio_run_async(h), "slio_lio_run_async")
-        lib.slio_lio_profile(h, 1 | L.SLIO_LIO_PROFILE_KEEP)
     L.check(lib.slio_lio_get_counts(h, C.byref(counts)), "counts")
-    ms, nl = C.c_double(), C.c_int64()
-    lib.slio_lio_profile_read(h, C.byref(ms), C.byref(nl))
+    n_ext, nc, ns = counts.n_extracted, counts.n_corner, counts.n_surface
+    # kernel time: HIP events on further scans of stream 0 alone, after the
+    # timed region (events cost idle time per launch)
+    roof, feat = (None, None)
+    if not args.no_kernel_timing:
+        roof, feat = frontend_rooflines(lib, h, args, "slio_lio", int(sc["x"].size), n_ext, nc + ns,
+                                        lib.slio_lio_run_async, "c3", ["k_fe_pick", "k_fe_ring"])
+        if S > 1:
+            roof["traffic"] = feat["traffic"] = None
     if world > 1:
         import torch
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     value = args.steps * S * world / el
-    avg_s = (ms.value / max(nl.value, 1)) * 1e-3
-    n_ext, nc, ns = counts.n_extracted, counts.n_corner, counts.n_surface
-    # feature stage (k_fe_pick .. k_fe_voxel) compulsory bytes: per extracted point curvature 4 + column 4
-    # + flag 1 + label 4 + the point 16 (surface / corner gathers), and the
-    # corner / surface outputs 16 B each
-    alg_bytes = 29 * n_ext + 16 * (nc + ns)
-    achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
@@ -257,20 +305,8 @@ def bench_c3(args, rank, world, dev, dist):
                             + (f"; {S} independent scans in flight per GPU (own handle and stream each)"
                                if S > 1 else "")),
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "feature stage: k_fe_pick + k_fe_ring (one timed span)",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": frontend_traffic("c3") if S == 1 else None,
-            "alg_bytes_per_launch": alg_bytes,
-            "avg_launch_us": avg_s * 1e6,
-            "launches": int(nl.value),
-            "timing": (f"HIP events in the dispatch packet, {args.timing_steps} further scans of one "
-                       "stream after the timed region"),
-        },
+        "roofline": roof,
+        "roofline_feature_stage": feat,
         "cpu_baseline": cpu,
     }
     if rank == 0:
@@ -415,28 +451,20 @@ def bench_lego(args, rank, world, dev, dist):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # the feature stage's kernel time (HIP events), further sweeps after the timed region
-    if not args.no_kernel_timing:
-        lib.slio_lego_profile(h, 1)
-        for k in range(max(1, args.timing_steps)):
-            L.check(lib.slio_lego_run_async(h), "slio_lego_run_async")
-        lib.slio_lego_profile(h, 1 | L.SLIO_LIO_PROFILE_KEEP)
     L.check(lib.slio_lego_get_counts(h, C.byref(counts)), "counts")
-    ms, nl = C.c_double(), C.c_int64()
-    lib.slio_lego_profile_read(h, C.byref(ms), C.byref(nl))
+    nseg = counts.n_segmented
+    nfeat = counts.n_sharp + counts.n_less_sharp + counts.n_flat + counts.n_less_flat
+    # kernel time (HIP events), further sweeps after the timed region
+    roof, feat = (None, None)
+    if not args.no_kernel_timing:
+        roof, feat = frontend_rooflines(lib, h, args, "slio_lego", int(sw["x"].size), nseg, nfeat,
+                                        lib.slio_lego_run_async, "lego", ["k_fe_pick", "k_fe_ring"])
     if world > 1:
         import torch
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     value = args.steps * world / el
-    avg_s = (ms.value / max(nl.value, 1)) * 1e-3
-    nseg = counts.n_segmented
-    nfeat = counts.n_sharp + counts.n_less_sharp + counts.n_flat + counts.n_less_flat
-    # feature stage compulsory bytes (as C3): per segmented point curvature 4 + column 4 + flag 1 +
-    # label 4 + the point 16, and the four feature clouds 16 B per point
-    alg_bytes = 29 * nseg + 16 * nfeat
-    achieved = alg_bytes / avg_s / 1e9 if avg_s > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
@@ -480,20 +508,8 @@ def bench_lego(args, rank, world, dev, dist):
             "parallelism": (f"replicas x{world}: one sweep stream per GPU, no collective"
                             if world > 1 else "single GPU"),
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "feature stage: k_fe_pick + k_fe_ring (one timed span)",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": frontend_traffic("lego"),
-            "alg_bytes_per_launch": alg_bytes,
-            "avg_launch_us": avg_s * 1e6,
-            "launches": int(nl.value),
-            "timing": (f"HIP events in the dispatch packet, {args.timing_steps} further sweeps after "
-                       "the timed region"),
-        },
+        "roofline": roof,
+        "roofline_feature_stage": feat,
         "cpu_baseline": cpu,
     }
     if rank == 0:

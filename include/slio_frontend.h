@@ -82,6 +82,9 @@ int slio_lio_get_counts(slio_lio_handle h, slio_lio_counts* counts);
  * the totals (pause / resume).  Read: accumulated ms and launch count
  * (synchronises the stream). */
 #define SLIO_LIO_PROFILE_KEEP 16
+/* enable | SLIO_LIO_PROFILE_SCAN: time every whole scan instead (the first
+ * launch's start to the last launch's end: all the front-end's kernels). */
+#define SLIO_LIO_PROFILE_SCAN 32
 int slio_lio_profile(slio_lio_handle h, int enable);
 int slio_lio_profile_read(slio_lio_handle h, double* ms, int64_t* launches);
 
@@ -188,7 +191,8 @@ int slio_lego_get_features(slio_lego_handle h, float* deskewed, float* curvature
 /* cornerPointsSharp, cornerPointsLessSharp, surfPointsFlat, surfPointsLessFlat. */
 int slio_lego_get_clouds(slio_lego_handle h, float* sharp, float* less_sharp, float* flat,
                          float* less_flat);
-/* Timing of the feature kernel, as slio_lio_profile. */
+/* Timing of the feature kernels (or, with SLIO_LIO_PROFILE_SCAN, of the
+ * whole sweep), as slio_lio_profile. */
 int slio_lego_profile(slio_lego_handle h, int enable);
 int slio_lego_profile_read(slio_lego_handle h, double* ms, int64_t* launches);
 
