@@ -511,7 +511,13 @@ def test_knn_certificate_bitwise(L, c2, npts, mode, ext, maxit, monkeypatch):
         assert per[0] == per[1] == per[2]
         if mode == 1:
             # fixed flow: pass 1 searches every query in full (new epoch);
-            # at C2 passes 2 and 3 certify ~86 % and > 99 % of the queries
+            # at C2 passes 2 and 3 certify ~98 % and 100 % of the queries.
+            # The 20,013-point case certifies far fewer (~9.5k of 40k) by
+            # geometry, not by a weaker certificate: the first 20,013 points in
+            # VoxelGrid order are one flat ground patch (29 x 33 x 0.6 m), the
+            # update is degenerate in-plane and the pose slides 72 / 52 mm
+            # between passes 1-2 / 2-3 (oracle, fixed flow) against 0.13 /
+            # 0.02 mm for the whole scan -- beyond most queries' certified radius
             cert, srch = per[0]
             assert srch >= npts and cert > 0
             if npts == 100_000:
