@@ -3961,6 +3961,76 @@ static hipError_t wait_stream(Ctx& c) {
   return e;
 }
 
+// The same polled wait for any stream (the map maintenance, scan VoxelGrid
+// and scan-to-map paths read counts and boxes back several times per scan):
+// one event per device and host thread.
+static hipError_t spin_sync(hipStream_t st) {
+  thread_local hipEvent_t evs[16] = {};
+  hipDevice_t dev = 0;
+  hipError_t e = hipStreamGetDevice(st, &dev);
+  if (e != hipSuccess || dev < 0 || dev >= 16) {
+    (void)hipGetLastError();
+    return hipStreamSynchronize(st);
+  }
+  if (!evs[dev]) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    e = hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming);
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e) return e;
+  }
+  if ((e = hipEventRecord(evs[dev], st))) return e;
+  while ((e = hipEventQuery(evs[dev])) == hipErrorNotReady) __builtin_ia32_pause();
+  return e;
+}
+
+// Small device -> host reads (scan totals, counters, boxes) through a pinned
+// staging buffer of the calling thread, then one polled wait: a copy into
+// pageable host memory waits inside the runtime, and a blocking stream
+// synchronisation wakes ~10-20 us late.
+struct Rb {
+  void* dst;
+  const void* src;
+  size_t n;
+};
+static hipError_t readback(hipStream_t st, const Rb* rb, int k) {
+  thread_local uint8_t* pin = nullptr;
+  thread_local size_t cap = 0;
+  size_t tot = 0;
+  for (int j = 0; j < k; ++j) tot += (rb[j].n + 15) & ~(size_t)15;
+  if (tot > cap) {
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(tot, 4096);
+    if (hipHostMalloc((void**)&pin, want) != hipSuccess) {
+      (void)hipGetLastError();
+      pin = nullptr;
+    } else {
+      cap = want;
+    }
+  }
+  hipError_t e = hipSuccess;
+  if (!pin) {  // (no pinned buffer: the plain copies)
+    for (int j = 0; j < k && !e; ++j) e = hipMemcpyAsync(rb[j].dst, rb[j].src, rb[j].n, hipMemcpyDeviceToHost, st);
+    return e ? e : hipStreamSynchronize(st);
+  }
+  size_t off = 0;
+  for (int j = 0; j < k && !e; ++j) {
+    e = hipMemcpyAsync(pin + off, rb[j].src, rb[j].n, hipMemcpyDeviceToHost, st);
+    off += (rb[j].n + 15) & ~(size_t)15;
+  }
+  if (!e) e = spin_sync(st);
+  if (e) return e;
+  off = 0;
+  for (int j = 0; j < k; ++j) {
+    std::memcpy(rb[j].dst, pin + off, rb[j].n);
+    off += (rb[j].n + 15) & ~(size_t)15;
+  }
+  return hipSuccess;
+}
+
 // Wait for the device-resident update to publish its result in the mapped
 // host block (one release store after x, P and the flags), which the host
 // sees ~1 us after it happens; the stream's completion event is polled now
@@ -5586,13 +5656,13 @@ static int scan_flags_k(int k, const uint32_t* const* flag, uint32_t* const* ran
   for (int j = 0; j < k; ++j) total[j] = 0;
   if (n == 0) return SLIO_OK;
   uint32_t last[4] = {0, 0, 0, 0};
-  hipError_t e = hipSuccess;
+  Rb rb[4];
   for (int j = 0; j < k; ++j) {
     if (int rc = scan_launch(flag[j], rank[j], n, st)) return rc;
-    if (!e) e = hipMemcpyAsync(&last[2 * j], rank[j] + n - 1, 4, hipMemcpyDeviceToHost, st);
-    if (!e) e = hipMemcpyAsync(&last[2 * j + 1], flag[j] + n - 1, 4, hipMemcpyDeviceToHost, st);
+    rb[2 * j] = Rb{&last[2 * j], rank[j] + n - 1, 4};
+    rb[2 * j + 1] = Rb{&last[2 * j + 1], flag[j] + n - 1, 4};
   }
-  if (!e) e = hipStreamSynchronize(st);
+  const hipError_t e = readback(st, rb, 2 * k);
   if (e) {
     set_error(std::string("slio map: scan total: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
@@ -5631,7 +5701,7 @@ static int add_reserve(MapDev& m, int64_t more, hipStream_t st) {
   }
   if (m.nadd > 0 && ((e = hipMemcpyAsync(a, m.add4, 16 * m.nadd, hipMemcpyDeviceToDevice, st)) ||
                      (e = hipMemcpyAsync(k, m.akeep, m.nadd, hipMemcpyDeviceToDevice, st)) ||
-                     (e = hipStreamSynchronize(st)))) {
+                     (e = spin_sync(st)))) {
     (void)hipFree(a);
     (void)hipFree(k);
     set_error(std::string("slio map: grow adds: ") + hipGetErrorString(e));
@@ -5685,13 +5755,16 @@ static int map_add_hashed(Ctx& c, const float4* in, int64_t n, float ds, int64_t
   k_ds_hash<<<grid_blocks(n), 256, 0, st>>>(in, n, ds, hb, hkey, hcnt, hmem, dcount + 2);
   k_ds_groups_hash<<<grid_blocks(H), 256, 0, st>>>(in, n, ds, hb, hkey, hcnt, hmem, map_view(m), m.keep, surv,
                                                    dcount);
-  uint32_t total = 0;
-  if (int rc = scan_flags(surv, rank, n, st, &total)) return rc;  // (reads `total` back: synchronises)
+  // the survivors' ranks, then their total and the counters in one readback
+  if (int rc = scan_launch(surv, rank, n, st)) return rc;
+  uint32_t last[2] = {0, 0};
   unsigned long long ops[3] = {0, 0, 0};
-  if ((e = hipMemcpyAsync(ops, dcount, 24, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+  const Rb rb[3] = {{&last[0], rank + n - 1, 4}, {&last[1], surv + n - 1, 4}, {ops, dcount, 24}};
+  if ((e = readback(st, rb, 3))) {
     set_error(std::string("slio map: groups: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
   }
+  const uint32_t total = last[0] + last[1];
   if (ops[2]) {
     *fallback = true;
     return SLIO_OK;
@@ -5798,7 +5871,8 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
         break;
       }
       k_ds_range<<<std::min(nb, 256), 256, 0, st>>>(in, n, ds, rg);
-      if ((e = hipMemcpyAsync(got, rg, 24, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+      const Rb rb{got, rg, 24};
+      if ((e = readback(st, &rb, 1))) {
         set_error(std::string("slio map: range: ") + hipGetErrorString(e));
         rc = SLIO_EDEVICE;
         break;
@@ -5830,7 +5904,8 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
     uint32_t total = 0;
     if ((rc = scan_flags(surv, rank, n, st, &total))) break;
     unsigned long long ops[2] = {0, 0};
-    if ((e = hipMemcpyAsync(ops, dcount, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+    const Rb rbo{ops, dcount, 16};
+    if ((e = readback(st, &rbo, 1))) {
       set_error(std::string("slio map: groups: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
@@ -5839,7 +5914,8 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
       // interacting groups (k_ds_conflicts): the exact sequential order
       k_ds_sequential<<<1, 1, 0, st>>>(in, k1, v1, n, ds, map_view(m), m.keep, surv, dcount);
       if ((rc = scan_flags(surv, rank, n, st, &total))) break;
-      if ((e = hipMemcpyAsync(ops, dcount, 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+      const Rb rbs{ops, dcount, 8};
+      if ((e = readback(st, &rbs, 1))) {
         set_error(std::string("slio map: sequential Add_Points: ") + hipGetErrorString(e));
         rc = SLIO_EDEVICE;
         break;
@@ -5995,13 +6071,14 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   if (n1)
     if (int rc = scan_launch(aflag, arank, n1, st)) return rc;
   uint32_t last[4] = {0, 0, 0, 0};
-  if ((e = hipMemcpyAsync(&last[0], rank + n0 - 1, 4, hipMemcpyDeviceToHost, st)) ||
-      (e = hipMemcpyAsync(&last[1], flag + n0 - 1, 4, hipMemcpyDeviceToHost, st)) ||
-      (n1 && (e = hipMemcpyAsync(&last[2], arank + n1 - 1, 4, hipMemcpyDeviceToHost, st))) ||
-      (n1 && (e = hipMemcpyAsync(&last[3], aflag + n1 - 1, 4, hipMemcpyDeviceToHost, st))))
-    return fail("counts", e);
   if (n1) k_compact4<<<grid_blocks(n1), 256, 0, st>>>(m.add4, aflag, arank, n1, acomp);
-  if ((e = hipStreamSynchronize(st))) return fail("counts", e);
+  {
+    const Rb rb[4] = {{&last[0], rank + n0 - 1, 4},
+                      {&last[1], flag + n0 - 1, 4},
+                      {&last[2], arank + (n1 ? n1 - 1 : 0), 4},
+                      {&last[3], aflag + (n1 ? n1 - 1 : 0), 4}};
+    if ((e = readback(st, rb, n1 ? 4 : 2))) return fail("counts", e);
+  }
   const uint32_t n0p = last[0] + last[1], na = last[2] + last[3];
   if (na) {
     // the live additions' box: they must lie a cell inside the kept grid
@@ -6009,8 +6086,8 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
     int32_t got[8];
     if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) return fail("box", e);
     k_bbox4<<<std::min(grid_blocks(na), 512), 256, 0, st>>>(acomp, na, bb);
-    if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
-      return fail("box", e);
+    const Rb rb{got, bb, 32};
+    if ((e = readback(st, &rb, 1))) return fail("box", e);
     if (got[6]) return SLIO_OK;  // non-finite: the sorting rebuild reports it
     const float o[3] = {g.ox, g.oy, g.oz};
     const int d[3] = {g.dx, g.dy, g.dz};
@@ -6057,7 +6134,7 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   // coarse level: the boxes widened by the additions (deleted points leave
   // them conservative); the points themselves are the fine runs
   if (na) k_coarse_extend<<<grid_blocks(na), 256, 0, st>>>(acomp, na, g, m.clo, m.chi, m.cg);
-  if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) return fail("coarse kernels", e);
+  if ((e = hipGetLastError()) || (e = spin_sync(st))) return fail("coarse kernels", e);
   m.blk = nullptr;
   m.bstart = nullptr;
   m.nblk = 0;
@@ -6145,7 +6222,8 @@ static int map_refresh_locked(Ctx& c, bool adds_only) {
     return SLIO_EDEVICE;
   }
   if (n) k_bbox4<<<std::min(grid_blocks(n), 512), 256, 0, st>>>(in4, n, bb);
-  if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+  const Rb rbb{got, bb, 32};
+  if ((e = readback(st, &rbb, 1))) {
     set_error(std::string("slio map rebuild: bbox: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
   }
@@ -6313,7 +6391,7 @@ int slio_map_add_points(slio_handle h, const float* x, const float* y, const flo
     } else {
       k_pack_ids<<<grid_blocks(n), 256, 0, c.stream>>>(dx_, dy_, dz_, n, 0u, in4);
       rc = map_add(c, in4, n, downsample != 0, downsample_size, &cnt);
-      if (!rc) (void)hipStreamSynchronize(c.stream);
+      if (!rc) (void)spin_sync(c.stream);
     }
     if (int rc2 = map_write_end(c); rc2 && !rc) rc = rc2;
     for (void* q : {(void*)dx_, (void*)dy_, (void*)dz_, (void*)in4})
@@ -6629,7 +6707,8 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
       break;
     }
     k_vg_bbox<<<std::min(grid_blocks(n), 64), 256, 0, st>>>(dx_, dy_, dz_, n, bb);
-    if ((e = hipMemcpyAsync(got, bb, 32, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st))) {
+    const Rb rbb{got, bb, 32};
+    if ((e = readback(st, &rbb, 1))) {
       set_error(std::string("slio_scan_upload_voxel: bbox: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
@@ -6698,7 +6777,7 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
   }
   if (!rc) {
     if (m > 0 && c.bx) (void)hipMemsetAsync(c.sel, 0, m, st);
-    (void)hipStreamSynchronize(st);
+    (void)spin_sync(st);
     c.n = m;
     c.searched = false;
     if (n_down) *n_down = m;
@@ -7083,18 +7162,23 @@ int slio_s2m_normal_equations(slio_handle h_corner, slio_handle h_surf, const fl
   T.sry = fs(transform[2]), T.cry = fc(transform[2]);
   T.srz = fs(transform[0]), T.crz = fc(transform[0]);
   double acc[kS2mSums] = {0};
-  // corners first, then surfs (combineOptimizationCoeffs :1517-1543)
-  for (slio_handle h : {h_corner, h_surf}) {
-    if (!h) continue;
+  // corners first, then surfs (combineOptimizationCoeffs :1517-1543); both
+  // clouds' rows launched before either is read back (their own streams)
+  slio_handle hs2[2] = {h_corner, h_surf};
+  for (slio_handle h : hs2) {
+    if (!h || h->c.n == 0) continue;
     Ctx& c = h->c;
-    const int64_t n = c.n;
-    if (n == 0) continue;
-    const int nb = (int)((n + 255) / 256);
-    k_s2m_rows<<<nb, 256, 0, c.stream>>>(c.bx, c.by, c.bz, c.plane, c.sel, n, T, c.chunk_part);
-    std::vector<double> part((size_t)nb * kS2mSums);
+    const int nb = (int)((c.n + 255) / 256);
+    k_s2m_rows<<<nb, 256, 0, c.stream>>>(c.bx, c.by, c.bz, c.plane, c.sel, c.n, T, c.chunk_part);
     SLIO_HIP(hipGetLastError());
-    SLIO_HIP(hipStreamSynchronize(c.stream));
-    SLIO_HIP(hipMemcpy(part.data(), c.chunk_part, 8 * part.size(), hipMemcpyDeviceToHost));
+  }
+  for (slio_handle h : hs2) {
+    if (!h || h->c.n == 0) continue;
+    Ctx& c = h->c;
+    const int nb = (int)((c.n + 255) / 256);
+    std::vector<double> part((size_t)nb * kS2mSums);
+    const Rb rb{part.data(), c.chunk_part, 8 * part.size()};
+    SLIO_HIP(readback(c.stream, &rb, 1));
     for (int b = 0; b < nb; ++b)
       for (int k = 0; k < kS2mSums; ++k) acc[k] = acc[k] + part[(size_t)b * kS2mSums + k];
   }
@@ -7253,7 +7337,7 @@ static int undistort_device(Ctx& c, const float* x, const float* y, const float*
       break;
     }
     k_undistort<<<nb, 256, 0, st>>>(dx_, dy_, dz_, dt_, v1, n, dp, np, E, ux, uy, uz, ut);
-    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
+    if ((e = hipGetLastError()) || (e = spin_sync(st))) {
       set_error(std::string("slio undistort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
