@@ -886,33 +886,6 @@ __device__ __forceinline__ void group_merge_rolled(Top5& t, int width) {
   }
 }
 
-// Butterfly merge of Top6M lists over `width` consecutive lanes (rolled
-// ds_bpermute rounds).  The merged list and dropped minimum do not depend on
-// how the candidates were split over the lanes: the 6 smallest keys of the
-// union and its 7th smallest distance.
-__device__ __forceinline__ void group_merge_rolled(Top6M& a, int width) {
-#pragma unroll 1
-  for (int m = 1; m < width; m <<= 1) {
-    uint64_t ok[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) ok[j] = __shfl_xor(a.k[j], m);
-    const float om = __shfl_xor(a.m, m);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) top6m_insert(a, ok[j]);
-    a.m = fminf(a.m, om);
-  }
-}
-
-// A wavefront's certificate-failed queries handed to 16-lane groups (the
-// kNN fast path of a certificate pass, search_pass_body): query, block-row
-// range, merged list and dropped minimum
-struct WideStage {
-  float4 q[4];
-  uint32_t b[4][2];
-  uint64_t k[4][6];
-  float m[4];
-};
-
 // Conservative lower bound of the distance from coordinate q to the points
 // assigned to grid cell i along one axis (cell edges are known to +-tol).
 __device__ __forceinline__ float axis_gap(float q, int i, float o, float h, float tol) {
@@ -2720,9 +2693,7 @@ struct SearchLds {
   // deferred (far) queries of this chunk and the far workers' scratch
   int far_cnt, ref_cnt;
   uint32_t cost;  // block-row candidates of the chunk's queries (chunk_order)
-  // scan_runs_wide's run tables, one per group (during the kNN fast path, the
-  // wavefronts' WideStage records: the tables are used only after it)
-  alignas(16) uint32_t tab_pre[NT / 16][kTab];
+  uint32_t tab_pre[NT / 16][kTab];  // scan_runs_wide's run tables, one per group
   int32_t tab_dl[NT / 16][kTab];
   float4 far_q[SLIO_CHUNK];
   uint8_t far_slot[SLIO_CHUNK];
@@ -2915,9 +2886,50 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
         }
       }
     }
-    // after the 3x3x3 block's scan: exact if the 5th distance lies inside the
-    // block faces' bound, else a refinement (or the far queue) follows
-    auto block_bound = [&]() {
+    if (finite && !reused) {
+      cx = cell_coord(qx, g.ox, g.inv_h);
+      cy = cell_coord(qy, g.oy, g.inv_h);
+      cz = cell_coord(qz, g.oz, g.inv_h);
+      const int ex = max(max(-cx, cx - (g.dx - 1)), 0);
+      const int ey = max(max(-cy, cy - (g.dy - 1)), 0);
+      const int ez = max(max(-cz, cz - (g.dz - 1)), 0);
+      r = max(1, max(ex, max(ey, ez)));
+      if (r == 1 && !SPHERE) {
+        // (1) the 3x3x3 block around the query cell: 9 runs, one batch
+        // (r == 1 also covers query cells one step outside the grid: the
+        // block rows exist only for cells inside it)
+        if (map.blk && (ex | ey | ez) == 0) {
+          const uint32_t rb = ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx;
+          uint32_t i0 = rb + max(cx - 1, 0), i1 = rb + min(cx + 1, g.dx - 1) + 1;
+          SLIO_BCHK(i0, map.ncells + 1, "bstart0");
+          SLIO_BCHK(i1, map.ncells + 1, "bstart1");
+          const uint32_t b0 = map.bstart[i0];
+          const uint32_t b1 = map.bstart[i1];
+#ifdef SLIO_BOUNDS_CHECK
+          if (b1 < b0 || (int64_t)b1 > map.nblk)
+            printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
+#endif
+          if (KC && cfg.kc_epoch) {
+            Top6M tm;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) tm.k[j] = kInfKey;
+            tm.m = __int_as_float(0x7f800000);
+            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, tm);
+            group_merge2(tm);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) t.k[j] = tm.k[j];
+            kx6 = (uint32_t)tm.k[5];
+            kG = tm.m;
+          } else {
+            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
+            group_merge<LPQ>(t);
+          }
+          if (sub == 0 && out.chunk_cost) atomicAdd(&lds.s.cost, b1 - b0);
+        } else {
+          RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
+          scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
+          group_merge<LPQ>(t);
+        }
         bool covers;
         const float b1 = outside_bound(g, cx, cy, cz, 1, qx, qy, qz, covers);
         const float d5 = __uint_as_float((uint32_t)(t.k[4] >> 32));
@@ -2946,65 +2958,6 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
                     ? d5 * 1.00001f
                     : __int_as_float(0x7f800000);
         }
-    };
-    // certificate passes: a query whose certificate failed, when at most 4 of
-    // the wavefront's did, scans its block rows after the branch below on 16
-    // lanes (wide), not on its own 2
-    bool wide = false;
-    uint32_t wb0 = 0, wb1 = 0;
-    if (finite && !reused) {
-      cx = cell_coord(qx, g.ox, g.inv_h);
-      cy = cell_coord(qy, g.oy, g.inv_h);
-      cz = cell_coord(qz, g.oz, g.inv_h);
-      const int ex = max(max(-cx, cx - (g.dx - 1)), 0);
-      const int ey = max(max(-cy, cy - (g.dy - 1)), 0);
-      const int ez = max(max(-cz, cz - (g.dz - 1)), 0);
-      r = max(1, max(ex, max(ey, ez)));
-      if (r == 1 && !SPHERE) {
-        // (1) the 3x3x3 block around the query cell: 9 runs, one batch
-        // (r == 1 also covers query cells one step outside the grid: the
-        // block rows exist only for cells inside it)
-        if (map.blk && (ex | ey | ez) == 0) {
-          const uint32_t rb = ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx;
-          uint32_t i0 = rb + max(cx - 1, 0), i1 = rb + min(cx + 1, g.dx - 1) + 1;
-          SLIO_BCHK(i0, map.ncells + 1, "bstart0");
-          SLIO_BCHK(i1, map.ncells + 1, "bstart1");
-          const uint32_t b0 = map.bstart[i0];
-          const uint32_t b1 = map.bstart[i1];
-#ifdef SLIO_BOUNDS_CHECK
-          if (b1 < b0 || (int64_t)b1 > map.nblk)
-            printf("slio bounds: block range %u %u nblk %lld\n", b0, b1, (long long)map.nblk);
-#endif
-          if (KC && cfg.kc_epoch) {
-            // (the lanes active here are exactly the wavefront's queries that
-            // failed their certificate and scan block rows)
-            wide = __popcll(__ballot(sub == 0)) <= 4;
-            if (wide) {
-              wb0 = b0;
-              wb1 = b1;
-            } else {
-              Top6M tm;
-#pragma unroll
-              for (int j = 0; j < 6; ++j) tm.k[j] = kInfKey;
-              tm.m = __int_as_float(0x7f800000);
-              scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, tm);
-              group_merge2(tm);
-#pragma unroll
-              for (int j = 0; j < 5; ++j) t.k[j] = tm.k[j];
-              kx6 = (uint32_t)tm.k[5];
-              kG = tm.m;
-            }
-          } else {
-            scan_block_rows<LPQ, U>(map.blk, b0, b1 - b0, sub, qx, qy, qz, t);
-            group_merge<LPQ>(t);
-          }
-          if (sub == 0 && out.chunk_cost) atomicAdd(&lds.s.cost, b1 - b0);
-        } else {
-          RunCtx rc{cx, cy, cz, qx, qy, qz, 1, 0.0f, 0.0f};
-          scan_runs<LPQ, U>(pts, start, g, rc, 0x739c0ull /* rows 6-8, 11-13, 16-18 */, sub, t);
-          group_merge<LPQ>(t);
-        }
-        if (!wide) block_bound();
         r = 2;
 #ifndef SLIO_NO_R2_REFINE
       } else if (r == 2 && !SPHERE) {
@@ -3043,47 +2996,6 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
           if (sub != 0) top5_clear(t);  // lane 0 keeps the merged list
         }
         r = 2;
-      }
-    }
-    if constexpr (KC) {
-      // the wide block-row scans (at most 4 per wavefront, 16 lanes each: one
-      // candidate round where a pair needs ~6), results back to the pairs;
-      // the same keys and dropped minimum as the pair's own scan would give
-      const uint64_t dm = __ballot(wide && sub == 0);
-      if (dm) {
-        const int lane = tid & 63;
-        WideStage& ws = reinterpret_cast<WideStage*>(&lds.s.tab_pre[0][0])[tid >> 6];
-        if (wide && sub == 0) {
-          const int j = __popcll(dm & ((1ull << lane) - 1));
-          ws.q[j] = make_float4(qx, qy, qz, 0.0f);
-          ws.b[j][0] = wb0;
-          ws.b[j][1] = wb1;
-        }
-        wave_fence();
-        const int gq = lane >> 4, gs = lane & 15;
-        Top6M tm;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) tm.k[j] = kInfKey;
-        tm.m = __int_as_float(0x7f800000);
-        if (gq < __popcll(dm)) {
-          const float4 wq = ws.q[gq];
-          scan_block_rows<16, U>(map.blk, ws.b[gq][0], ws.b[gq][1] - ws.b[gq][0], gs, wq.x, wq.y, wq.z, tm);
-        }
-        group_merge_rolled(tm, 16);
-        if (gq < __popcll(dm) && gs == 0) {
-#pragma unroll
-          for (int j = 0; j < 6; ++j) ws.k[gq][j] = tm.k[j];
-          ws.m[gq] = tm.m;
-        }
-        wave_fence();
-        if (wide) {
-          const int j = __popcll(dm & ((1ull << (lane & ~1)) - 1));  // the pair's (its sub-0 lane's)
-#pragma unroll
-          for (int q = 0; q < 5; ++q) t.k[q] = ws.k[j][q];
-          kx6 = (uint32_t)ws.k[j][5];
-          kG = ws.m[j];
-          block_bound();
-        }
       }
     }
     if (!SPHERE) {
