@@ -1582,6 +1582,47 @@ __device__ __forceinline__ double ld_sys(const double* p) {
 __device__ __forceinline__ uint32_t ld_sys_u32(const uint32_t* p) {
   return __hip_atomic_load((const guint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Per-point outputs of a pass (plane, selection, residual, neighbour
+// positions, certificates), stored write-through (sc1): they leave no dirty
+// lines in the XCDs' L2s for the end-of-kernel write-back that every pass
+// boundary waits for (SLIO_PLAIN_OUT: plain stores, the A/B baseline)
+typedef __attribute__((address_space(1))) uint8_t gu8;
+__device__ __forceinline__ void st_out(float4* p, float4 v) {
+#ifdef SLIO_PLAIN_OUT
+  *p = v;
+#else
+  const uint64_t lo = ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
+  const uint64_t hi = ((uint64_t)__float_as_uint(v.w) << 32) | __float_as_uint(v.z);
+  __hip_atomic_store((guint64*)(uint64_t*)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((guint64*)(uint64_t*)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+__device__ __forceinline__ void st_out(uint4* p, uint4 v) {
+#ifdef SLIO_PLAIN_OUT
+  *p = v;
+#else
+  __hip_atomic_store((guint64*)(uint64_t*)p, ((uint64_t)v.y << 32) | v.x, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((guint64*)(uint64_t*)p + 1, ((uint64_t)v.w << 32) | v.z, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+__device__ __forceinline__ void st_out(uint32_t* p, uint32_t v) {
+#ifdef SLIO_PLAIN_OUT
+  *p = v;
+#else
+  __hip_atomic_store((guint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+__device__ __forceinline__ void st_out(float* p, float v) { st_out(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
+__device__ __forceinline__ void st_out(uint8_t* p, uint8_t v) {
+#ifdef SLIO_PLAIN_OUT
+  *p = v;
+#else
+  __hip_atomic_store((gu8*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
 __device__ __forceinline__ uint32_t arrive(uint32_t* p) {
   return __hip_atomic_fetch_add((guint*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2410,9 +2451,9 @@ __device__ __forceinline__ void reuse_row(const ScanDev& scan, const PoseDev& po
       row[12] = -(double)pd2;
       row[13] = 1.0;
     }
-    out.sel[i] = sel ? 1 : 0;
+    st_out(out.sel + i, (uint8_t)(sel ? 1 : 0));
   }
-  out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
+  st_out(out.resid + i, sel ? pd2 : __int_as_float(0x7fc00000));
 }
 
 // The chunk's 91 products of the rows in LDS (256 threads): on the matrix
@@ -3253,15 +3294,15 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
         }
       }
       FSTAMP(2, false);
-      out.plane[i] = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
-      out.sel[i] = sel ? 1 : 0;
-      out.resid[i] = sel ? pd2 : __int_as_float(0x7fc00000);
+      st_out(out.plane + i, make_float4(abcd[0], abcd[1], abcd[2], abcd[3]));
+      st_out(out.sel + i, (uint8_t)(sel ? 1 : 0));
+      st_out(out.resid + i, sel ? pd2 : __int_as_float(0x7fc00000));
       if constexpr (KC) {
         // this search's certificate: the query and G (its 5 go to nbr_pos),
         // and the 6th (a certified pass's: the one of the 6 left out)
         if (cfg.kc_epoch) {
-          if (q.w != -2.0f) out.kq[i] = q;
-          out.k6[i] = lds.s.kx6[slot];
+          if (q.w != -2.0f) st_out(out.kq + i, q);
+          st_out(out.k6 + i, lds.s.kx6[slot]);
         }
       }
       if (sel) {
@@ -3315,13 +3356,13 @@ __device__ __forceinline__ void search_pass_body(PassLds<search_block<LPQ>()>& l
       for (int k = tid; k < na * nv; k += NT) {
         const int a = k >= nv ? (k >= 2 * nv ? 2 : 1) : 0;
         const int v = k - a * nv;
-        reinterpret_cast<uint4*>(dst(a))[v] = reinterpret_cast<const uint4*>(src(a))[v];
+        st_out(reinterpret_cast<uint4*>(dst(a)) + v, reinterpret_cast<const uint4*>(src(a))[v]);
       }
     } else {
       for (int k = tid; k < na * nw; k += NT) {
         const int a = k >= nw ? (k >= 2 * nw ? 2 : 1) : 0;
         const int v = k - a * nw;
-        dst(a)[v] = src(a)[v];
+        st_out(dst(a) + v, src(a)[v]);
       }
     }
   }
