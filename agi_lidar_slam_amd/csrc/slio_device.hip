@@ -557,10 +557,10 @@ __device__ __forceinline__ void atomic_fmax(float* a, float v) {
 }
 // widen the boxes (and counts) of the coarse cells the na additions fall in;
 // a point's coarse cell is its (clamped) fine cell / 4 on every axis
-__global__ void k_coarse_extend(const float4* __restrict__ adds, int64_t na, GridGeom g,
-                                float4* __restrict__ lo, float4* __restrict__ hi, GridGeom cg) {
+__global__ void k_coarse_extend(const float4* __restrict__ adds, const uint8_t* __restrict__ keep, int64_t na,
+                                GridGeom g, float4* __restrict__ lo, float4* __restrict__ hi, GridGeom cg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= na) return;
+  if (i >= na || (keep && !keep[i])) return;
   const float4 v = adds[i];
   const int fx = min(max(cell_coord(v.x, g.ox, g.inv_h), 0), g.dx - 1);
   const int fy = min(max(cell_coord(v.y, g.oy, g.inv_h), 0), g.dy - 1);
@@ -4700,6 +4700,87 @@ __global__ void k_widen_flags(const uint8_t* __restrict__ k, int64_t n, uint32_t
 
 static int grid_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
 
+// ---- survivor ranks straight from the keep bytes (the merge rebuild's
+// exclusive prefix count of the stored points): per-tile counts, one
+// workgroup's scan of the tile counts, then each tile's ranks -- 10 + 10 MB
+// read and 40 MB written for the 10M map (the flags widened to 32 bits and a
+// device-wide scan moved ~170 MB in ~110 us)
+constexpr int kRankTile = 4096;  // keep bytes per workgroup: 256 threads x 16
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t w) {  // per byte: 0x80 when non-zero
+  return (((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;
+}
+__device__ __forceinline__ uint4 load_keep16(const uint8_t* __restrict__ keep, int64_t i, int64_t n) {
+  if (i + 16 <= n) return *reinterpret_cast<const uint4*>(keep + i);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int b = 0; b < 16 && i + b < n; ++b) w[b >> 2] |= (uint32_t)(keep[i + b] != 0) << (8 * (b & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// block-wide exclusive sum of one value per thread (256 threads); *total gets the sum
+__device__ __forceinline__ uint32_t block_excl_256(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t ws[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t s = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(s, d, 64);
+    if (lane >= d) s += u;
+  }
+  if (lane == 63) ws[w] = s;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int k = 0; k < w; ++k) off += ws[k];
+  if (total) *total = ws[0] + ws[1] + ws[2] + ws[3];
+  __syncthreads();
+  return off + s - v;
+}
+__global__ __launch_bounds__(256) void k_keep_tiles(const uint8_t* __restrict__ keep, int64_t n,
+                                                    uint32_t* __restrict__ tcnt) {
+  const uint4 v = load_keep16(keep, (int64_t)blockIdx.x * kRankTile + threadIdx.x * 16, n);
+  const uint32_t c = __popc(nz_bytes(v.x)) + __popc(nz_bytes(v.y)) + __popc(nz_bytes(v.z)) + __popc(nz_bytes(v.w));
+  uint32_t tot;
+  (void)block_excl_256(c, &tot);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
+}
+// in place: tcnt[0..nt) -> exclusive prefix, tcnt[nt] = the total (one workgroup)
+__global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tcnt, int64_t nt) {
+  const int64_t per = (nt + 255) / 256, a = min((int64_t)threadIdx.x * per, nt), b = min(a + per, nt);
+  uint32_t s = 0;
+  for (int64_t i = a; i < b; ++i) s += tcnt[i];
+  uint32_t tot;
+  uint32_t run = block_excl_256(s, &tot);
+  for (int64_t i = a; i < b; ++i) {
+    const uint32_t v = tcnt[i];
+    tcnt[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) {
+    tcnt[nt] = tot;
+    tcnt[nt + 1] = 0;  // (k_merge_keys' live count and edge flag)
+    tcnt[nt + 2] = 0;
+  }
+}
+__global__ __launch_bounds__(256) void k_keep_rank(const uint8_t* __restrict__ keep, int64_t n,
+                                                   const uint32_t* __restrict__ tbase, uint32_t* __restrict__ rank) {
+  const int64_t i0 = (int64_t)blockIdx.x * kRankTile + threadIdx.x * 16;
+  const uint4 v = load_keep16(keep, i0, n);
+  const uint32_t m[4] = {nz_bytes(v.x), nz_bytes(v.y), nz_bytes(v.z), nz_bytes(v.w)};
+  const uint32_t c = __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
+  uint32_t r = tbase[blockIdx.x] + block_excl_256(c, nullptr);
+  uint32_t o[16];
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    o[b] = r;
+    r += (m[b >> 2] >> (8 * (b & 3) + 7)) & 1u;
+  }
+  if (i0 + 16 <= n) {
+    uint4* d = reinterpret_cast<uint4*>(rank + i0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  } else {
+    for (int b = 0; b < 16 && i0 + b < n; ++b) rank[i0 + b] = o[b];
+  }
+}
+
 // Build the grid index of m from the n points in `in` (device, x y z
 // bits(id), any order, all ids distinct) with bounding box mn / mx: the cell
 // table, the cell-sorted points, the coarse level and (speed only) the
@@ -6012,7 +6093,8 @@ __global__ void k_merge_tiles(const uint32_t* __restrict__ sk, uint32_t na, int6
   jt[t] = lower_bound_u32(sk, 0, na, (uint32_t)min(t * (int64_t)kMergeTile, ncells1));
 }
 __global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict__ old_start,
-                                                     const uint32_t* __restrict__ rank, int64_t n0, uint32_t n0p,
+                                                     const uint32_t* __restrict__ rank, int64_t n0,
+                                                     const uint32_t* __restrict__ n0p_p,
                                                      const uint32_t* __restrict__ sk, const uint32_t* __restrict__ jt,
                                                      int64_t ncells1, uint32_t* __restrict__ new_start) {
   __shared__ uint32_t lk[kMergeTile];
@@ -6033,6 +6115,7 @@ __global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict_
     const int64_t c = c0 + t + 256 * u;
     os[u] = c < c1 ? old_start[c] : 0u;
   }
+  const uint32_t n0p = *n0p_p;
 #pragma unroll
   for (int u = 0; u < kPer; ++u) r[u] = (int64_t)os[u] < n0 ? rank[os[u]] : n0p;
   __syncthreads();
@@ -6051,19 +6134,91 @@ __global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict_
     new_start[c] = r[u] + j0 + lo;
   }
 }
-__global__ void k_merge_pts(const float4* __restrict__ pts, const uint8_t* __restrict__ keep,
-                            const uint32_t* __restrict__ rank, const uint32_t* __restrict__ old_start,
-                            const uint32_t* __restrict__ new_start, int64_t n0, GridGeom g,
-                            float4* __restrict__ out) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n0 || !keep[p]) return;
-  const float4 v = pts[p];
+__device__ __forceinline__ uint32_t map_cell(const float4& v, const GridGeom& g) {
   const int cx = min(max(cell_coord(v.x, g.ox, g.inv_h), 0), g.dx - 1);
   const int cy = min(max(cell_coord(v.y, g.oy, g.inv_h), 0), g.dy - 1);
   const int cz = min(max(cell_coord(v.z, g.oz, g.inv_h), 0), g.dz - 1);
-  const uint32_t c = ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx + (uint32_t)cx;
-  const uint32_t os = old_start[c];  // <= p < n0
-  out[new_start[c] + rank[p] - rank[os]] = v;
+  return ((uint32_t)cz * (uint32_t)g.dy + (uint32_t)cy) * (uint32_t)g.dx + (uint32_t)cx;
+}
+// jp[t] = lb(cell of point t * kRankTile), t < ntiles; jp[ntiles] = na.  The
+// stored points are in cell order, so a point p of tile t in cell c has
+// jp[t] <= lb(c) <= jp[t + 1]
+__global__ void k_merge_ptiles(const float4* __restrict__ pts, int64_t ntiles, GridGeom g,
+                               const uint32_t* __restrict__ sk, uint32_t na, uint32_t* __restrict__ jp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  jp[t] = t == ntiles ? na : lower_bound_u32(sk, 0, na, map_cell(pts[t * kRankTile], g));
+}
+// survivor p of cell c goes to new_start[c] + rank[p] - rank(old_start[c])
+// = rank[p] + lb(c): one tile of kRankTile points per workgroup, 16 per
+// thread with every load in flight before any use, lb(c) from the tile's
+// additions in LDS (no per-point cell-table gathers: the dependent
+// pts -> old_start -> rank chain made the one-point-per-thread kernel
+// latency-bound, ~104 us for the 10M map)
+__global__ __launch_bounds__(256) void k_merge_pts(const float4* __restrict__ pts, const uint8_t* __restrict__ keep,
+                                                   const uint32_t* __restrict__ rank, const uint32_t* __restrict__ sk,
+                                                   const uint32_t* __restrict__ jp, int64_t n0, GridGeom g,
+                                                   float4* __restrict__ out) {
+  constexpr int kPer = kRankTile / 256, kLds = 1024;
+  __shared__ uint32_t lk[kLds];
+  const int64_t p0 = (int64_t)blockIdx.x * kRankTile + threadIdx.x;
+  const uint32_t j0 = jp[blockIdx.x], m = jp[blockIdx.x + 1] - j0;
+  const bool inl = m <= (uint32_t)kLds;
+  if (inl)
+    for (uint32_t k = threadIdx.x; k < m; k += 256) lk[k] = sk[j0 + k];
+  float4 v[kPer];
+  uint32_t r[kPer];
+  uint8_t kp[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t p = p0 + 256 * u;
+    kp[u] = p < n0 ? keep[p] : (uint8_t)0;
+    v[u] = p < n0 ? pts[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+    r[u] = p < n0 ? rank[p] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    if (!kp[u]) continue;
+    const uint32_t c = map_cell(v[u], g);
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((inl ? lk[mid] : sk[j0 + mid]) < c)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    out[r[u] + j0 + lo] = v[u];
+  }
+}
+// the additions' fine cell keys, dead ones keyed kDeadKey (sorted after
+// every live one, and above every cell a lower bound asks for); chk[0] += the
+// live count, chk[1] = 1 when a live addition is not a cell inside the grid
+// (or not finite): the merge is then void and the caller re-grids by sorting
+constexpr uint32_t kDeadKey = 0xFFFFFFFFu;
+struct MergeBox {
+  float lo[3], hi[3];
+};
+__global__ __launch_bounds__(256) void k_merge_keys(const float4* __restrict__ adds, const uint8_t* __restrict__ akeep,
+                                                    int64_t n1, GridGeom g, MergeBox bx, uint32_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ vals, uint32_t* __restrict__ chk) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool live = false, fits = true;
+  if (i < n1) {
+    live = akeep[i] != 0;
+    const float4 v = adds[i];
+    fits = v.x >= bx.lo[0] && v.x <= bx.hi[0] && v.y >= bx.lo[1] && v.y <= bx.hi[1] && v.z >= bx.lo[2] &&
+           v.z <= bx.hi[2];
+    keys[i] = live ? map_cell(v, g) : kDeadKey;
+    vals[i] = (uint32_t)i;
+  }
+  const int cnt = __syncthreads_count(live);
+  const int bad = __syncthreads_or(live && !fits);
+  if (threadIdx.x == 0) {
+    if (cnt) atomicAdd(chk, (uint32_t)cnt);
+    if (bad) atomicOr(chk + 1, 1u);
+  }
 }
 __global__ void k_merge_adds(const float4* __restrict__ adds, const uint32_t* __restrict__ sk,
                              const uint32_t* __restrict__ sv, uint32_t na, const uint32_t* __restrict__ new_start,
@@ -6071,14 +6226,18 @@ __global__ void k_merge_adds(const float4* __restrict__ adds, const uint32_t* __
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= na) return;
   const uint32_t c = sk[j];
+  if (c == kDeadKey) return;
   const uint32_t e = lower_bound_u32(sk, j, na, c + 1);
   out[new_start[c + 1] - (e - j)] = adds[sv[j]];
 }
 
 // The merge rebuild (see k_merge_start) of m: *handled = false when the
 // additions do not all lie at least one cell inside the grid (then the caller
-// rebuilds by sorting, with a new grid).  Stream-ordered; synchronises twice
-// (the counts, the additions' box) and once at the end.
+// rebuilds by sorting, with a new grid).  Stream-ordered and speculative: the
+// merge runs into temporaries while k_merge_keys checks the additions, and
+// ONE readback (survivor count, live additions, the edge flag) decides
+// whether the map takes the result (three synchronisations before: the
+// counts, the additions' box, the end).
 static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   *handled = false;
   const int64_t n0 = m.n, n1 = m.nadd;
@@ -6089,80 +6248,61 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
     return err == hipErrorOutOfMemory ? SLIO_ENOMEM : SLIO_EDEVICE;
   };
   const int64_t na_cap = std::max<int64_t>(n1, 1);
-  if ((e = m.take(m.b_ref[1], 4 * n0)) || (e = m.take(m.b_ref[2], 4 * n0)) || (e = m.take(m.b_ref[3], 32)) ||
-      (e = m.take(m.b_ref[4], 4 * na_cap)) || (e = m.take(m.b_ref[5], 4 * na_cap)) ||
-      (e = m.take(m.b_tmp[0], 16 * na_cap)) || (e = m.take(m.b_tmp[1], 4 * na_cap)) ||
-      (e = m.take(m.b_tmp[2], 4 * na_cap)) || (e = m.take(m.b_tmp[3], 4 * na_cap)) ||
-      (e = m.take(m.b_tmp[4], 4 * na_cap)))
+  const int64_t rtiles = (n0 + kRankTile - 1) / kRankTile;
+  const int64_t nc1 = m.ncells + 1, ntiles = (nc1 + kMergeTile - 1) / kMergeTile;
+  if ((e = m.take(m.b_ref[1], 4 * (rtiles + 3))) || (e = m.take(m.b_ref[2], 4 * n0)) ||
+      (e = m.take(m.b_tmp[1], 4 * na_cap)) || (e = m.take(m.b_tmp[2], 4 * na_cap)) ||
+      (e = m.take(m.b_tmp[3], 4 * na_cap)) || (e = m.take(m.b_tmp[4], 4 * na_cap)) ||
+      (e = m.take(m.b_tmp[5], 4 * (ntiles + 1))) || (e = m.take(m.b_tmp[6], 4 * (rtiles + 1))) ||
+      (e = m.take(m.b_ref[0], 16 * (n0 + n1))) || (e = m.take(m.b_start2, sizeof(uint32_t) * nc1)))
     return fail("hipMalloc", e);
-  uint32_t* flag = (uint32_t*)m.b_ref[1].p;
+  uint32_t* tcnt = (uint32_t*)m.b_ref[1].p;  // [rtiles] tile bases, survivors, live additions, edge flag
   uint32_t* rank = (uint32_t*)m.b_ref[2].p;
-  int32_t* bb = (int32_t*)m.b_ref[3].p;
-  uint32_t* aflag = (uint32_t*)m.b_ref[4].p;
-  uint32_t* arank = (uint32_t*)m.b_ref[5].p;
-  float4* acomp = (float4*)m.b_tmp[0].p;
   uint32_t* ak = (uint32_t*)m.b_tmp[1].p;
   uint32_t* sk = (uint32_t*)m.b_tmp[2].p;
   uint32_t* av = (uint32_t*)m.b_tmp[3].p;
   uint32_t* sv = (uint32_t*)m.b_tmp[4].p;
-  // survivor ranks and the live additions' ranks, one readback
-  k_widen_flags<<<grid_blocks(n0), 256, 0, st>>>(m.keep, n0, flag);
-  if (n1) k_widen_flags<<<grid_blocks(n1), 256, 0, st>>>(m.akeep, n1, aflag);
-  if (int rc = scan_launch(flag, rank, n0, st)) return rc;
-  if (n1)
-    if (int rc = scan_launch(aflag, arank, n1, st)) return rc;
-  uint32_t last[4] = {0, 0, 0, 0};
-  if (n1) k_compact4<<<grid_blocks(n1), 256, 0, st>>>(m.add4, aflag, arank, n1, acomp);
-  {
-    const Rb rb[4] = {{&last[0], rank + n0 - 1, 4},
-                      {&last[1], flag + n0 - 1, 4},
-                      {&last[2], arank + (n1 ? n1 - 1 : 0), 4},
-                      {&last[3], aflag + (n1 ? n1 - 1 : 0), 4}};
-    if ((e = readback(st, rb, n1 ? 4 : 2))) return fail("counts", e);
-  }
-  const uint32_t n0p = last[0] + last[1], na = last[2] + last[3];
-  if (na) {
-    // the live additions' box: they must lie a cell inside the kept grid
-    const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
-    int32_t got[8];
-    if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) return fail("box", e);
-    k_bbox4<<<std::min(grid_blocks(na), 512), 256, 0, st>>>(acomp, na, bb);
-    const Rb rb{got, bb, 32};
-    if ((e = readback(st, &rb, 1))) return fail("box", e);
-    if (got[6]) return SLIO_OK;  // non-finite: the sorting rebuild reports it
-    const float o[3] = {g.ox, g.oy, g.oz};
-    const int d[3] = {g.dx, g.dy, g.dz};
-    for (int a = 0; a < 3; ++a)
-      if (!(fkey_inv(got[a]) >= o[a] + g.h && fkey_inv(got[3 + a]) <= o[a] + (float)(d[a] - 1) * g.h))
-        return SLIO_OK;  // an addition near or past the grid's edge: re-grid by sorting
-  }
-  *handled = true;
-  const int64_t n = (int64_t)n0p + na;
-  if ((e = m.take(m.b_ref[0], 16 * std::max<int64_t>(n, 1))) ||
-      (e = m.take(m.b_start2, sizeof(uint32_t) * (m.ncells + 1))))
-    return fail("hipMalloc", e);
+  uint32_t* jt = (uint32_t*)m.b_tmp[5].p;
+  uint32_t* jp = (uint32_t*)m.b_tmp[6].p;
   float4* out = (float4*)m.b_ref[0].p;
   uint32_t* new_start = (uint32_t*)m.b_start2.p;
-  int cbits = 1;
-  while (cbits < 32 && ((int64_t)1 << cbits) < m.ncells) ++cbits;
-  if (na) {
-    k_coarse_keys<<<grid_blocks(na), 256, 0, st>>>(acomp, na, g, ak, av);  // fine cell keys (same formula)
+  k_keep_tiles<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, tcnt);
+  k_tile_scan<<<1, 256, 0, st>>>(tcnt, rtiles);
+  k_keep_rank<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, tcnt, rank);
+  if (n1) {
+    // the live additions must lie a cell inside the kept grid
+    MergeBox bx;
+    const float o[3] = {g.ox, g.oy, g.oz};
+    const int d[3] = {g.dx, g.dy, g.dz};
+    for (int a = 0; a < 3; ++a) {
+      bx.lo[a] = o[a] + g.h;
+      bx.hi[a] = o[a] + (float)(d[a] - 1) * g.h;
+    }
+    k_merge_keys<<<grid_blocks(n1), 256, 0, st>>>(m.add4, m.akeep, n1, g, bx, ak, av, tcnt + rtiles + 1);
+    // (stable: a cell's additions stay in id order; the dead ones sort last)
     size_t tb = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ak, sk, av, sv, (int)na, 0, cbits, st)) ||
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ak, sk, av, sv, (int)n1, 0, 32, st)) ||
         (e = m.take(m.b_tmp[7], tb)))
       return fail("sort size", e);
     tb = m.b_tmp[7].cap;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(m.b_tmp[7].p, tb, ak, sk, av, sv, (int)na, 0, cbits, st)))
+    if ((e = hipcub::DeviceRadixSort::SortPairs(m.b_tmp[7].p, tb, ak, sk, av, sv, (int)n1, 0, 32, st)))
       return fail("sort", e);
   }
-  const int64_t nc1 = m.ncells + 1, ntiles = (nc1 + kMergeTile - 1) / kMergeTile;
-  if ((e = m.take(m.b_tmp[5], 4 * (ntiles + 1)))) return fail("hipMalloc", e);
-  uint32_t* jt = (uint32_t*)m.b_tmp[5].p;
-  k_merge_tiles<<<grid_blocks(ntiles + 1), 256, 0, st>>>(sk, na, ntiles, nc1, jt);
-  k_merge_start<<<(unsigned)ntiles, 256, 0, st>>>(m.start, rank, n0, n0p, sk, jt, nc1, new_start);
-  k_merge_pts<<<grid_blocks(n0), 256, 0, st>>>(m.pts, m.keep, rank, m.start, new_start, n0, g, out);
-  if (na) k_merge_adds<<<grid_blocks(na), 256, 0, st>>>(acomp, sk, sv, na, new_start, out);
+  k_merge_tiles<<<grid_blocks(ntiles + 1), 256, 0, st>>>(sk, (uint32_t)n1, ntiles, nc1, jt);
+  k_merge_start<<<(unsigned)ntiles, 256, 0, st>>>(m.start, rank, n0, tcnt + rtiles, sk, jt, nc1, new_start);
+  k_merge_ptiles<<<grid_blocks(rtiles + 1), 256, 0, st>>>(m.pts, rtiles, g, sk, (uint32_t)n1, jp);
+  k_merge_pts<<<(unsigned)rtiles, 256, 0, st>>>(m.pts, m.keep, rank, sk, jp, n0, g, out);
+  if (n1) k_merge_adds<<<grid_blocks(n1), 256, 0, st>>>(m.add4, sk, sv, (uint32_t)n1, new_start, out);
   if ((e = hipGetLastError())) return fail("merge kernels", e);
+  uint32_t cnt[3] = {0, 0, 0};
+  {
+    const Rb rb{cnt, tcnt + rtiles, 12};
+    if ((e = readback(st, &rb, 1))) return fail("counts", e);
+  }
+  if (cnt[2]) return SLIO_OK;  // an addition near or past the grid's edge (or non-finite): re-grid by sorting
+  const uint32_t n0p = cnt[0], na = cnt[1];
+  *handled = true;
+  const int64_t n = (int64_t)n0p + na;
   // new views: points and cell table swap buffers with their temporaries
   std::swap(m.b_pts, m.b_ref[0]);
   std::swap(m.b_start, m.b_start2);
@@ -6171,11 +6311,11 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   m.n = n;
   if ((e = m.take(m.b_keep, std::max<int64_t>(n, 1)))) return fail("hipMalloc", e);
   m.keep = (uint8_t*)m.b_keep.p;
-  k_fill_u8<<<grid_blocks(n), 256, 0, st>>>(m.keep, n, 1);
+  if ((e = hipMemsetAsync(m.keep, 1, n, st))) return fail("keep", e);
   // coarse level: the boxes widened by the additions (deleted points leave
   // them conservative); the points themselves are the fine runs
-  if (na) k_coarse_extend<<<grid_blocks(na), 256, 0, st>>>(acomp, na, g, m.clo, m.chi, m.cg);
-  if ((e = hipGetLastError()) || (e = spin_sync(st))) return fail("coarse kernels", e);
+  if (na) k_coarse_extend<<<grid_blocks(n1), 256, 0, st>>>(m.add4, m.akeep, n1, g, m.clo, m.chi, m.cg);
+  if ((e = hipGetLastError())) return fail("coarse kernels", e);
   m.blk = nullptr;
   m.bstart = nullptr;
   m.nblk = 0;
