@@ -5506,6 +5506,19 @@ __global__ void k_ds_hash(const float4* __restrict__ in, int64_t n, float ds, in
   if (pos < (uint32_t)kDsInline) hmem[h * kDsInline + pos] = (uint32_t)i;
 }
 
+// the hash table emptied, survivor flags and counters zeroed: one launch
+// (four fills were four launches in a row)
+__global__ void k_ds_init(uint64_t* __restrict__ hkey, uint32_t* __restrict__ hcnt, int64_t H,
+                          uint32_t* __restrict__ surv, int64_t n, unsigned long long* __restrict__ dcount) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = i0; i < H; i += st) {
+    hkey[i] = kDsEmpty;
+    hcnt[i] = 0;
+  }
+  for (int64_t i = i0; i < n; i += st) surv[i] = 0;
+  if (i0 < 3) dcount[i0] = 0;
+}
+
 // one thread per occupied slot: its members sorted into list order, then
 // ds_group
 __global__ void k_ds_groups_hash(const float4* __restrict__ in, int64_t n, float ds, int hb,
@@ -5869,16 +5882,18 @@ static int map_add_hashed(Ctx& c, const float4* in, int64_t n, float ds, int64_t
   uint32_t* surv = (uint32_t*)B[4].p;
   uint32_t* rank = (uint32_t*)B[5].p;
   unsigned long long* dcount = (unsigned long long*)B[6].p;
-  if ((e = hipMemsetAsync(hkey, 0xFF, 8 * H, st)) || (e = hipMemsetAsync(hcnt, 0, 4 * H, st)) ||
-      (e = hipMemsetAsync(surv, 0, 4 * n, st)) || (e = hipMemsetAsync(dcount, 0, 24, st))) {
-    set_error(std::string("slio map: memset: ") + hipGetErrorString(e));
-    return SLIO_EDEVICE;
-  }
+  // room for every point up front: the survivors are appended (past m.nadd)
+  // before the readback that counts them
+  if (int rc = add_reserve(m, n, st)) return rc;
+  k_ds_init<<<grid_blocks(std::max<int64_t>(H, n)), 256, 0, st>>>(hkey, hcnt, H, surv, n, dcount);
   k_ds_hash<<<grid_blocks(n), 256, 0, st>>>(in, n, ds, hb, hkey, hcnt, hmem, dcount + 2);
   k_ds_groups_hash<<<grid_blocks(H), 256, 0, st>>>(in, n, ds, hb, hkey, hcnt, hmem, map_view(m), m.keep, surv,
                                                    dcount);
-  // the survivors' ranks, then their total and the counters in one readback
+  // the survivors' ranks and their append, then their total and the
+  // counters in one readback (a key out of range: nothing was appended past
+  // m.nadd that counts, and no flag changed)
   if (int rc = scan_launch(surv, rank, n, st)) return rc;
+  k_append<<<grid_blocks(n), 256, 0, st>>>(in, surv, rank, n, m.add4, m.akeep, m.nadd, m.next_id);
   uint32_t last[2] = {0, 0};
   unsigned long long ops[3] = {0, 0, 0};
   const Rb rb[3] = {{&last[0], rank + n - 1, 4}, {&last[1], surv + n - 1, 4}, {ops, dcount, 24}};
@@ -5892,8 +5907,6 @@ static int map_add_hashed(Ctx& c, const float4* in, int64_t n, float ds, int64_t
     return SLIO_OK;
   }
   *counter = (int64_t)ops[0];
-  if (int rc = add_reserve(m, total, st)) return rc;
-  k_append<<<grid_blocks(n), 256, 0, st>>>(in, surv, rank, n, m.add4, m.akeep, m.nadd, m.next_id);
   if ((e = hipGetLastError())) {
     set_error(std::string("slio map: append: ") + hipGetErrorString(e));
     return SLIO_EDEVICE;
@@ -6707,7 +6720,7 @@ int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_
       if ((rc = map_add(c, l1, na, true, (float)filter_size_map_min, &cnt))) break;
       if ((rc = map_add(c, l2, nn, false, (float)filter_size_map_min, &cnt2))) break;
       out[2] = cnt;
-      SLIO_HIP(hipStreamSynchronize(c.stream));
+      SLIO_HIP(spin_sync(c.stream));
     } while (0);
     if (int rc2 = map_write_end(c); rc2 && !rc) rc = rc2;
     if (rc) return rc;
