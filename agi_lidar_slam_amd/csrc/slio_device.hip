@@ -224,7 +224,7 @@ struct MapDev {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf b_pts, b_keep, b_start, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6], b_add[8], b_start2;
+  Buf b_pts, b_keep, b_start, b_clo, b_chi, b_bstart, b_blk, b_tmp[8], b_ref[6], b_add[8], b_start2, b_keep2;
   static hipError_t take(Buf& b, size_t bytes) {
     bytes = std::max<size_t>(bytes, 16);
     if (bytes <= b.cap) return hipSuccess;
@@ -253,7 +253,7 @@ struct MapDev {
   }
   ~MapDev() {
     if (ready) (void)hipEventDestroy(ready);
-    for (Buf* b : {&b_pts, &b_keep, &b_start, &b_clo, &b_chi, &b_bstart, &b_blk, &b_start2})
+    for (Buf* b : {&b_pts, &b_keep, &b_start, &b_clo, &b_chi, &b_bstart, &b_blk, &b_start2, &b_keep2})
       if (b->p) (void)hipFree(b->p);
     for (Buf& b : b_tmp)
       if (b.p) (void)hipFree(b.p);
@@ -4733,39 +4733,33 @@ __device__ __forceinline__ uint32_t block_excl_256(uint32_t v, uint32_t* total) 
   __syncthreads();
   return off + s - v;
 }
-__global__ __launch_bounds__(256) void k_keep_tiles(const uint8_t* __restrict__ keep, int64_t n,
+// tcnt[t] = tile t's survivors; tcnt[nt + 1], tcnt[nt + 2] zeroed (k_merge_keys'
+// live count and edge flag)
+__global__ __launch_bounds__(256) void k_keep_tiles(const uint8_t* __restrict__ keep, int64_t n, int64_t nt,
                                                     uint32_t* __restrict__ tcnt) {
   const uint4 v = load_keep16(keep, (int64_t)blockIdx.x * kRankTile + threadIdx.x * 16, n);
   const uint32_t c = __popc(nz_bytes(v.x)) + __popc(nz_bytes(v.y)) + __popc(nz_bytes(v.z)) + __popc(nz_bytes(v.w));
   uint32_t tot;
   (void)block_excl_256(c, &tot);
   if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
+  if (blockIdx.x == 0 && threadIdx.x < 2) tcnt[nt + 1 + threadIdx.x] = 0;
 }
-// in place: tcnt[0..nt) -> exclusive prefix, tcnt[nt] = the total (one workgroup)
-__global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tcnt, int64_t nt) {
-  const int64_t per = (nt + 255) / 256, a = min((int64_t)threadIdx.x * per, nt), b = min(a + per, nt);
-  uint32_t s = 0;
-  for (int64_t i = a; i < b; ++i) s += tcnt[i];
-  uint32_t tot;
-  uint32_t run = block_excl_256(s, &tot);
-  for (int64_t i = a; i < b; ++i) {
-    const uint32_t v = tcnt[i];
-    tcnt[i] = run;
-    run += v;
-  }
-  if (threadIdx.x == 0) {
-    tcnt[nt] = tot;
-    tcnt[nt + 1] = 0;  // (k_merge_keys' live count and edge flag)
-    tcnt[nt + 2] = 0;
-  }
-}
-__global__ __launch_bounds__(256) void k_keep_rank(const uint8_t* __restrict__ keep, int64_t n,
-                                                   const uint32_t* __restrict__ tbase, uint32_t* __restrict__ rank) {
+// rank[i] = survivors before i: the tile's base summed by the workgroup from
+// the tile counts before it (L2-resident: no separate scan launch), the last
+// tile also writes the total to tcnt[nt]
+__global__ __launch_bounds__(256) void k_keep_rank(const uint8_t* __restrict__ keep, int64_t n, int64_t nt,
+                                                   uint32_t* __restrict__ tcnt, uint32_t* __restrict__ rank) {
   const int64_t i0 = (int64_t)blockIdx.x * kRankTile + threadIdx.x * 16;
   const uint4 v = load_keep16(keep, i0, n);
+  uint32_t bs = 0;
+  for (int64_t t = threadIdx.x; t < (int64_t)blockIdx.x; t += 256) bs += tcnt[t];
+  uint32_t base;
+  (void)block_excl_256(bs, &base);
   const uint32_t m[4] = {nz_bytes(v.x), nz_bytes(v.y), nz_bytes(v.z), nz_bytes(v.w)};
   const uint32_t c = __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
-  uint32_t r = tbase[blockIdx.x] + block_excl_256(c, nullptr);
+  uint32_t tot;
+  uint32_t r = base + block_excl_256(c, &tot);
+  if (blockIdx.x == nt - 1 && threadIdx.x == 0) tcnt[nt] = base + tot;
   uint32_t o[16];
 #pragma unroll
   for (int b = 0; b < 16; ++b) {
@@ -5482,11 +5476,14 @@ __global__ void k_ds_groups(const float4* __restrict__ in, const uint64_t* __res
 // kernel): the caller then takes the sorting path.
 constexpr int kDsInline = 16;
 constexpr uint64_t kDsEmpty = ~0ull;
+// (nl: when set, the list holds nl[0] + nl[1] points -- an exclusive scan's
+// last rank and flag -- of the n it has room for)
 __global__ void k_ds_hash(const float4* __restrict__ in, int64_t n, float ds, int hb, uint64_t* __restrict__ hkey,
                           uint32_t* __restrict__ hcnt, uint32_t* __restrict__ hmem,
-                          unsigned long long* __restrict__ flag) {
+                          unsigned long long* __restrict__ flag, const uint32_t* __restrict__ nl_rank = nullptr,
+                          const uint32_t* __restrict__ nl_flag = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= (nl_rank ? (int64_t)(*nl_rank + *nl_flag) : n)) return;
   const float4 p = in[i];
   const int64_t kx = (int64_t)floorf(p.x / ds), ky = (int64_t)floorf(p.y / ds), kz = (int64_t)floorf(p.z / ds);
   constexpr int64_t kLim = (1 << 20) - 1;
@@ -5567,6 +5564,32 @@ __global__ void k_append(const float4* __restrict__ in, const uint32_t* __restri
   const float4 p = in[i];
   add4[base + r] = make_float4(p.x, p.y, p.z, __uint_as_float(next_id + r));
   akeep[base + r] = 1;
+}
+
+// map_incremental's PointNoNeedDownsample after its PointToAdd survivors,
+// both counts on the device: cnt = *cr + *cf points of `in`, placed after
+// the *sr + *sf survivors at add4[base ...] with ids continuing next_id
+__global__ void k_append_after(const float4* __restrict__ in, int64_t n, const uint32_t* __restrict__ cr,
+                               const uint32_t* __restrict__ cf, const uint32_t* __restrict__ sr,
+                               const uint32_t* __restrict__ sf, float4* __restrict__ add4,
+                               uint8_t* __restrict__ akeep, int64_t base, uint32_t next_id) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || i >= (int64_t)(*cr + *cf)) return;
+  const uint32_t r = *sr + *sf + (uint32_t)i;
+  const float4 p = in[i];
+  add4[base + r] = make_float4(p.x, p.y, p.z, __uint_as_float(next_id + r));
+  akeep[base + r] = 1;
+}
+// the six scan totals (rank + flag of the last entry) map_incremental reads back
+__global__ void k_inc_counts(const uint32_t* __restrict__ a0, const uint32_t* __restrict__ a1,
+                             const uint32_t* __restrict__ b0, const uint32_t* __restrict__ b1,
+                             const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1,
+                             uint32_t* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    out[0] = *a0 + *a1;
+    out[1] = *b0 + *b1;
+    out[2] = *c0 + *c1;
+  }
 }
 
 // pointBodyToWorld (laserMapping.cpp:276-287) with the rotation matrices
@@ -6096,15 +6119,6 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__
   }
   return lo;
 }
-// jt[t] = lb(t * kMergeTile), t <= ntiles: every tile's first addition, one
-// thread per tile (a per-workgroup search at the head of k_merge_start put
-// ~15 dependent loads in front of every tile: 294 us for the 10M map's grid)
-__global__ void k_merge_tiles(const uint32_t* __restrict__ sk, uint32_t na, int64_t ntiles, int64_t ncells1,
-                              uint32_t* __restrict__ jt) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > ntiles) return;
-  jt[t] = lower_bound_u32(sk, 0, na, (uint32_t)min(t * (int64_t)kMergeTile, ncells1));
-}
 __global__ __launch_bounds__(256) void k_merge_start(const uint32_t* __restrict__ old_start,
                                                      const uint32_t* __restrict__ rank, int64_t n0,
                                                      const uint32_t* __restrict__ n0p_p,
@@ -6156,9 +6170,19 @@ __device__ __forceinline__ uint32_t map_cell(const float4& v, const GridGeom& g)
 // jp[t] = lb(cell of point t * kRankTile), t < ntiles; jp[ntiles] = na.  The
 // stored points are in cell order, so a point p of tile t in cell c has
 // jp[t] <= lb(c) <= jp[t + 1]
+// (and in the same launch jt[t] = lb(t * kMergeTile), t <= ctiles: every
+// cell tile's first addition for k_merge_start, one thread per tile -- a
+// per-workgroup search at the head of k_merge_start put ~15 dependent loads
+// in front of every tile: 294 us for the 10M map's grid)
 __global__ void k_merge_ptiles(const float4* __restrict__ pts, int64_t ntiles, GridGeom g,
-                               const uint32_t* __restrict__ sk, uint32_t na, uint32_t* __restrict__ jp) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                               const uint32_t* __restrict__ sk, uint32_t na, uint32_t* __restrict__ jp,
+                               int64_t ctiles, int64_t ncells1, uint32_t* __restrict__ jt) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t <= ctiles) {
+    jt[t] = lower_bound_u32(sk, 0, na, (uint32_t)min(t * (int64_t)kMergeTile, ncells1));
+    return;
+  }
+  t -= ctiles + 1;
   if (t > ntiles) return;
   jp[t] = t == ntiles ? na : lower_bound_u32(sk, 0, na, map_cell(pts[t * kRankTile], g));
 }
@@ -6171,7 +6195,7 @@ __global__ void k_merge_ptiles(const float4* __restrict__ pts, int64_t ntiles, G
 __global__ __launch_bounds__(256) void k_merge_pts(const float4* __restrict__ pts, const uint8_t* __restrict__ keep,
                                                    const uint32_t* __restrict__ rank, const uint32_t* __restrict__ sk,
                                                    const uint32_t* __restrict__ jp, int64_t n0, GridGeom g,
-                                                   float4* __restrict__ out) {
+                                                   float4* __restrict__ out, uint8_t* __restrict__ okeep) {
   constexpr int kPer = kRankTile / 256, kLds = 1024;
   __shared__ uint32_t lk[kLds];
   const int64_t p0 = (int64_t)blockIdx.x * kRankTile + threadIdx.x;
@@ -6203,6 +6227,7 @@ __global__ __launch_bounds__(256) void k_merge_pts(const float4* __restrict__ pt
         hi = mid;
     }
     out[r[u] + j0 + lo] = v[u];
+    okeep[r[u] + j0 + lo] = 1;
   }
 }
 // the additions' fine cell keys, dead ones keyed kDeadKey (sorted after
@@ -6235,13 +6260,14 @@ __global__ __launch_bounds__(256) void k_merge_keys(const float4* __restrict__ a
 }
 __global__ void k_merge_adds(const float4* __restrict__ adds, const uint32_t* __restrict__ sk,
                              const uint32_t* __restrict__ sv, uint32_t na, const uint32_t* __restrict__ new_start,
-                             float4* __restrict__ out) {
+                             float4* __restrict__ out, uint8_t* __restrict__ okeep) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= na) return;
   const uint32_t c = sk[j];
   if (c == kDeadKey) return;
   const uint32_t e = lower_bound_u32(sk, j, na, c + 1);
   out[new_start[c + 1] - (e - j)] = adds[sv[j]];
+  okeep[new_start[c + 1] - (e - j)] = 1;
 }
 
 // The merge rebuild (see k_merge_start) of m: *handled = false when the
@@ -6267,7 +6293,8 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
       (e = m.take(m.b_tmp[1], 4 * na_cap)) || (e = m.take(m.b_tmp[2], 4 * na_cap)) ||
       (e = m.take(m.b_tmp[3], 4 * na_cap)) || (e = m.take(m.b_tmp[4], 4 * na_cap)) ||
       (e = m.take(m.b_tmp[5], 4 * (ntiles + 1))) || (e = m.take(m.b_tmp[6], 4 * (rtiles + 1))) ||
-      (e = m.take(m.b_ref[0], 16 * (n0 + n1))) || (e = m.take(m.b_start2, sizeof(uint32_t) * nc1)))
+      (e = m.take(m.b_ref[0], 16 * (n0 + n1))) || (e = m.take(m.b_start2, sizeof(uint32_t) * nc1)) ||
+      (e = m.take(m.b_keep2, n0 + n1)))
     return fail("hipMalloc", e);
   uint32_t* tcnt = (uint32_t*)m.b_ref[1].p;  // [rtiles] tile bases, survivors, live additions, edge flag
   uint32_t* rank = (uint32_t*)m.b_ref[2].p;
@@ -6279,9 +6306,8 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   uint32_t* jp = (uint32_t*)m.b_tmp[6].p;
   float4* out = (float4*)m.b_ref[0].p;
   uint32_t* new_start = (uint32_t*)m.b_start2.p;
-  k_keep_tiles<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, tcnt);
-  k_tile_scan<<<1, 256, 0, st>>>(tcnt, rtiles);
-  k_keep_rank<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, tcnt, rank);
+  k_keep_tiles<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, rtiles, tcnt);
+  k_keep_rank<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, rtiles, tcnt, rank);
   if (n1) {
     // the live additions must lie a cell inside the kept grid
     MergeBox bx;
@@ -6301,11 +6327,17 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
     if ((e = hipcub::DeviceRadixSort::SortPairs(m.b_tmp[7].p, tb, ak, sk, av, sv, (int)n1, 0, 32, st)))
       return fail("sort", e);
   }
-  k_merge_tiles<<<grid_blocks(ntiles + 1), 256, 0, st>>>(sk, (uint32_t)n1, ntiles, nc1, jt);
+  uint8_t* okeep = (uint8_t*)m.b_keep2.p;
+  k_merge_ptiles<<<grid_blocks(ntiles + rtiles + 2), 256, 0, st>>>(m.pts, rtiles, g, sk, (uint32_t)n1, jp, ntiles,
+                                                                    nc1, jt);
   k_merge_start<<<(unsigned)ntiles, 256, 0, st>>>(m.start, rank, n0, tcnt + rtiles, sk, jt, nc1, new_start);
-  k_merge_ptiles<<<grid_blocks(rtiles + 1), 256, 0, st>>>(m.pts, rtiles, g, sk, (uint32_t)n1, jp);
-  k_merge_pts<<<(unsigned)rtiles, 256, 0, st>>>(m.pts, m.keep, rank, sk, jp, n0, g, out);
-  if (n1) k_merge_adds<<<grid_blocks(n1), 256, 0, st>>>(m.add4, sk, sv, (uint32_t)n1, new_start, out);
+  k_merge_pts<<<(unsigned)rtiles, 256, 0, st>>>(m.pts, m.keep, rank, sk, jp, n0, g, out, okeep);
+  if (n1) k_merge_adds<<<grid_blocks(n1), 256, 0, st>>>(m.add4, sk, sv, (uint32_t)n1, new_start, out, okeep);
+  // coarse level: the boxes widened by the additions (deleted points leave
+  // them conservative); the points themselves are the fine runs.  In place
+  // before the readback: a declined merge re-grids by sorting, which builds
+  // the coarse level anew
+  if (n1) k_coarse_extend<<<grid_blocks(n1), 256, 0, st>>>(m.add4, m.akeep, n1, g, m.clo, m.chi, m.cg);
   if ((e = hipGetLastError())) return fail("merge kernels", e);
   uint32_t cnt[3] = {0, 0, 0};
   {
@@ -6322,13 +6354,8 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   m.pts = (float4*)m.b_pts.p;
   m.start = (uint32_t*)m.b_start.p;
   m.n = n;
-  if ((e = m.take(m.b_keep, std::max<int64_t>(n, 1)))) return fail("hipMalloc", e);
+  std::swap(m.b_keep, m.b_keep2);  // (set by k_merge_pts / k_merge_adds)
   m.keep = (uint8_t*)m.b_keep.p;
-  if ((e = hipMemsetAsync(m.keep, 1, n, st))) return fail("keep", e);
-  // coarse level: the boxes widened by the additions (deleted points leave
-  // them conservative); the points themselves are the fine runs
-  if (na) k_coarse_extend<<<grid_blocks(n1), 256, 0, st>>>(m.add4, m.akeep, n1, g, m.clo, m.chi, m.cg);
-  if ((e = hipGetLastError())) return fail("coarse kernels", e);
   m.blk = nullptr;
   m.bstart = nullptr;
   m.nblk = 0;
@@ -6635,6 +6662,74 @@ int slio_map_delete_boxes(slio_handle h, const float* boxes, int64_t nboxes, int
   return map_write_end(c);
 }
 
+// map_incremental's two Add_Points in one stream of launches with ONE
+// readback (exact hash boxes, nothing pending in the index): the lists'
+// counts, the survivors and the counters stay on the device until the end,
+// where the classify counts used to be read back first and the appends
+// launched after.  *fallback: a voxel key outside ds_key's range (nothing
+// added, no flag changed): the caller takes the per-call path.
+static int map_incremental_hashed(Ctx& c, const float4* w4, uint32_t* fa, uint32_t* fn, uint32_t* ra,
+                                  uint32_t* rn, float4* l1, float4* l2, int64_t n, float ds, int64_t out[3],
+                                  bool* fallback) {
+  MapDev& m = *c.map;
+  hipStream_t st = c.stream;
+  *fallback = false;
+  const int nb = grid_blocks(n);
+  if (int rc = scan_launch(fa, ra, n, st)) return rc;
+  if (int rc = scan_launch(fn, rn, n, st)) return rc;
+  k_compact4<<<nb, 256, 0, st>>>(w4, fa, ra, n, l1);
+  k_compact4<<<nb, 256, 0, st>>>(w4, fn, rn, n, l2);
+  int hb = 10;
+  while (((int64_t)1 << hb) < 2 * n) ++hb;
+  const int64_t H = (int64_t)1 << hb;
+  auto& B = m.b_add;
+  hipError_t e;
+  if ((e = m.take(B[0], 8 * H)) || (e = m.take(B[1], 4 * H)) || (e = m.take(B[2], 4 * kDsInline * H)) ||
+      (e = m.take(B[4], 4 * n)) || (e = m.take(B[5], 4 * n)) || (e = m.take(B[6], 64))) {
+    set_error(std::string("slio map: hipMalloc: ") + hipGetErrorString(e));
+    return SLIO_ENOMEM;
+  }
+  uint64_t* hkey = (uint64_t*)B[0].p;
+  uint32_t* hcnt = (uint32_t*)B[1].p;
+  uint32_t* hmem = (uint32_t*)B[2].p;
+  uint32_t* surv = (uint32_t*)B[4].p;
+  uint32_t* rank = (uint32_t*)B[5].p;
+  unsigned long long* dcount = (unsigned long long*)B[6].p;  // [0, 24): ops, -, out of range; [24, 36): counts
+  uint32_t* cnt = (uint32_t*)((char*)B[6].p + 24);
+  if (int rc = add_reserve(m, 2 * n, st)) return rc;
+  k_ds_init<<<grid_blocks(std::max<int64_t>(H, n)), 256, 0, st>>>(hkey, hcnt, H, surv, n, dcount);
+  k_ds_hash<<<nb, 256, 0, st>>>(l1, n, ds, hb, hkey, hcnt, hmem, dcount + 2, ra + n - 1, fa + n - 1);
+  k_ds_groups_hash<<<grid_blocks(H), 256, 0, st>>>(l1, n, ds, hb, hkey, hcnt, hmem, map_view(m), m.keep, surv,
+                                                   dcount);
+  if (int rc = scan_launch(surv, rank, n, st)) return rc;
+  k_append<<<nb, 256, 0, st>>>(l1, surv, rank, n, m.add4, m.akeep, m.nadd, m.next_id);
+  k_append_after<<<nb, 256, 0, st>>>(l2, n, rn + n - 1, fn + n - 1, rank + n - 1, surv + n - 1, m.add4, m.akeep,
+                                     m.nadd, m.next_id);
+  k_inc_counts<<<1, 64, 0, st>>>(ra + n - 1, fa + n - 1, rn + n - 1, fn + n - 1, rank + n - 1, surv + n - 1, cnt);
+  unsigned long long got[5];  // ops, -, out of range, then the three counts as 32-bit words
+  {
+    const Rb rb{got, dcount, 36};
+    if ((e = hipGetLastError()) || (e = readback(st, &rb, 1))) {
+      set_error(std::string("slio_map_incremental: ") + hipGetErrorString(e));
+      return SLIO_EDEVICE;
+    }
+  }
+  if (got[2]) {
+    *fallback = true;
+    return SLIO_OK;
+  }
+  uint32_t k3[3];
+  std::memcpy(k3, &got[3], 12);
+  const uint32_t na = k3[0], nn = k3[1], total = k3[2];
+  out[0] = na;
+  out[1] = nn;
+  out[2] = (int64_t)got[0];
+  m.nadd += (int64_t)total + nn;
+  m.next_id += total + nn;
+  if (na || nn) m.dirty = true;  // deletions (keep flags) and / or additions (as the per-call path)
+  return SLIO_OK;
+}
+
 int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_map_min, int ekf_inited,
                          int64_t counts[3]) {
   SLIO_CHECK_H(h);
@@ -6710,6 +6805,18 @@ int slio_map_incremental(slio_handle h, const slio_state* x, double filter_size_
       const int nb = grid_blocks(n);
       k_map_classify<<<nb, 256, 0, c.stream>>>(c.bx, c.by, c.bz, n, W, c.nbr_pos, c.map->pts,
                                                filter_size_map_min, ekf_inited, w4, fa, fn);
+      {
+        MapDev& m = *c.map;
+        const float ds = (float)filter_size_map_min;
+        int ds_exp = 0;
+        const char* nh = std::getenv("SLIO_NO_DS_HASH");
+        if (!(nh && nh[0] && nh[0] != '0') && std::frexp(ds, &ds_exp) == 0.5f && ds <= 1.0f &&
+            !(m.dirty && m.nadd > 0) && (int64_t)m.next_id + 2 * n < (int64_t)0x7FFFFFFF) {
+          bool fallback = false;
+          if ((rc = map_incremental_hashed(c, w4, fa, fn, ra, rn, l1, l2, n, ds, out, &fallback))) break;
+          if (!fallback) break;
+        }
+      }
       uint32_t na = 0, nn = 0;
       if ((rc = scan_flags2(fa, ra, fn, rn, n, c.stream, &na, &nn))) break;
       k_compact4<<<nb, 256, 0, c.stream>>>(w4, fa, ra, n, l1);
