@@ -196,6 +196,9 @@ struct MapDev {
   uint8_t* akeep = nullptr;
   int64_t nadd = 0, add_cap = 0;
   uint32_t next_id = 0;
+  // stored points deleted since the coarse boxes were last made tight (merge
+  // rebuilds only widen them): past n / kCoarseRetighten they are rebuilt
+  int64_t del_loose = 0;
   std::atomic<uint64_t> version{1};  // bumped by every rebuild (positions change)
   std::atomic<bool> dirty{false};
   // block rows of a rebuilt map are built once it has been searched
@@ -5007,6 +5010,7 @@ static int build_index(MapDev& m, const float4* in, int64_t n, const float mn[3]
     k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, cg, m.nccells, cnt);
     k_coarse_boxes<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, cg, cnt, m.nccells, m.clo,
                                                                    m.chi);
+    m.del_loose = 0;
     if ((e = hipGetLastError()) || (e = hipStreamSynchronize(st))) {
       rc = fail("build kernels", e);
       break;
@@ -6107,7 +6111,8 @@ static int map_add(Ctx& c, const float4* in, int64_t n, bool downsample, float d
 //   addition j, cell c -> new_start[c + 1] - (lb(c + 1) - j)
 // (rank(n0) = the survivor count).  Bit-identical to the sort: same points,
 // same order, same cell table.
-constexpr int kMergeTile = 4096;  // cells per workgroup of k_merge_start (256 threads x 16)
+constexpr int kMergeTile = 4096;
+constexpr int64_t kCoarseRetighten = 16;  // cells per workgroup of k_merge_start (256 threads x 16)
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t lo, uint32_t hi,
                                                     uint32_t v) {
   while (lo < hi) {
@@ -6356,6 +6361,18 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   m.n = n;
   std::swap(m.b_keep, m.b_keep2);  // (set by k_merge_pts / k_merge_adds)
   m.keep = (uint8_t*)m.b_keep.p;
+  // the boxes only widen through merges: once the deletions since they were
+  // tight pass n / kCoarseRetighten, the coarse level is rebuilt from the new
+  // cell table -- the boxes a sorting rebuild gives
+  m.del_loose += n0 - (int64_t)n0p;
+  if (m.del_loose * kCoarseRetighten > n) {
+    if ((e = m.take(m.b_tmp[6], 4 * (m.nccells + 1)))) return fail("hipMalloc", e);
+    uint32_t* ccnt = (uint32_t*)m.b_tmp[6].p;
+    k_coarse_count<<<grid_blocks(m.nccells), 256, 0, st>>>(m.start, g, m.cg, m.nccells, ccnt);
+    k_coarse_boxes<<<grid_blocks(m.nccells), 256, 0, st>>>(m.pts, m.start, g, m.cg, ccnt, m.nccells, m.clo, m.chi);
+    if ((e = hipGetLastError())) return fail("coarse boxes", e);
+    m.del_loose = 0;
+  }
   m.blk = nullptr;
   m.bstart = nullptr;
   m.nblk = 0;
@@ -6904,6 +6921,26 @@ int slio_dbg_map_raw(slio_handle h, float* xyzw, int64_t cap, int64_t* n) {
   if (cap < c.map->n || (c.map->n > 0 && !xyzw)) return SLIO_ECAPACITY;
   if (c.map->n) {
     SLIO_HIP(hipMemcpyAsync(xyzw, c.map->pts, 16 * c.map->n, hipMemcpyDeviceToHost, c.stream));
+    SLIO_HIP(hipStreamSynchronize(c.stream));
+  }
+  return SLIO_OK;
+}
+
+// test support (not in include/slio.h): the coarse level's boxes, lo then hi
+// (nccells float4 each: x, y, z and the count word), after the pending rebuild
+int slio_dbg_map_coarse(slio_handle h, float* lohi, int64_t cap, int64_t* nccells) {
+  SLIO_CHECK_H(h);
+  Ctx& c = h->c;
+  if (!c.map || !nccells) return SLIO_ESTATE;
+  if (int rc = map_refresh(c)) return rc;
+  std::shared_lock<std::shared_mutex> lk(c.map->mu);
+  if (int rc = map_read_sync(c)) return rc;
+  const int64_t nc = c.map->nccells;
+  *nccells = nc;
+  if (cap < 2 * nc || (nc > 0 && !lohi)) return SLIO_ECAPACITY;
+  if (nc) {
+    SLIO_HIP(hipMemcpyAsync(lohi, c.map->clo, 16 * nc, hipMemcpyDeviceToHost, c.stream));
+    SLIO_HIP(hipMemcpyAsync(lohi + 4 * nc, c.map->chi, 16 * nc, hipMemcpyDeviceToHost, c.stream));
     SLIO_HIP(hipStreamSynchronize(c.stream));
   }
   return SLIO_OK;

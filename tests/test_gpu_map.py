@@ -470,3 +470,65 @@ def test_merge_rebuild_equals_sort(L, oracle_mod, seed, monkeypatch):
     finally:
         L.load().slio_destroy(hm)
         L.load().slio_destroy(hs)
+
+
+def _coarse(L, h):
+    lib = L.load()
+    nc = C.c_int64()
+    lib.slio_dbg_map_coarse.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+    lib.slio_dbg_map_coarse(h, None, 0, C.byref(nc))   # the size (and the pending rebuild)
+    out = np.zeros((2 * max(nc.value, 1), 4), np.float32)
+    L.check(lib.slio_dbg_map_coarse(h, out.ctypes.data, out.shape[0], C.byref(nc)), "coarse")
+    return out[:2 * nc.value].view(np.uint32)
+
+
+def test_coarse_boxes_retightened_after_deletions(L, oracle_mod, monkeypatch):
+    """Merge rebuilds only widen the coarse boxes (deleted points leave them
+    conservative).  Once the stored points deleted since the boxes were
+    tight pass n / 16, the merge rebuild recomputes the coarse level from the
+    new cell table: the boxes (and counts) of a sorting rebuild, bit for
+    bit, while the index itself still equals the sort's and the oracle's."""
+    rng = np.random.default_rng(7)
+    base = rng.uniform(-20, 20, (60000, 3)).astype(np.float32)
+    base[:, 2] *= 0.2
+    hm = mk(L, n_max=1000, cell=1.0)
+    hs = mk(L, n_max=1000, cell=1.0)
+    om = oracle_mod.Map(base)
+    try:
+        upload_map(L, hm, base)
+        upload_map(L, hs, base)
+
+        def both(fn):
+            monkeypatch.delenv("SLIO_NO_MERGE", raising=False)
+            a = fn(hm)
+            monkeypatch.setenv("SLIO_NO_MERGE", "1")
+            b = fn(hs)
+            monkeypatch.delenv("SLIO_NO_MERGE", raising=False)
+            return a, b
+
+        # a few deletions (below the threshold): the merge keeps widened boxes
+        boxes = np.array([[-3, -3, -2, -1, -1, 2]], np.float32)
+        da, db = both(lambda h: delete(L, h, boxes))
+        assert da == db == om.delete_boxes(boxes)
+        new = (rng.uniform(-18, 18, (500, 3)) * [1, 1, 0.2]).astype(np.float32)
+        assert both(lambda h: add(L, h, new, False)) == (0, 0)
+        om.add_points(new, False, 0.5)
+        np.testing.assert_array_equal(*both(lambda h: _raw(L, h)))
+        ca, cs = both(lambda h: _coarse(L, h))
+        assert ca.shape == cs.shape
+        assert not np.array_equal(ca, cs)   # (deleted points still inside the merged map's boxes)
+        # a quarter of the map deleted: the next merge re-tightens
+        boxes = np.array([[-20, -20, -5, 0, 0, 5]], np.float32)
+        da, db = both(lambda h: delete(L, h, boxes))
+        assert da == db == om.delete_boxes(boxes)
+        assert da * 16 > base.shape[0]
+        new = (rng.uniform(1, 18, (500, 3)) * [1, 1, 0.2]).astype(np.float32)
+        assert both(lambda h: add(L, h, new, False)) == (0, 0)
+        om.add_points(new, False, 0.5)
+        np.testing.assert_array_equal(*both(lambda h: _raw(L, h)))
+        ca, cs = both(lambda h: _coarse(L, h))
+        np.testing.assert_array_equal(ca, cs)
+        assert_same_map(L, hm, om)
+    finally:
+        L.load().slio_destroy(hm)
+        L.load().slio_destroy(hs)
