@@ -3127,6 +3127,174 @@ __global__ __launch_bounds__(256) void k_lego_half(const float4* seg, const int3
   if (threadIdx.x == 0) slot[blockIdx.x] = min(min(wmin[0], wmin[1]), min(wmin[2], wmin[3]));
 }
 
+// k_lego_rowcount + k_lego_extract + k_lego_label + k_lego_half in ONE
+// launch of kLegoRowsSplit workgroups per ring (block b = r S + s takes the
+// ring's s-th column range; all N S <= 1024 blocks resident at once): each
+// block classifies its cells once (root / segmented / outlier, kept in
+// registers), publishes its three counts, waits for the blocks before it (in
+// row-major order) to publish theirs -- a decoupled look-back over blocks
+// dispatched earlier -- and writes its part of the segmented cloud, the
+// outliers and its roots' labelCount numbers (write-through); after a second
+// publication it labels its cells once the earlier blocks' numbers are out (a
+// component's root is its first row-major cell: in this block or an earlier
+// one).  halfPassed's first switch point per block goes to slot[b]
+// (k_lego_deskew takes the minimum).  Flags carry the sweep's sequence number
+// (no reset); a wait gives up after ~0.5 s and marks the sweep failed
+// (n_segmented = -1) instead of hanging.
+// (8 blocks of 256 per ring measured slower: 26.9 vs 21.8 us a VLP-16 sweep --
+// the look-back over 8x the blocks and the phases' round trips dominate)
+constexpr int kLegoRowsSplit = 1;    // blocks per ring
+constexpr int kLegoRowsThreads = 1024;
+constexpr int kLegoRowsPer = 8;      // cells per thread: rings of <= 8192 columns
+__device__ __forceinline__ bool lego_wait_blocks(const uint32_t* flag, int b, uint32_t seq) {
+  bool ok = true;
+  const unsigned long long t0 = wall_clock64();
+  for (int q = threadIdx.x; q < b && ok; q += kLegoRowsThreads)
+    while (__hip_atomic_load(flag + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
+      if (wall_clock64() - t0 > 50000000ull) {  // 100 MHz: 0.5 s
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return __syncthreads_and(ok);
+}
+__global__ __launch_bounds__(kLegoRowsThreads) void k_lego_rows(
+    LGeo g, const int8_t* ground, const int32_t* parent, const int32_t* csize, const unsigned long long* rows,
+    const float* range_mat, const float4* full, int32_t* rootlab, LegoSeg sg, int32_t* label, int32_t* clear,
+    uint32_t* rsync /* [B] ready, [B] done, [3 B] counts */, uint32_t seq, float so, uint32_t* slot,
+    LegoImuOutDev* io, float al0, float al1, float al2) {
+  __shared__ int scratch[kLegoRowsThreads / 64 + 1];
+  __shared__ uint32_t wmin[kLegoRowsThreads / 64];
+  const int b = blockIdx.x, t = threadIdx.x, B = g.N * kLegoRowsSplit;
+  const int r = b / kLegoRowsSplit, sp = b % kLegoRowsSplit;
+  uint32_t* ready = rsync;
+  uint32_t* done = rsync + B;
+  uint32_t* cnt = rsync + 2 * B;
+  if (b == 0 && t == 0) {  // the state adjustDistortion leaves when it writes nothing
+    *io = LegoImuOutDev{};
+    io->ang_last[0] = al0;
+    io->ang_last[1] = al1;
+    io->ang_last[2] = al2;
+  }
+  const int c0 = (int)((int64_t)g.H * sp / kLegoRowsSplit), c1 = (int)((int64_t)g.H * (sp + 1) / kLegoRowsSplit);
+  const int per = (c1 - c0 + kLegoRowsThreads - 1) / kLegoRowsThreads;
+  const int j0 = c0 + t * per, j1 = min(j0 + per, c1);
+  int32_t rt[kLegoRowsPer];
+  uint8_t cls[kLegoRowsPer];  // 1 root, 2 segmented, 4 outlier, 8 feasible root, 16 has a parent
+  int a = 0, bb = 0, d = 0;
+#pragma unroll
+  for (int k = 0; k < kLegoRowsPer; ++k) {
+    const int j = j0 + k;
+    rt[k] = -1;
+    cls[k] = 0;
+    if (j >= j1) continue;
+    const int64_t c = j + (int64_t)r * g.H;
+    const int32_t p = parent[c];
+    const bool gnd = ground[c] == 1;
+    bool positive = false, rejected = false;
+    uint8_t f = 0;
+    if (p >= 0) {
+      rt[k] = uf_find(parent, p);
+      const bool feas = lego_feasible(g, csize, rows, rt[k]);
+      positive = feas;
+      rejected = !feas;
+      f |= 16 | (feas ? 8 : 0) | (feas && rt[k] == c ? 1 : 0);
+    }
+    // lego_cell_class
+    if (positive || rejected || gnd) {
+      if (rejected) {
+        if (r > g.gsi && j % 5 == 0) f |= 4;
+      } else if (!(gnd && j % 5 != 0 && j > 5 && j < g.H - 5)) {
+        f |= 2;
+      }
+    }
+    cls[k] = f;
+    a += f & 1;
+    bb += (f >> 1) & 1;
+    d += (f >> 2) & 1;
+  }
+  int ea, eb, ed;
+  const int ta = block_exclusive_scan<kLegoRowsThreads>(a, scratch, ea);
+  const int tb = block_exclusive_scan<kLegoRowsThreads>(bb, scratch, eb);
+  const int td = block_exclusive_scan<kLegoRowsThreads>(d, scratch, ed);
+  if (t == 0) {
+    __hip_atomic_store(cnt + 3 * b, (uint32_t)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt + 3 * b + 1, (uint32_t)tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt + 3 * b + 2, (uint32_t)td, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ready + b, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  bool ok = lego_wait_blocks(ready, b, seq);
+  int pa = 0, pb = 0, pd = 0;
+  for (int q = t; q < b; q += kLegoRowsThreads) {
+    pa += (int)__hip_atomic_load(cnt + 3 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pb += (int)__hip_atomic_load(cnt + 3 * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pd += (int)__hip_atomic_load(cnt + 3 * q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  int e;
+  const int oa = block_exclusive_scan<kLegoRowsThreads>(pa, scratch, e);
+  const int ob = block_exclusive_scan<kLegoRowsThreads>(pb, scratch, e);
+  const int od = block_exclusive_scan<kLegoRowsThreads>(pd, scratch, e);
+  if (t == 0) {
+    if (sp == 0) sg.start_ring[r] = ob - 1 + 5;
+    if (sp == kLegoRowsSplit - 1) sg.end_ring[r] = ob + tb - 1 - 5;
+    if (b == B - 1) {
+      sg.n[0] = ok ? ob + tb : -1;
+      sg.n[1] = od + td;
+    }
+  }
+  int ka = oa + ea, kb = ob + eb, kd = od + ed;
+  uint32_t sw = kNone;  // halfPassed: the block's first segmented point past the switch
+#pragma unroll
+  for (int k = 0; k < kLegoRowsPer; ++k) {
+    const int j = j0 + k;
+    if (j >= j1) continue;
+    const int64_t c = j + (int64_t)r * g.H;
+    const uint8_t f = cls[k];
+    if (f & 1) __hip_atomic_store(rootlab + c, 1 + ka++, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f & 2) {
+      const float4 q = full[c];
+      sg.ground_flag[kb] = ground[c] == 1;
+      sg.col_ind[kb] = j;
+      sg.range[kb] = range_mat[c];
+      sg.xyzi[kb] = q;
+      bool pass;
+      ori_a(so, q.y, q.x, pass);  // point.x = y, point.z = x
+      if (pass) sw = min(sw, (uint32_t)kb);
+      ++kb;
+    }
+    if (f & 4) sg.outlier[kd++] = full[c];
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sw = min(sw, (uint32_t)__shfl_xor((int)sw, o, 64));
+  if ((t & 63) == 0) wmin[t >> 6] = sw;
+  // every wave's root numbers out (write-through, drained) before "done"
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (t == 0) {
+    uint32_t m = wmin[0];
+    for (int q = 1; q < kLegoRowsThreads / 64; ++q) m = min(m, wmin[q]);
+    slot[b] = m;
+    __hip_atomic_store(done + b, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ok = lego_wait_blocks(done, b, seq) && ok;
+  if (!ok && t == 0) sg.n[0] = -1;
+#pragma unroll
+  for (int k = 0; k < kLegoRowsPer; ++k) {
+    const int j = j0 + k;
+    if (j >= j1) continue;
+    const int64_t c = j + (int64_t)r * g.H;
+    clear[c] = -1;  // the other owner table, for the next sweep
+    const uint8_t f = cls[k];
+    label[c] = !(f & 16) ? -1
+                         : (f & 8) ? (int32_t)__hip_atomic_load(rootlab + rt[k], __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT)
+                                   : 999999;
+  }
+}
+
 struct ImuCur {
   float r, p, y, vx, vy, vz;
   bool after;
@@ -3431,6 +3599,9 @@ struct slio_lego {
   int32_t* csize = nullptr;
   unsigned long long* rows = nullptr;
   int32_t* cnt = nullptr;
+  uint32_t* rsync = nullptr;  // k_lego_rows' flags and counts per block ([B] ready, [B] done, [3 B])
+  uint32_t sweep_seq = 0;
+  bool rows_split = false;    // SLIO_LEGO_ROWS_SPLIT=1: the four-launch row stage (A/B)
   int32_t* rootlab = nullptr;
   int32_t* label = nullptr;
   int32_t *start_ring = nullptr, *end_ring = nullptr, *col_ind = nullptr, *nseg = nullptr;
@@ -3487,7 +3658,7 @@ void lego_free(slio_lego* h) {
                  h->slot, h->desk, h->io, h->curvature, h->picked0, h->flabel, h->corner_stage,
                  h->corner_sharp, h->corner_count, h->sharp_count, h->flat_count, h->surf_count,
                  h->flat_stage, h->surf_stage, h->c_sharp, h->c_less_sharp, h->c_flat,
-                 h->c_less_flat, h->counts, h->seam, h->cc_arrive};
+                 h->c_less_flat, h->counts, h->seam, h->cc_arrive, h->rsync};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   feat_work_free(h->fw);
@@ -3580,6 +3751,7 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   A(h->csize, 4 * C);
   A(h->rows, 16 * C);
   A(h->cnt, 12 * R);
+  A(h->rsync, 20 * R * kLegoRowsSplit);
   A(h->rootlab, 4 * C);
   A(h->label, 4 * C);
   A(h->start_ring, 4 * R);
@@ -3590,7 +3762,7 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   A(h->srange, 4 * C);
   A(h->sxyzi, 16 * C);
   A(h->outlier, 16 * C);
-  A(h->slot, 4 * ((C + 255) / 256 + 1));
+  A(h->slot, 4 * std::max<int64_t>((C + 255) / 256 + 1, R * kLegoRowsSplit));
   A(h->desk, 16 * C);
   A(h->io, sizeof(LegoImuOutDev));
   A(h->curvature, 4 * C);
@@ -3611,6 +3783,7 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
   A(h->counts, 32);
 #undef A
   if (!e) e = hipMemset(h->io, 0, sizeof(LegoImuOutDev));
+  if (!e) e = hipMemset(h->rsync, 0, 20 * R * kLegoRowsSplit);
   if (e) {
     set_error(std::string("slio_lego_create: ") + hipGetErrorString(e));
     lego_free(h);
@@ -3648,6 +3821,8 @@ int slio_lego_create(slio_lego_handle* out, const slio_lego_params* p) {
     h->cc_global = cg && cg[0] && cg[0] != '0';
     const char* c1 = std::getenv("SLIO_LEGO_CC_LDS1");
     h->cc_lds1 = c1 && c1[0] && c1[0] != '0';
+    const char* rs = std::getenv("SLIO_LEGO_ROWS_SPLIT");
+    h->rows_split = rs && rs[0] && rs[0] != '0';
   }
   if (lego_band_ok(h->g)) {
     const int nb = (h->g.H + kLegoBandW - 1) / kLegoBandW;
@@ -3844,21 +4019,31 @@ int slio_lego_run_async(slio_lego_handle h) {
     k_lego_union<<<cb, 256, 0, h->stream>>>(g, h->range_mat, h->parent);
     k_lego_compress<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows);
   }
-  k_lego_rowcount<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
-                                                        h->cnt);
   const LegoSeg sg{h->start_ring, h->end_ring, h->col_ind, h->gflag, h->srange, h->sxyzi,
                    h->outlier, h->nseg};
-  k_lego_extract<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
-                                                       h->cnt, h->range_mat, h->full, h->rootlab, sg);
-  k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label, idle);
+  int nslot = (int)cb;
+  if (!h->rows_split) {
+    if (++h->sweep_seq == 0) h->sweep_seq = 1;
+    k_lego_rows<<<R * kLegoRowsSplit, kLegoRowsThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows, h->range_mat,
+                                                      h->full, h->rootlab, sg, h->label, idle, h->rsync,
+                                                      h->sweep_seq, h->orient[0], h->slot, h->io,
+                                                      h->imu.ang_last[0], h->imu.ang_last[1], h->imu.ang_last[2]);
+    nslot = R * kLegoRowsSplit;
+  } else {
+    k_lego_rowcount<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
+                                                          h->cnt);
+    k_lego_extract<<<R, kLegoRowThreads, 0, h->stream>>>(g, h->ground, h->parent, h->csize, h->rows,
+                                                         h->cnt, h->range_mat, h->full, h->rootlab, sg);
+    k_lego_label<<<cb, 256, 0, h->stream>>>(g, h->parent, h->csize, h->rows, h->rootlab, h->label, idle);
+  }
   if (const hipError_t e = hipGetLastError()) return fail(e);
   h->owner = own;
   h->owner_alt = idle;
   h->swept = true;
   // adjustDistortion
-  const int nslot = (int)cb;
-  k_lego_half<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->orient[0], h->slot, h->io,
-                                          h->imu.ang_last[0], h->imu.ang_last[1], h->imu.ang_last[2]);
+  if (h->rows_split)
+    k_lego_half<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->orient[0], h->slot, h->io,
+                                            h->imu.ang_last[0], h->imu.ang_last[1], h->imu.ang_last[2]);
   k_lego_deskew<<<cb, 256, 0, h->stream>>>(h->sxyzi, h->nseg, h->slot, nslot, h->orient[0],
                                             h->orient[1], h->orient[2], h->prm.scan_period, h->imu,
                                             h->desk, h->io);
