@@ -73,12 +73,16 @@ def check_features(oracle_mod, fe, si, P, imu=None, t0=0.0):
     return got
 
 
-@pytest.mark.parametrize("with_imu,cc", [(False, "band"), (True, "band"), (False, "lds1"), (False, "global")])
+@pytest.mark.parametrize("with_imu,cc", [(False, "band"), (True, "band"), (False, "lds1"), (False, "global"),
+                                         (True, "band-rows-split")])
 def test_vlp16_sweep_bitexact(oracle_mod, with_imu, cc, monkeypatch):
     """cc: labelComponents in 64-column bands with a last-arriver seam merge
     (k_lego_cc_band, the default for <= 64 rows), by the one-workgroup LDS
     union-find (k_lego_cc, SLIO_LEGO_CC_LDS1) or by the global-atomic kernels
-    (SLIO_LEGO_CC_GLOBAL): the same labels."""
+    (SLIO_LEGO_CC_GLOBAL): the same labels.  band-rows-split: the row stage as
+    four launches (SLIO_LEGO_ROWS_SPLIT, the A/B baseline of k_lego_rows)."""
+    if cc == "band-rows-split":
+        monkeypatch.setenv("SLIO_LEGO_ROWS_SPLIT", "1")
     if cc == "global":
         monkeypatch.setenv("SLIO_LEGO_CC_GLOBAL", "1")
     if cc == "lds1":
