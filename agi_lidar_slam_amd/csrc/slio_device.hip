@@ -1588,39 +1588,49 @@ __device__ __forceinline__ uint32_t ld_sys_u32(const uint32_t* p) {
 // Per-point outputs of a pass (plane, selection, residual, neighbour
 // positions, certificates), stored write-through (sc1): they leave no dirty
 // lines in the XCDs' L2s for the end-of-kernel write-back that every pass
-// boundary waits for (SLIO_PLAIN_OUT: plain stores, the A/B baseline)
+// boundary waits for.  SLIO_OUT_MODE (A/B): 0 plain stores, 1 agent-scope
+// atomic stores (16-B values as two 8-B halves), 2 non-temporal stores, 3
+// (default) 16-B values as one global_store_dwordx4 sc1 -- whole lines per
+// wavefront instead of two half-line writes each
+#ifndef SLIO_OUT_MODE
+#define SLIO_OUT_MODE 3
+#endif
 typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out16(void* p, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+#if SLIO_OUT_MODE == 0
+  *reinterpret_cast<uint4*>(p) = make_uint4(x, y, z, w);
+#elif SLIO_OUT_MODE == 1
+  __hip_atomic_store((guint64*)(uint64_t*)p, ((uint64_t)y << 32) | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((guint64*)(uint64_t*)p + 1, ((uint64_t)w << 32) | z, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#elif SLIO_OUT_MODE == 2
+  v4u32 v = {x, y, z, w};
+  __builtin_nontemporal_store(v, reinterpret_cast<v4u32*>(p));
+#else
+  v4u32 v = {x, y, z, w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#endif
+}
 __device__ __forceinline__ void st_out(float4* p, float4 v) {
-#ifdef SLIO_PLAIN_OUT
-  *p = v;
-#else
-  const uint64_t lo = ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
-  const uint64_t hi = ((uint64_t)__float_as_uint(v.w) << 32) | __float_as_uint(v.z);
-  __hip_atomic_store((guint64*)(uint64_t*)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((guint64*)(uint64_t*)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+  st_out16(p, __float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
 }
-__device__ __forceinline__ void st_out(uint4* p, uint4 v) {
-#ifdef SLIO_PLAIN_OUT
-  *p = v;
-#else
-  __hip_atomic_store((guint64*)(uint64_t*)p, ((uint64_t)v.y << 32) | v.x, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((guint64*)(uint64_t*)p + 1, ((uint64_t)v.w << 32) | v.z, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
+__device__ __forceinline__ void st_out(uint4* p, uint4 v) { st_out16(p, v.x, v.y, v.z, v.w); }
 __device__ __forceinline__ void st_out(uint32_t* p, uint32_t v) {
-#ifdef SLIO_PLAIN_OUT
+#if SLIO_OUT_MODE == 0
   *p = v;
+#elif SLIO_OUT_MODE == 2
+  __builtin_nontemporal_store(v, p);
 #else
   __hip_atomic_store((guint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
 }
 __device__ __forceinline__ void st_out(float* p, float v) { st_out(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
 __device__ __forceinline__ void st_out(uint8_t* p, uint8_t v) {
-#ifdef SLIO_PLAIN_OUT
+#if SLIO_OUT_MODE == 0
   *p = v;
+#elif SLIO_OUT_MODE == 2
+  __builtin_nontemporal_store(v, p);
 #else
   __hip_atomic_store((gu8*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif

@@ -1,5 +1,5 @@
 # PMC passes of every kernel of the C3 scan (LIO-SAM, scripts/run_lio.py: 6
-# launches) and of the LeGO sweep (scripts/run_lego.py: 12 launches):
+# launches) and of the LeGO sweep (scripts/run_lego.py: 9 launches):
 # FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md) ->
 # gpurun_out/<tag>_{c3,lego}_traffic.json (per kernel, and summed per scan)
 set -o pipefail
@@ -8,7 +8,7 @@ tag=${1:-pmcfe}
 for W in c3 lego; do
   S=scripts/run_lio.py; [ $W = lego ] && S=scripts/run_lego.py
   K=k_lio_claim,k_lio_fill,k_lio_extract,k_fe_pick,k_fe_ring,k_lio_concat
-  [ $W = lego ] && K=k_lego_claim,k_lego_fill,k_lego_ground,k_lego_cc_band,k_lego_rowcount,k_lego_extract,k_lego_label,k_lego_half,k_lego_deskew,k_fe_pick,k_fe_ring,k_lego_concat
+  [ $W = lego ] && K=k_lego_claim,k_lego_fill,k_lego_ground,k_lego_cc_band,k_lego_rows,k_lego_deskew,k_fe_pick,k_fe_ring,k_lego_concat
   i=0
   for PMC in "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
