@@ -1074,6 +1074,28 @@ def main():
     # multi-rank run be compared with a single-rank one
     import hashlib
     digest = hashlib.sha256(C.string_at(C.addressof(xs), C.sizeof(xs)) + P.tobytes()).hexdigest()[:16]
+    # every iteration's 5 nearest are exact: searched in full, or certified from
+    # the update's earlier search (kNN certificates).  Per pass from updates of
+    # 1 .. maxit passes from the same prior (fixed flow: the same first passes),
+    # after the timed region: the counters cost two atomics per workgroup
+    knn = {"label": "exact 5-NN every iteration (searched or certified)"}
+    if args.mode == "fixed" and not args.host_loop and world == 1 and hasattr(lib, "slio_debug_knn_cert"):
+        cc = (C.c_uint32 * 2)()
+        L.check(lib.slio_debug_knn_cert(h, cc), "knn_cert")
+        cert, srch = [], []
+        for k in range(1, args.iters + 1):
+            it_c.value = k
+            a0, a1 = int(cc[0]), int(cc[1])
+            step()
+            L.check(lib.slio_debug_knn_cert(h, cc), "knn_cert")
+            cert.append((int(cc[0]) - a0) % (1 << 32))
+            srch.append((int(cc[1]) - a1) % (1 << 32))
+        it_c.value = args.iters
+        cert_pass = [cert[0]] + [cert[k] - cert[k - 1] for k in range(1, len(cert))]
+        srch_pass = [srch[0]] + [srch[k] - srch[k - 1] for k in range(1, len(srch))]
+        srch_pass[0] = shard_pts  # pass 0 searches every query (no certificate to use)
+        knn["certified_per_pass"] = cert_pass
+        knn["searched_in_full_per_pass"] = srch_pass
     # HBM bytes per launch from the committed PMC summary (rocprofv3 --pmc
     # cannot run inside this process): only for the same workload, one rank
     # holding the whole scan, and the library built from the same sources
@@ -1167,6 +1189,7 @@ def main():
             "caller": ("native: scripts/bench_loop.c calls slio_ikf_update_device once per step, as "
                        "laserMapping's C++ loop does" if loop is not None else "Python ctypes loop"),
             "python_loop_value": (passes / py_el) if py_el else None,
+            "knn": knn,
         },
         "roofline": {
             "bound": "hbm",
