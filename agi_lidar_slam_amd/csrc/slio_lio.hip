@@ -4070,6 +4070,12 @@ int slio_lego_get_counts(slio_lego_handle h, slio_lego_counts* c) {
   LIO_HIP(hipMemcpyAsync(ns, h->nseg, 8, hipMemcpyDeviceToHost, h->stream));
   LIO_HIP(hipMemcpyAsync(k, h->counts, 32, hipMemcpyDeviceToHost, h->stream));
   LIO_HIP(hipStreamSynchronize(h->stream));
+  if (ns[0] < 0) {
+    // k_lego_rows gave up waiting for an earlier ring's counts (~0.5 s): the
+    // sweep's outputs are void; the next sweep's flags carry a new sequence
+    set_error("slio_lego: the row stage's wait for an earlier ring gave up; this sweep's outputs are void");
+    return SLIO_ETIMEOUT;
+  }
   if (c) {
     c->n_segmented = ns[0];
     c->n_outlier = ns[1];

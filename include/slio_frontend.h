@@ -173,6 +173,9 @@ int slio_lego_set_imu(slio_lego_handle h, const slio_lego_imu* imu);
 int slio_lego_upload(slio_lego_handle h, const float* x, const float* y, const float* z, int64_t n);
 int slio_lego_run_async(slio_lego_handle h);
 int slio_lego_run(slio_lego_handle h, slio_lego_counts* counts);
+/* Waits for the sweep.  SLIO_ETIMEOUT: the row stage's wait for an earlier
+ * ring gave up (~0.5 s; the sweep's outputs are void, the next sweep is not
+ * affected). */
 int slio_lego_get_counts(slio_lego_handle h, slio_lego_counts* counts);
 /* rangeMat, the input index that filled each cell (-1 empty), groundMat, labelMat. */
 int slio_lego_get_image(slio_lego_handle h, float* range_mat, int32_t* cell_point, int8_t* ground,
