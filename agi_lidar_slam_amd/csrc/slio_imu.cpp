@@ -58,7 +58,7 @@ int slio_ikf_predict(slio_state* x, double P[576], double dt, const double Q[144
     f[i + 12] = ai + x->grav[i];
   }
   // df_dx (use-ikfom.hpp:75-96) and df_dw (:105-117), before I + . * dt
-  static thread_local double Fx[576], Fw[288];
+  double Fx[576], Fw[288];
   std::memset(Fx, 0, sizeof Fx);
   std::memset(Fw, 0, sizeof Fw);
   const double hat[9] = {0.0, -am[2], am[1], am[2], 0.0, -am[0], -am[1], am[0], 0.0};
@@ -82,29 +82,105 @@ int slio_ikf_predict(slio_state* x, double P[576], double dt, const double Q[144
   for (int k = 0; k < 24; ++k) fd[k] = f[k] * dt;
   boxplus24(*x, fd);
   // F = I + Fx dt; P = F P F^T + (dt Fw) Q (dt Fw)^T
-  static thread_local double F[576], FP[576], G[288], GQ[288], Pn[576];
+  // Every product element is summed over k in ascending order from 0.0, as
+  // esekf::predict's dense products do, except that terms whose F or G factor
+  // is structurally zero are skipped: F = I + Fx dt has 51 possible non-zeros
+  // of 576 and G = Fw dt 18 of 288 (df_dx / df_dw above).  A sum that starts
+  // at +0.0 is never -0.0 under round-to-nearest (+0 + -0 = +0, x + -x = +0),
+  // so adding a +-0 term leaves it unchanged: the same bits for finite P and
+  // Q (an Inf or NaN in P no longer leaks through a zero factor).
+  double F[576], FP[576], G[288], GQ[288], Pn[576];
   for (int i = 0; i < 24; ++i)
     for (int j = 0; j < 24; ++j) F[i * 24 + j] = (i == j ? 1.0 : 0.0) + Fx[i * 24 + j] * dt;
   for (int k = 0; k < 288; ++k) G[k] = dt * Fw[k];
-  for (int i = 0; i < 24; ++i)
-    for (int j = 0; j < 24; ++j) {
-      double s = 0.0;
-      for (int k = 0; k < 24; ++k) s = s + F[i * 24 + k] * P[k * 24 + j];
-      FP[i * 24 + j] = s;
+  // the structurally non-zero columns of each row of F and G, ascending
+  struct Nz {
+    int fnz[24][8], fn[24], gnz[24][3], gn[24];
+  };
+  static const Nz nzt = [] {
+    Nz z{};
+    for (int i = 0; i < 24; ++i) {
+      int* c = z.fnz[i];
+      int n = 0;
+      if (i < 3) {
+        c[n++] = i;
+        c[n++] = 12 + i;
+      } else if (i < 6) {
+        c[n++] = i;
+        c[n++] = 12 + i;  // 15 + (i - 3)
+      } else if (i >= 12 && i < 15) {
+        for (int j = 3; j < 6; ++j) c[n++] = j;
+        c[n++] = i;
+        for (int j = 18; j < 21; ++j) c[n++] = j;
+        c[n++] = 9 + i;  // 21 + (i - 12)
+      } else {
+        c[n++] = i;
+      }
+      z.fn[i] = n;
+      int m = 0;
+      if (i >= 3 && i < 6) z.gnz[i][m++] = i - 3;
+      if (i >= 12 && i < 15)
+        for (int j = 3; j < 6; ++j) z.gnz[i][m++] = j;
+      if (i >= 15 && i < 18) z.gnz[i][m++] = i - 9;   // 6 + (i - 15)
+      if (i >= 18 && i < 21) z.gnz[i][m++] = i - 9;   // 9 + (i - 18)
+      z.gn[i] = m;
     }
-  for (int i = 0; i < 24; ++i)
-    for (int j = 0; j < 12; ++j) {
-      double s = 0.0;
-      for (int k = 0; k < 12; ++k) s = s + G[i * 12 + k] * Q[k * 12 + j];
-      GQ[i * 12 + j] = s;
+    return z;
+  }();
+  const auto& fnz = nzt.fnz;
+  const auto& fn = nzt.fn;
+  const auto& gnz = nzt.gnz;
+  const auto& gn = nzt.gn;
+  // FP = F P (row i: the rows k of P with F[i][k] != 0, k ascending)
+  for (int i = 0; i < 24; ++i) {
+    double* r = FP + i * 24;
+    for (int j = 0; j < 24; ++j) r[j] = 0.0;
+    for (int t = 0; t < fn[i]; ++t) {
+      const int k = fnz[i][t];
+      const double f = F[i * 24 + k];
+      const double* p = P + k * 24;
+      for (int j = 0; j < 24; ++j) r[j] = r[j] + f * p[j];
     }
-  for (int i = 0; i < 24; ++i)
-    for (int j = 0; j < 24; ++j) {
-      double a = 0.0, b = 0.0;
-      for (int k = 0; k < 24; ++k) a = a + FP[i * 24 + k] * F[j * 24 + k];
-      for (int k = 0; k < 12; ++k) b = b + GQ[i * 12 + k] * G[j * 12 + k];
-      Pn[i * 24 + j] = a + b;
+  }
+  // GQ = G Q
+  for (int i = 0; i < 24; ++i) {
+    double* r = GQ + i * 12;
+    for (int j = 0; j < 12; ++j) r[j] = 0.0;
+    for (int t = 0; t < gn[i]; ++t) {
+      const int k = gnz[i][t];
+      const double gk = G[i * 12 + k];
+      const double* q = Q + k * 12;
+      for (int j = 0; j < 12; ++j) r[j] = r[j] + gk * q[j];
     }
+  }
+  // Pn = FP F^T + GQ G^T.  Element (i, j) sums FP[i][k] F[j][k] over the k of
+  // row j of F (ascending), and GQ[i][k] G[j][k] separately, then adds the
+  // two; computed as column j of Pn from the transposed FP / GQ so the 24
+  // elements of a column go side by side
+  double FPT[576], GQT[288], PnT[576], Bt[24];
+  for (int i = 0; i < 24; ++i) {
+    for (int k = 0; k < 24; ++k) FPT[k * 24 + i] = FP[i * 24 + k];
+    for (int k = 0; k < 12; ++k) GQT[k * 24 + i] = GQ[i * 12 + k];
+  }
+  for (int j = 0; j < 24; ++j) {
+    double* a = PnT + j * 24;
+    for (int i = 0; i < 24; ++i) a[i] = Bt[i] = 0.0;
+    for (int t = 0; t < fn[j]; ++t) {
+      const int k = fnz[j][t];
+      const double f = F[j * 24 + k];
+      const double* c = FPT + k * 24;
+      for (int i = 0; i < 24; ++i) a[i] = a[i] + c[i] * f;
+    }
+    for (int t = 0; t < gn[j]; ++t) {
+      const int k = gnz[j][t];
+      const double gk = G[j * 12 + k];
+      const double* c = GQT + k * 24;
+      for (int i = 0; i < 24; ++i) Bt[i] = Bt[i] + c[i] * gk;
+    }
+    for (int i = 0; i < 24; ++i) a[i] = a[i] + Bt[i];
+  }
+  for (int i = 0; i < 24; ++i)
+    for (int j = 0; j < 24; ++j) Pn[i * 24 + j] = PnT[j * 24 + i];
   std::memcpy(P, Pn, sizeof Pn);
   return SLIO_OK;
 }
