@@ -7631,6 +7631,21 @@ __global__ void k_undistort(const float* __restrict__ x, const float* __restrict
   oz[i] = cz;
 }
 
+// whether the host's point times are already in k_time_keys' order (the
+// same unsigned keys, non-decreasing): then the stable sort is the identity
+// and is skipped (a driver's scan usually arrives in firing order)
+static bool time_keys_sorted(const float* t, int64_t n) {
+  uint32_t prev = 0, bad = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t b;
+    std::memcpy(&b, t + i, 4);
+    const uint32_t k = (uint32_t)(b >= 0 ? b : b ^ 0x7FFFFFFF) ^ 0x80000000u;
+    bad |= (uint32_t)(k < prev);
+    prev = k;
+  }
+  return bad == 0;
+}
+
 // undistorted scan in time order into device arrays ux, uy, uz, ut (n each)
 static int undistort_device(Ctx& c, const float* x, const float* y, const float* z, const float* t, int64_t n,
                             const slio_imu_pose* poses, int np, const slio_state* xe, float* ux, float* uy, float* uz,
@@ -7676,15 +7691,17 @@ static int undistort_device(Ctx& c, const float* x, const float* y, const float*
     }
     const int nb = grid_blocks(n);
     k_time_keys<<<nb, 256, 0, st>>>(dt_, n, k0, v0);
+    const bool in_order = time_keys_sorted(t, n);  // (while the copies and keys run)
     size_t tb = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
-        (e = MapDev::take(B[3], tb)) ||
-        (e = hipcub::DeviceRadixSort::SortPairs(B[3].p, tb, k0, k1, v0, v1, (int)n, 0, 32, st))) {
+    if (!in_order &&
+        ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
+         (e = MapDev::take(B[3], tb)) ||
+         (e = hipcub::DeviceRadixSort::SortPairs(B[3].p, tb, k0, k1, v0, v1, (int)n, 0, 32, st)))) {
       set_error(std::string("slio undistort: sort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
     }
-    k_undistort<<<nb, 256, 0, st>>>(dx_, dy_, dz_, dt_, v1, n, dp, np, E, ux, uy, uz, ut);
+    k_undistort<<<nb, 256, 0, st>>>(dx_, dy_, dz_, dt_, in_order ? v0 : v1, n, dp, np, E, ux, uy, uz, ut);
     if ((e = hipGetLastError()) || (e = spin_sync(st))) {
       set_error(std::string("slio undistort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;

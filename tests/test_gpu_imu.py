@@ -17,11 +17,18 @@ from test_gpu_parity import L  # noqa: E402,F401
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seed,first_late", [(0, False), (1, True)])
-def test_undistort_vs_oracle(L, oracle_mod, seed, first_late):
+@pytest.mark.parametrize("seed,first_late,presorted", [(0, False, False), (1, True, False), (2, False, True)])
+def test_undistort_vs_oracle(L, oracle_mod, seed, first_late, presorted):
+    """presorted: the points arrive in time order (a driver's firing order),
+    so the device skips its stable time sort (the identity then)."""
     from agi_lidar_slam_amd.esekf import Esekf, StateIkfom
     from agi_lidar_slam_amd.imu import ImuProcess, MeasureGroup
     cs = make_case(seed, first_late)
+    if presorted:
+        order = np.argsort(cs["t"], kind="stable")
+        cs["pts"], cs["t"] = np.ascontiguousarray(cs["pts"][order]), np.ascontiguousarray(cs["t"][order])
+    else:
+        assert (np.diff(cs["t"]) < 0).any()   # the sort path
     ref = oracle_mod.imu_undistort(cs["imu"], cs["beg"], cs["end"], cs["last_end"], cs["mean_acc_norm"],
                                    cs["cov12"], cs["acc_s_last"], cs["angvel_last"], cs["state"], cs["P"],
                                    cs["pts"], cs["t"])
