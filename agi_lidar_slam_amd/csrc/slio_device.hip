@@ -5734,10 +5734,55 @@ struct VgGeom {
 
 // voxel index idx = ijk0 + ijk1 * div0 + ijk2 * div0 * div1, ijk =
 // int(floor(p * inv) - float(min_b)); non-finite points sort last (dropped)
+// PCL's geometry (voxel_grid.hpp applyFilter) from the bounding box keys, on
+// the device (the same float arithmetic the host did after reading the box
+// back): flags[0] = 1 when no point is finite (empty output), flags[1] = 1
+// when the leaf is too small for the cloud (PCL passes the input through).
+// With either flag set the keys below are meaningless and the caller,
+// reading the flags with the voxel count, ignores them.
+__global__ void k_vg_geom(const int32_t* __restrict__ bb, float leaf, VgGeom* __restrict__ G,
+                          uint32_t* __restrict__ flags) {
+  if (threadIdx.x != 0) return;
+  VgGeom g;
+  float mn[3], mx[3];
+  int64_t dd[3];
+  for (int a = 0; a < 3; ++a) {
+    const int32_t lo = bb[a] >= 0 ? bb[a] : bb[a] ^ 0x7FFFFFFF, hi = bb[3 + a] >= 0 ? bb[3 + a] : bb[3 + a] ^ 0x7FFFFFFF;
+    mn[a] = __int_as_float(lo);
+    mx[a] = __int_as_float(hi);
+    g.inv[a] = 1.0f / leaf;
+    const float span = (mx[a] - mn[a]) * g.inv[a];
+    dd[a] = isfinite(span) && span < 9.2e18f ? (int64_t)span + 1 : INT64_MAX / 4;
+  }
+  const bool empty = bb[6] == 0;
+  bool pass = dd[0] > INT32_MAX || dd[1] > INT32_MAX || dd[2] > INT32_MAX;
+  if (!pass) {
+    const int64_t d01 = dd[0] * dd[1];  // (<= 2^62)
+    pass = d01 > INT32_MAX || d01 * dd[2] > (int64_t)INT32_MAX;
+  }
+  pass = pass && !empty;
+  int div[3] = {1, 1, 1};
+  for (int a = 0; a < 3; ++a) {
+    g.minb[a] = 0;
+    if (!empty && !pass) {
+      g.minb[a] = (int)floorf(mn[a] * g.inv[a]);
+      div[a] = (int)floorf(mx[a] * g.inv[a]) - g.minb[a] + 1;
+    }
+  }
+  g.mul[0] = 1;
+  g.mul[1] = div[0];
+  g.mul[2] = div[0] * div[1];
+  *G = g;
+  flags[0] = empty ? 1u : 0u;
+  flags[1] = pass ? 1u : 0u;
+}
+
 __global__ void k_vg_keys(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
-                          int64_t n, VgGeom G, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                          int64_t n, const VgGeom* __restrict__ Gp, uint32_t* __restrict__ keys,
+                          uint32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const VgGeom G = *Gp;
   const float c[3] = {x[i], y[i], z[i]};
   uint32_t key = 0xFFFFFFFFu;
   if (isfinite(c[0]) && isfinite(c[1]) && isfinite(c[2])) {
@@ -7035,7 +7080,7 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
     MapDev::Buf* B = c.pre + 8;
     if ((e = MapDev::take(B[0], 4 * n)) || (e = MapDev::take(B[1], 4 * n)) || (e = MapDev::take(B[2], 4 * n)) ||
         (e = MapDev::take(B[3], 4 * n)) || (e = MapDev::take(B[4], 4 * n)) || (e = MapDev::take(B[5], 4 * n)) ||
-        (e = MapDev::take(B[6], 32))) {
+        (e = MapDev::take(B[6], 32 + sizeof(VgGeom) + 8))) {
       set_error(std::string("slio_scan_upload_voxel: hipMalloc: ") + hipGetErrorString(e));
       rc = SLIO_ENOMEM;
       break;
@@ -7048,44 +7093,20 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
     rk = (uint32_t*)B[5].p;
     bb = (int32_t*)B[6].p;
     const int32_t init[8] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN, 0, 0};
-    int32_t got[8];
     if ((e = hipMemcpyAsync(bb, init, 32, hipMemcpyHostToDevice, st))) {
       set_error(std::string("slio_scan_upload_voxel: H2D: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
     }
+    // the box, the geometry and the voxel keys stay on the device: ONE
+    // readback below (voxel count and the geometry's flags) where the box used
+    // to come back first
+    VgGeom* gdev = reinterpret_cast<VgGeom*>((char*)B[6].p + 32);
+    uint32_t* vflags = reinterpret_cast<uint32_t*>((char*)B[6].p + 32 + sizeof(VgGeom));
     k_vg_bbox<<<std::min(grid_blocks(n), 64), 256, 0, st>>>(dx_, dy_, dz_, n, bb);
-    const Rb rbb{got, bb, 32};
-    if ((e = readback(st, &rbb, 1))) {
-      set_error(std::string("slio_scan_upload_voxel: bbox: ") + hipGetErrorString(e));
-      rc = SLIO_EDEVICE;
-      break;
-    }
-    if (got[6] == 0) break;  // no finite point: empty scan
-    // PCL's geometry (voxel_grid.hpp applyFilter), float arithmetic
-    VgGeom G;
-    float mn[3], mx[3];
-    int64_t dd[3];
-    for (int a = 0; a < 3; ++a) {
-      mn[a] = fkey_inv(got[a]);
-      mx[a] = fkey_inv(got[3 + a]);
-      G.inv[a] = 1.0f / leaf;
-      dd[a] = (int64_t)((mx[a] - mn[a]) * G.inv[a]) + 1;
-    }
-    if (dd[0] * dd[1] * dd[2] > (int64_t)INT32_MAX) {
-      passthrough = true;  // PCL: leaf too small for the cloud, output = input
-      break;
-    }
-    int div[3];
-    for (int a = 0; a < 3; ++a) {
-      G.minb[a] = (int)std::floor(mn[a] * G.inv[a]);
-      div[a] = (int)std::floor(mx[a] * G.inv[a]) - G.minb[a] + 1;
-    }
-    G.mul[0] = 1;
-    G.mul[1] = div[0];
-    G.mul[2] = div[0] * div[1];
+    k_vg_geom<<<1, 64, 0, st>>>(bb, leaf, gdev, vflags);
     const int nb = grid_blocks(n);
-    k_vg_keys<<<nb, 256, 0, st>>>(dx_, dy_, dz_, n, G, k0, v0);
+    k_vg_keys<<<nb, 256, 0, st>>>(dx_, dy_, dz_, n, gdev, k0, v0);
     size_t tb = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)n, 0, 32, st)) ||
         (e = MapDev::take(B[7], tb)) ||
@@ -7095,9 +7116,22 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
       break;
     }
     k_vg_heads<<<nb, 256, 0, st>>>(k1, n, hd);
-    uint32_t total = 0;
-    if ((rc = scan_flags(hd, rk, n, st, &total))) break;
-    m = total;
+    if ((rc = scan_launch(hd, rk, n, st))) break;
+    uint32_t got[4] = {0, 0, 0, 0};
+    {
+      const Rb rb[3] = {{&got[0], rk + n - 1, 4}, {&got[1], hd + n - 1, 4}, {&got[2], vflags, 8}};
+      if ((e = readback(st, rb, 3))) {
+        set_error(std::string("slio_scan_upload_voxel: counts: ") + hipGetErrorString(e));
+        rc = SLIO_EDEVICE;
+        break;
+      }
+    }
+    if (got[2]) break;  // no finite point: empty scan
+    if (got[3]) {
+      passthrough = true;  // PCL: leaf too small for the cloud, output = input
+      break;
+    }
+    m = (int64_t)got[0] + got[1];
     if (m > c.prm.max_points) {
       set_error("slio_scan_upload_voxel: downsampled scan exceeds max_points");
       rc = SLIO_ECAPACITY;
@@ -7124,8 +7158,13 @@ static int voxel_device(Ctx& c, const float* dx_, const float* dy_, const float*
     }
   }
   if (!rc) {
+    // (no synchronisation: every user of the scan buffers runs on this
+    // stream, after the centroids)
     if (m > 0 && c.bx) (void)hipMemsetAsync(c.sel, 0, m, st);
-    (void)spin_sync(st);
+    if (const hipError_t e = hipGetLastError()) {
+      set_error(std::string("slio_scan_upload_voxel: ") + hipGetErrorString(e));
+      return SLIO_EDEVICE;
+    }
     c.n = m;
     c.searched = false;
     if (n_down) *n_down = m;
@@ -7649,7 +7688,7 @@ static bool time_keys_sorted(const float* t, int64_t n) {
 // undistorted scan in time order into device arrays ux, uy, uz, ut (n each)
 static int undistort_device(Ctx& c, const float* x, const float* y, const float* z, const float* t, int64_t n,
                             const slio_imu_pose* poses, int np, const slio_state* xe, float* ux, float* uy, float* uz,
-                            float* ut) {
+                            float* ut, bool sync_end = true) {
   hipStream_t st = c.stream;
   UndistEnd E;
   qmatrix(Quat{xe->rot[0], xe->rot[1], xe->rot[2], xe->rot[3]}, E.R);
@@ -7702,7 +7741,9 @@ static int undistort_device(Ctx& c, const float* x, const float* y, const float*
       break;
     }
     k_undistort<<<nb, 256, 0, st>>>(dx_, dy_, dz_, dt_, in_order ? v0 : v1, n, dp, np, E, ux, uy, uz, ut);
-    if ((e = hipGetLastError()) || (e = spin_sync(st))) {
+    // (the combined entry's VoxelGrid step follows on the stream and reads back
+    // itself: no synchronisation here)
+    if ((e = hipGetLastError()) || (sync_end && (e = spin_sync(st)))) {
       set_error(std::string("slio undistort: ") + hipGetErrorString(e));
       rc = SLIO_EDEVICE;
       break;
@@ -7754,7 +7795,8 @@ int slio_scan_upload_undistort_voxel(slio_handle h, const float* x, const float*
     SLIO_HIP(MapDev::take(c.pre[0], 16 * n));
     u = (float*)c.pre[0].p;
   }
-  int rc = n > 0 ? undistort_device(c, x, y, z, t_ms, n, poses, npose, x_end, u, u + n, u + 2 * n, u + 3 * n)
+  int rc = n > 0 ? undistort_device(c, x, y, z, t_ms, n, poses, npose, x_end, u, u + n, u + 2 * n, u + 3 * n,
+                                    false)
                  : SLIO_OK;
   if (!rc) rc = voxel_device(c, u, u ? u + n : nullptr, u ? u + 2 * n : nullptr, n, leaf, n_down);
   return rc;

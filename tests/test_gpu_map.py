@@ -272,6 +272,21 @@ def test_voxel_grid_vs_oracle(L, oracle_mod, leaf):
         kf.close()
 
 
+def test_voxel_grid_no_finite_point(L):
+    """A scan without a finite point downsamples to nothing (PCL's
+    getMinMax3D finds no point); the device decides it from the box it keeps
+    on the device, with the voxel count, in one readback."""
+    from agi_lidar_slam_amd.esekf import Esekf
+    raw = np.full((5000, 3), np.nan, np.float32)
+    raw[::7, 0] = np.inf
+    kf = Esekf(max_points=raw.shape[0])
+    try:
+        assert kf.downsample_scan(raw, 0.5) == 0
+        assert kf.downsample_scan(np.zeros((1, 3), np.float32), 0.5) == 1   # and the next scan is normal
+    finally:
+        kf.close()
+
+
 def test_voxel_scan_feeds_update(L, oracle_mod):
     """The device-downsampled scan goes straight into the IKF update (no host
     round trip) and gives the same result as uploading the oracle's
