@@ -4757,22 +4757,31 @@ __global__ __launch_bounds__(256) void k_keep_tiles(const uint8_t* __restrict__ 
   if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
   if (blockIdx.x == 0 && threadIdx.x < 2) tcnt[nt + 1 + threadIdx.x] = 0;
 }
-// rank[i] = survivors before i: the tile's base summed by the workgroup from
-// the tile counts before it (L2-resident: no separate scan launch), the last
-// tile also writes the total to tcnt[nt]
-__global__ __launch_bounds__(256) void k_keep_rank(const uint8_t* __restrict__ keep, int64_t n, int64_t nt,
-                                                   uint32_t* __restrict__ tcnt, uint32_t* __restrict__ rank) {
+// in place: tcnt[0..nt) -> exclusive prefix, tcnt[nt] = the total (one
+// workgroup: O(nt); summing the earlier tiles' counts in every rank
+// workgroup instead was O(nt^2) -- 73M loads for a 50M map)
+__global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tcnt, int64_t nt) {
+  const int64_t per = (nt + 255) / 256, a = min((int64_t)threadIdx.x * per, nt), b = min(a + per, nt);
+  uint32_t s = 0;
+  for (int64_t i = a; i < b; ++i) s += tcnt[i];
+  uint32_t tot;
+  uint32_t run = block_excl_256(s, &tot);
+  for (int64_t i = a; i < b; ++i) {
+    const uint32_t v = tcnt[i];
+    tcnt[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) tcnt[nt] = tot;
+}
+// rank[i] = survivors before i: the tile's base plus the exclusive count
+// within the tile
+__global__ __launch_bounds__(256) void k_keep_rank(const uint8_t* __restrict__ keep, int64_t n,
+                                                   const uint32_t* __restrict__ tbase, uint32_t* __restrict__ rank) {
   const int64_t i0 = (int64_t)blockIdx.x * kRankTile + threadIdx.x * 16;
   const uint4 v = load_keep16(keep, i0, n);
-  uint32_t bs = 0;
-  for (int64_t t = threadIdx.x; t < (int64_t)blockIdx.x; t += 256) bs += tcnt[t];
-  uint32_t base;
-  (void)block_excl_256(bs, &base);
   const uint32_t m[4] = {nz_bytes(v.x), nz_bytes(v.y), nz_bytes(v.z), nz_bytes(v.w)};
   const uint32_t c = __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
-  uint32_t tot;
-  uint32_t r = base + block_excl_256(c, &tot);
-  if (blockIdx.x == nt - 1 && threadIdx.x == 0) tcnt[nt] = base + tot;
+  uint32_t r = tbase[blockIdx.x] + block_excl_256(c, nullptr);
   uint32_t o[16];
 #pragma unroll
   for (int b = 0; b < 16; ++b) {
@@ -6367,7 +6376,8 @@ static int merge_rebuild(MapDev& m, hipStream_t st, bool* handled) {
   float4* out = (float4*)m.b_ref[0].p;
   uint32_t* new_start = (uint32_t*)m.b_start2.p;
   k_keep_tiles<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, rtiles, tcnt);
-  k_keep_rank<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, rtiles, tcnt, rank);
+  k_tile_scan<<<1, 256, 0, st>>>(tcnt, rtiles);
+  k_keep_rank<<<(unsigned)rtiles, 256, 0, st>>>(m.keep, n0, tcnt, rank);
   if (n1) {
     // the live additions must lie a cell inside the kept grid
     MergeBox bx;
